@@ -1,0 +1,145 @@
+/*
+ * mmf_hip.h — C-ABI of libmmf_hip.so, the MI355X-native (gfx950) hot path of the reference's
+ * MisinfoForensics.analyze() 5-signal forward.
+ *
+ * The reference has no FFI: its boundary is the Python API of misinfo_forensics.py.  Each entry
+ * point below replaces one reference call site; the Python host side (mmf_amd/hip.py, ctypes)
+ * keeps the reference's method names and return dicts on top of these.
+ *
+ * Conventions
+ *   - Plain C types only; every function returns 0 on success or a negative errno-style code
+ *     (MMF_EINVAL bad argument/shape/missing weight, MMF_ENOMEM allocation, MMF_EIO HIP error).
+ *     Nothing throws across the ABI.  mmf_last_error() gives a thread-local message.
+ *   - All tensor I/O of the forward calls are caller-owned DEVICE pointers (e.g. torch tensors'
+ *     data_ptr()), enqueued asynchronously on the caller's hipStream_t `stream` (NULL = default
+ *     stream).  No implicit device synchronisation.
+ *   - Weights, workspaces and the Truth-Vault are owned by the handle.  A handle is bound to one
+ *     device and is not thread-safe: one handle per (process, device).
+ *   - Layouts: token ids / masks int32 row-major [B, L]; images uint8 [B, 224, 224, 3] (HWC, RGB);
+ *     embeddings / logits / scores fp32 row-major.
+ */
+#ifndef MMF_HIP_H
+#define MMF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMF_OK 0
+#define MMF_EINVAL (-22)
+#define MMF_ENOMEM (-12)
+#define MMF_EIO (-5)
+
+#define MMF_DTYPE_F32 0
+#define MMF_DTYPE_I64 1
+
+typedef struct mmf_handle mmf_handle;
+
+/* Create a handle on HIP device `device` (ordinal within HIP_VISIBLE_DEVICES). */
+int mmf_create(int device, mmf_handle** out);
+void mmf_destroy(mmf_handle* h);
+/* Thread-local description of the last error (empty string if none). */
+const char* mmf_last_error(void);
+/* Library/ABI version string. */
+const char* mmf_version(void);
+
+/* Stage one host tensor under its state-dict name.  Names are the reference's state-dict keys:
+ * detector keys as in MultiModalMisinfoDetector (misinfo_forensics.py:43-108 — "roberta.*",
+ * "ai_head.*", "misinfo_head.*", "efficientnet.*", "fusion_layer.*") and CLIP keys as in HF
+ * CLIPModel prefixed with "clip." (misinfo_forensics.py:210-212).  Replaces the reference's
+ * load_state_dict (misinfo_forensics.py:175-186, 260-317); the data are copied. */
+int mmf_load_tensor(mmf_handle* h, const char* name, int dtype, int ndim, const int64_t* shape,
+                    const void* host_data);
+/* Pack staged tensors into device layouts (fused QKV, BatchNorm folded into convs, bf16 GEMM
+ * operands).  Components whose tensors are all present become available; `clip_eos_token_id`
+ * selects the HF EOS-pooling rule (2 = argmax(ids), else first index of that id;
+ * TF clip:561-582). */
+int mmf_finalize(mmf_handle* h, int clip_eos_token_id);
+/* Bit mask of ready components: 1 text(RoBERTa+heads) 2 effnet 4 clip-vision 8 clip-text
+ * 16 fusion 32 vault. */
+int mmf_ready(mmf_handle* h);
+
+/* Allocate activation workspaces for up to `max_batch` rows with RoBERTa length `max_text_len`
+ * (<= 512) and CLIP text length `max_clip_len` (<= 77).  Forward calls with larger shapes fail
+ * with MMF_EINVAL; call before graph capture. */
+int mmf_reserve(mmf_handle* h, int max_batch, int max_text_len, int max_clip_len);
+
+/* Signals 1-2 — analyze_text (misinfo_forensics.py:319-352): RoBERTa + dual heads.
+ * ids/mask int32 [B, L] device.  Outputs fp32 [B, 2] logits each (may be NULL) and
+ * scores fp32 [B, 2] = softmax(.)[:,1] of (ai, misinfo) (may be NULL). */
+int mmf_text_forward(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L,
+                     float* ai_logits, float* misinfo_logits, float* scores2, void* stream);
+
+/* Signal 3 — analyze_image (misinfo_forensics.py:354-373, 249-253): ImageNet normalisation +
+ * EfficientNet-B0.  img uint8 [B, 224, 224, 3] device.  logits fp32 [B, 2] (may be NULL),
+ * deepfake_score fp32 [B] (may be NULL). */
+int mmf_effnet_forward(mmf_handle* h, const uint8_t* img, int B, float* logits, float* deepfake_score,
+                       void* stream);
+
+/* CLIP image embedding — get_image_features + L2 normalisation (misinfo_forensics.py:395-401,
+ * 432-439).  img uint8 [B, 224, 224, 3] (CLIP-preprocessed geometry); emb fp32 [B, 512] unit. */
+int mmf_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb_unit, void* stream);
+
+/* CLIP text embedding — get_text_features + L2 normalisation (misinfo_forensics.py:395-401,
+ * 473-481).  ids/mask int32 [B, L<=77]; emb fp32 [B, 512] unit. */
+int mmf_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* emb_unit,
+                  void* stream);
+
+/* Truth-Vault (misinfo_forensics.py:214-246, 443-445): host fp32 [N, D=512] raw embeddings; rows
+ * are L2-normalised once here instead of on every search call. */
+int mmf_set_vault(mmf_handle* h, const float* host_vault, int N, int D);
+/* Pre-compute the CLIP text embeddings of the vault titles (used for text_similarity,
+ * misinfo_forensics.py:467-484) from device ids/mask int32 [N, L<=77].  Synchronous. */
+int mmf_set_vault_titles(mmf_handle* h, const int32_t* ids, const int32_t* mask, int N, int L, void* stream);
+
+/* search_vault core (misinfo_forensics.py:443-464, 467-484): q fp32 [B, 512] unit image
+ * embeddings; top-k (k <= 8) similarities fp32 [B, k] and indices int32 [B, k] (descending);
+ * discrepancy fp32 [B] = top1 > thresh ? top1 : 0; optional text_emb fp32 [B, 512] unit caption
+ * embeddings -> text_sim fp32 [B] = cos(caption, title[top1]) where top1 > thresh, else 0. */
+int mmf_vault_topk(mmf_handle* h, const float* q_unit, int B, int k, float thresh, float* sims, int32_t* idx,
+                   float* discrepancy, const float* text_emb, float* text_sim, void* stream);
+
+/* fusion_verdict (misinfo_forensics.py:575-615): scores5 fp32 [B, 5] -> probs fp32 [B, 2]
+ * (real, fake); verdict int32 [B] (fake > 0.5); confidence fp32 [B]; explanation rule index
+ * int32 [B] of _generate_fallback_explanation (misinfo_forensics.py:742-765; 0 vault, 1 deepfake,
+ * 2 ai, 3 misinfo, 4 clip, 5 default).  Any output except probs may be NULL. */
+int mmf_fusion(mmf_handle* h, const float* scores5, int B, float* probs2, int32_t* verdict, float* confidence,
+               int32_t* rule, void* stream);
+
+/* The whole text+image analyze() path for B pairs (misinfo_forensics.py:767-927) with the ViT
+ * computed once per pair.  Inputs device: RoBERTa ids/mask [B, Lr], CLIP ids/mask [B, Lc],
+ * img_effnet uint8 [B,224,224,3], img_clip uint8 [B,224,224,3] (may equal img_effnet).
+ * Outputs device (all fp32 unless noted): scores5 [B,5] (ai, misinfo, deepfake, clip_similarity,
+ * vault_discrepancy), text_sim [B], probs2 [B,2], verdict int32 [B], confidence [B], rule int32 [B],
+ * top_sims [B,5], top_idx int32 [B,5].  Vault outputs are zero when no vault is set. */
+int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_mask, int Lr,
+                      const int32_t* clip_ids, const int32_t* clip_mask, int Lc, const uint8_t* img_effnet,
+                      const uint8_t* img_clip, int B, float* scores5, float* text_sim, float* probs2,
+                      int32_t* verdict, float* confidence, int32_t* rule, float* top_sims, int32_t* top_idx,
+                      void* stream);
+
+/* Per-kernel timing for roofline accounting: while profiling is on, every kernel launch of the
+ * forward calls is bracketed by two hipEvents on its stream.  mmf_profile_end synchronises and
+ * aggregates per kernel kind (arrays of >= 16 entries): launch counts, summed device ms, summed
+ * ALGORITHMIC flops and HBM bytes; returns the number of kinds.  Names via mmf_profile_kind_name. */
+int mmf_profile_begin(mmf_handle* h);
+int mmf_profile_end(mmf_handle* h, int max_kinds, int* counts, double* ms, double* flops, double* bytes);
+const char* mmf_profile_kind_name(int kind);
+
+/* Low-level op exported for unit tests of the GEMM kernel: C = act(A @ W^T + bias) + residual.
+ * A bf16 [M,K] (lda), W bf16 [N,K] (ldw), bias fp32 [N] or NULL, residual fp32 [M,N] (ldc) or NULL,
+ * act 0 none 1 gelu-erf 2 quick_gelu 3 silu 4 relu; outputs fp32 (c32) and/or bf16 (c16) [M,N] ldc. */
+int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual,
+                  float* c32, void* c16, int ldc, int M, int N, int K, int act, void* stream);
+
+/* Low-level attention op for tests: qkv bf16 [B*L, 3*H*64] (q|k|v), mask int32 [B,L] or NULL,
+ * causal 0/1 -> out bf16 [B*L, H*64]. */
+int mmf_attention_bf16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMF_HIP_H */

@@ -1,0 +1,164 @@
+// Fused multi-head attention for the three encoders (head_dim 64, sequence <= 128):
+//   RoBERTa  L=128, 12 heads, key-padding mask          (TF roberta:158-251)
+//   CLIP ViT L=50,  12 heads, no mask                    (TF clip:280-333)
+//   CLIP txt L=77,   8 heads, causal + key-padding mask  (TF clip:494-590)
+// One workgroup (4 waves) per (sequence, head).  K (row-major, XOR-swizzled) and V (transposed
+// [d][key]) of the whole head live in LDS; each wave takes 16-query tiles:
+//   S = Q K^T   (v_mfma_f32_16x16x32_bf16, Q fragments straight from global/L2)
+//   fp32 masked softmax in registers (rows spread over 16 lanes -> 4 xor-shuffles)
+//   O^T = V^T P^T so each lane ends with 4 consecutive head dims of one query (8-B stores).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int LMAX = 128;
+constexpr int VT_LD = LMAX + 8;   // padded row of the transposed V / P tiles (272 B)
+
+__global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict__ qkv, int ld,
+                                                        const int32_t* __restrict__ mask, bf16_t* __restrict__ out,
+                                                        int ldo, int L, int H, int causal) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[LMAX * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[64 * VT_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ps[4][16 * VT_LD];
+  __shared__ float kbias[LMAX];
+
+  const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
+  const int D = H * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Lk = (L + 31) & ~31;  // keys padded to the 32-deep PV k-step
+  const bf16_t* base = qkv + (size_t)bi * L * ld;
+
+  // stage K (swizzled rows) and V^T; zero the padded keys so 0 * pad stays finite
+  for (int c = tid; c < Lk * 8; c += 256) {
+    const int key = c >> 3, kc = c & 7;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (key < L) {
+      kv = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + D + h * 64 + kc * 8);
+      vv = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + 2 * D + h * 64 + kc * 8);
+    }
+    *reinterpret_cast<uint4*>(Ks + key * 64 + ((kc ^ (key & 7)) << 3)) = kv;
+    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      Vt[(kc * 8 + 2 * j) * VT_LD + key] = (bf16_t)(w[j] & 0xffff);
+      Vt[(kc * 8 + 2 * j + 1) * VT_LD + key] = (bf16_t)(w[j] >> 16);
+    }
+  }
+  for (int k = tid; k < Lk; k += 256)
+    kbias[k] = (k < L && (!mask || mask[(size_t)bi * L + k])) ? 0.f : -INFINITY;
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nqt = (L + 15) >> 4, nkt = Lk >> 4;
+  bf16_t* P = Ps[wave];
+
+  for (int qt = wave; qt < nqt; qt += 4) {
+    // Q fragments: row q = qt*16 + fr, dims 32*ks + 8*fg .. +7
+    bf16x8 qf[2];
+    {
+      const int q = qt * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (q < L) v = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + h * 64 + ks * 32 + fg * 8);
+        qf[ks] = as_bf16x8(v);
+      }
+    }
+    // S[q][key]: lane holds rows q = qt*16 + fg*4 + r, key = j*16 + fr
+    f32x4 s[LMAX / 16];
+#pragma unroll
+    for (int j = 0; j < LMAX / 16; ++j) {
+      s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (j < nkt) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int key = j * 16 + fr, kc = ks * 4 + fg;
+          const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + key * 64 + ((kc ^ (key & 7)) << 3)));
+          s[j] = mfma16x16x32(qf[ks], kf, s[j]);
+        }
+      }
+    }
+    // masked softmax (fp32), scale 1/sqrt(64)
+    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int j = 0; j < LMAX / 16; ++j) {
+      if (j < nkt) {
+        const int key = j * 16 + fr;
+        const float kb = kbias[key];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = qt * 16 + fg * 4 + r;
+          float v = s[j][r] * 0.125f + kb;
+          if (causal && key > q) v = -INFINITY;
+          s[j][r] = v;
+          mx[r] = fmaxf(mx[r], v);
+        }
+      }
+    }
+    float sum[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
+      sum[r] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < LMAX / 16; ++j) {
+      if (j < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = (mx[r] == -INFINITY) ? 0.f : __expf(s[j][r] - mx[r]);
+          s[j][r] = e;
+          sum[r] += e;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
+      sum[r] = sum[r] > 0.f ? 1.0f / sum[r] : 0.f;
+    }
+    // P (bf16, normalised) -> this wave's LDS tile [q][key]
+#pragma unroll
+    for (int j = 0; j < LMAX / 16; ++j) {
+      if (j < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[(fg * 4 + r) * VT_LD + j * 16 + fr] = f2bf(s[j][r] * sum[r]);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed
+    __builtin_amdgcn_wave_barrier();
+    // O^T[d][q] = sum_key V^T[d][key] P^T[key][q]; lane: d = dt*16 + fg*4 + r, q = qt*16 + fr
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < Lk; kk += 32) {
+      const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(P + fr * VT_LD + kk + fg * 8));
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 vf = as_bf16x8(*reinterpret_cast<const uint4*>(Vt + (dt * 16 + fr) * VT_LD + kk + fg * 8));
+        o[dt] = mfma16x16x32(vf, pf, o[dt]);
+      }
+    }
+    const int q = qt * 16 + fr;
+    if (q < L) {
+      bf16_t* dst = out + ((size_t)bi * L + q) * ldo + h * 64 + fg * 4;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *reinterpret_cast<uint2*>(dst + dt * 16) =
+            make_uint2(pack2bf(o[dt][0], o[dt][1]), pack2bf(o[dt][2], o[dt][3]));
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+}  // namespace
+
+hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, bf16_t* out, int ldo, int B, int L,
+                            int H, int causal, hipStream_t s) {
+  if (L <= 0 || L > LMAX || (ldqkv & 7) || (ldo & 3)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(attention_kernel, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal);
+  return hipGetLastError();
+}

@@ -1,0 +1,974 @@
+// C-ABI of libmmf_hip.so (include/mmf_hip.h): handle, weight packing, workspaces and the launch
+// sequences of the five signals.  Host C++ over the HIP runtime; no torch types cross this ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mmf_hip.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) return fail(MMF_EIO, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+#define CHK(expr)            \
+  do {                       \
+    int r_ = (expr);         \
+    if (r_ != 0) return r_;  \
+  } while (0)
+
+uint16_t f2bf_host(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct HostT {
+  std::vector<int64_t> shape;
+  std::vector<float> f;
+  size_t numel() const { return f.size(); }
+};
+
+struct Lin16 { bf16_t* w = nullptr; float* b = nullptr; int out = 0, in = 0; };
+struct LNp { float* g = nullptr; float* b = nullptr; };
+struct EncLayer { Lin16 qkv, o, fc1, fc2; LNp ln1, ln2; };
+
+struct EffBlock {
+  int expand, k, stride, cin, cout, cexp, csq, residual;
+  Lin16 e, p;            // expand / project 1x1 convs (BN folded)
+  float* wd = nullptr;   // depthwise [cexp][k*k] (BN folded)
+  float* bd = nullptr;
+  float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;  // SE
+};
+
+const int kStages[7][6] = {{1, 3, 1, 32, 16, 1},  {6, 3, 2, 16, 24, 2},   {6, 5, 2, 24, 40, 2},  {6, 3, 2, 40, 80, 3},
+                           {6, 5, 1, 80, 112, 3}, {6, 5, 2, 112, 192, 4}, {6, 3, 1, 192, 320, 1}};
+
+struct Workspace {
+  // RoBERTa
+  float *r_x = nullptr, *r_y = nullptr;
+  bf16_t *r_xb = nullptr, *r_qkv = nullptr, *r_ctx = nullptr, *r_h = nullptr;
+  // CLIP vision
+  bf16_t *v_col = nullptr, *v_xb = nullptr, *v_qkv = nullptr, *v_ctx = nullptr, *v_h = nullptr, *v_cls = nullptr;
+  float *v_patch = nullptr, *v_x = nullptr, *v_emb = nullptr;
+  // CLIP text
+  bf16_t *t_xb = nullptr, *t_qkv = nullptr, *t_ctx = nullptr, *t_h = nullptr, *t_pool = nullptr;
+  float *t_x = nullptr, *t_emb = nullptr;
+  int32_t* t_eos = nullptr;
+  // EfficientNet
+  bf16_t *e_a = nullptr, *e_b = nullptr, *e_exp = nullptr, *e_dw = nullptr;
+  float *e_pool = nullptr, *e_scale = nullptr;
+  // vault
+  float* s_sims = nullptr;
+  int s_cap_n = 0;
+};
+
+}  // namespace
+
+struct mmf_handle {
+  int device = 0;
+  int eos_id = 49407;
+  std::map<std::string, HostT> staged;
+  std::vector<void*> allocs;
+  int ready = 0;
+  // RoBERTa + heads
+  float *r_word = nullptr, *r_pos = nullptr, *r_type0 = nullptr;
+  LNp r_embln;
+  EncLayer r_layers[12];
+  float *h_w1a = nullptr, *h_b1a = nullptr, *h_w2a = nullptr, *h_b2a = nullptr;
+  float *h_w1m = nullptr, *h_b1m = nullptr, *h_w2m = nullptr, *h_b2m = nullptr;
+  // EfficientNet
+  float *e_stem_w = nullptr, *e_stem_b = nullptr;
+  std::vector<EffBlock> e_blocks;
+  Lin16 e_head;
+  float *e_cls_w = nullptr, *e_cls_b = nullptr;
+  // CLIP vision
+  bf16_t* v_patch_w = nullptr;
+  float *v_cls = nullptr, *v_pos = nullptr;
+  LNp v_pre, v_post;
+  EncLayer v_layers[12];
+  bf16_t* v_proj = nullptr;
+  // CLIP text
+  float *t_tok = nullptr, *t_pos = nullptr;
+  EncLayer t_layers[12];
+  LNp t_final;
+  bf16_t* t_proj = nullptr;
+  // fusion
+  float *f_w0 = nullptr, *f_b0 = nullptr, *f_w3 = nullptr, *f_b3 = nullptr, *f_w5 = nullptr, *f_b5 = nullptr;
+  // vault
+  float* vault = nullptr;        // [N][512] unit rows
+  float* vault_title = nullptr;  // [N][512] unit title text embeddings (or null)
+  int vault_n = 0;
+  // workspace capacity
+  Workspace ws;
+  int cap_b = 0, cap_lr = 0, cap_lc = 0;
+  std::vector<void*> ws_allocs;
+  // per-kernel event timing (mmf_profile_begin/end)
+  struct ProfRec { int ev; int kind; double flops, bytes; };
+  bool prof = false;
+  std::vector<ProfRec> prof_recs;
+  std::vector<hipEvent_t> ev_pool;
+  int ev_used = 0;
+
+  ~mmf_handle() {
+    for (void* p : allocs) (void)hipFree(p);
+    for (void* p : ws_allocs) (void)hipFree(p);
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+  }
+};
+
+namespace {
+
+int dev_alloc(mmf_handle* h, void** p, size_t bytes, bool workspace = false) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return fail(MMF_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  (workspace ? h->ws_allocs : h->allocs).push_back(*p);
+  return 0;
+}
+
+// ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
+enum ProfKind {
+  PK_GEMM0 = 0, PK_GEMM1, PK_GEMM2, PK_GEMM3, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
+  PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
+};
+const char* prof_kind_name(int k) {
+  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, "attention", "layernorm",
+                                        "embed+ln", "clip_im2col", "effnet_stem", "dwconv", "se", "gap_classifier",
+                                        "text_heads", "vault", "fusion"};
+  if (k >= 0 && k < 4) return gemm_config_name(k);
+  return (k >= 0 && k < PK_COUNT) ? names[k] : "?";
+}
+
+struct ProfScope {
+  mmf_handle* h;
+  hipStream_t s;
+  int ev = -1;
+  ProfScope(mmf_handle* h_, hipStream_t s_, int kind, double flops, double bytes) : h(h_), s(s_) {
+    if (!h->prof) return;
+    while ((int)h->ev_pool.size() < h->ev_used + 2) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      h->ev_pool.push_back(e);
+    }
+    ev = h->ev_used;
+    h->ev_used += 2;
+    (void)hipEventRecord(h->ev_pool[ev], s);
+    h->prof_recs.push_back({ev, kind, flops, bytes});
+  }
+  ~ProfScope() {
+    if (ev >= 0) (void)hipEventRecord(h->ev_pool[ev + 1], s);
+  }
+};
+
+template <typename T>
+int upload(mmf_handle* h, T** dst, const std::vector<T>& v) {
+  void* p;
+  CHK(dev_alloc(h, &p, v.size() * sizeof(T)));
+  HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  *dst = (T*)p;
+  return 0;
+}
+
+int up_f32(mmf_handle* h, float** dst, const std::vector<float>& v) { return upload(h, dst, v); }
+int up_bf16(mmf_handle* h, bf16_t** dst, const std::vector<float>& v) {
+  std::vector<uint16_t> b(v.size());
+  for (size_t i = 0; i < v.size(); ++i) b[i] = f2bf_host(v[i]);
+  return upload(h, dst, b);
+}
+
+const HostT* get(mmf_handle* h, const std::string& name, size_t numel) {
+  auto it = h->staged.find(name);
+  if (it == h->staged.end()) {
+    fail(MMF_EINVAL, "missing weight '%s'", name.c_str());
+    return nullptr;
+  }
+  if (numel && it->second.numel() != numel) {
+    fail(MMF_EINVAL, "weight '%s' has %zu elements, expected %zu", name.c_str(), it->second.numel(), numel);
+    return nullptr;
+  }
+  return &it->second;
+}
+bool has(mmf_handle* h, const std::string& name) { return h->staged.count(name) != 0; }
+
+#define GET(var, name, n)                       \
+  const HostT* var = get(h, (name), (n));       \
+  if (!var) return MMF_EINVAL;
+
+int load_f32(mmf_handle* h, float** dst, const std::string& name, size_t n) {
+  GET(t, name, n);
+  return up_f32(h, dst, t->f);
+}
+int load_ln(mmf_handle* h, LNp* ln, const std::string& p, int n) {
+  CHK(load_f32(h, &ln->g, p + ".weight", n));
+  return load_f32(h, &ln->b, p + ".bias", n);
+}
+int load_lin(mmf_handle* h, Lin16* l, const std::string& p, int out, int in, bool bias) {
+  GET(w, p + ".weight", (size_t)out * in);
+  CHK(up_bf16(h, &l->w, w->f));
+  if (bias) CHK(load_f32(h, &l->b, p + ".bias", out));
+  l->out = out;
+  l->in = in;
+  return 0;
+}
+// fused QKV: rows [q; k; v] of [3*H][H] + bias
+int load_qkv(mmf_handle* h, Lin16* l, const std::string& q, const std::string& k, const std::string& v, int H) {
+  std::vector<float> w((size_t)3 * H * H), b((size_t)3 * H);
+  const std::string names[3] = {q, k, v};
+  for (int i = 0; i < 3; ++i) {
+    GET(tw, names[i] + ".weight", (size_t)H * H);
+    GET(tb, names[i] + ".bias", (size_t)H);
+    std::memcpy(w.data() + (size_t)i * H * H, tw->f.data(), sizeof(float) * H * H);
+    std::memcpy(b.data() + (size_t)i * H, tb->f.data(), sizeof(float) * H);
+  }
+  CHK(up_bf16(h, &l->w, w));
+  CHK(up_f32(h, &l->b, b));
+  l->out = 3 * H;
+  l->in = H;
+  return 0;
+}
+
+// BatchNorm (eval) folded into the preceding conv: w' = w * g/sqrt(v+eps), b' = beta - m*g/sqrt(v+eps)
+int fold_bn(mmf_handle* h, const std::string& conv, const std::string& bn, int cout, size_t per_out,
+            std::vector<float>* w, std::vector<float>* b) {
+  GET(cw, conv + ".weight", (size_t)cout * per_out);
+  GET(g, bn + ".weight", cout);
+  GET(be, bn + ".bias", cout);
+  GET(m, bn + ".running_mean", cout);
+  GET(v, bn + ".running_var", cout);
+  w->resize((size_t)cout * per_out);
+  b->resize(cout);
+  for (int o = 0; o < cout; ++o) {
+    const double s = (double)g->f[o] / std::sqrt((double)v->f[o] + 1e-5);
+    for (size_t i = 0; i < per_out; ++i) (*w)[(size_t)o * per_out + i] = (float)(cw->f[(size_t)o * per_out + i] * s);
+    (*b)[o] = (float)((double)be->f[o] - (double)m->f[o] * s);
+  }
+  return 0;
+}
+
+std::vector<float> transpose(const std::vector<float>& a, int rows, int cols) {
+  std::vector<float> t((size_t)rows * cols);
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c) t[(size_t)c * rows + r] = a[(size_t)r * cols + c];
+  return t;
+}
+
+int finalize_text(mmf_handle* h) {
+  const std::string p = "roberta.";
+  CHK(load_f32(h, &h->r_word, p + "embeddings.word_embeddings.weight", (size_t)50265 * 768));
+  CHK(load_f32(h, &h->r_pos, p + "embeddings.position_embeddings.weight", (size_t)514 * 768));
+  {
+    GET(t, p + "embeddings.token_type_embeddings.weight", 0);
+    std::vector<float> t0(t->f.begin(), t->f.begin() + 768);
+    CHK(up_f32(h, &h->r_type0, t0));
+  }
+  CHK(load_ln(h, &h->r_embln, p + "embeddings.LayerNorm", 768));
+  for (int i = 0; i < 12; ++i) {
+    const std::string l = p + "encoder.layer." + std::to_string(i) + ".";
+    EncLayer& L = h->r_layers[i];
+    CHK(load_qkv(h, &L.qkv, l + "attention.self.query", l + "attention.self.key", l + "attention.self.value", 768));
+    CHK(load_lin(h, &L.o, l + "attention.output.dense", 768, 768, true));
+    CHK(load_ln(h, &L.ln1, l + "attention.output.LayerNorm", 768));
+    CHK(load_lin(h, &L.fc1, l + "intermediate.dense", 3072, 768, true));
+    CHK(load_lin(h, &L.fc2, l + "output.dense", 768, 3072, true));
+    CHK(load_ln(h, &L.ln2, l + "output.LayerNorm", 768));
+  }
+  for (int hd = 0; hd < 2; ++hd) {
+    const std::string n = hd ? "misinfo_head" : "ai_head";
+    GET(w1, n + ".0.weight", (size_t)256 * 768);
+    float** w1d = hd ? &h->h_w1m : &h->h_w1a;
+    CHK(up_f32(h, w1d, transpose(w1->f, 256, 768)));
+    CHK(load_f32(h, hd ? &h->h_b1m : &h->h_b1a, n + ".0.bias", 256));
+    CHK(load_f32(h, hd ? &h->h_w2m : &h->h_w2a, n + ".3.weight", 512));
+    CHK(load_f32(h, hd ? &h->h_b2m : &h->h_b2a, n + ".3.bias", 2));
+  }
+  return 0;
+}
+
+int finalize_effnet(mmf_handle* h) {
+  const std::string p = "efficientnet.features.";
+  std::vector<float> w, b;
+  CHK(fold_bn(h, p + "0.0", p + "0.1", 32, 27, &w, &b));
+  CHK(up_f32(h, &h->e_stem_w, w));
+  CHK(up_f32(h, &h->e_stem_b, b));
+  h->e_blocks.clear();
+  for (int si = 0; si < 7; ++si) {
+    const int* st = kStages[si];
+    for (int j = 0; j < st[5]; ++j) {
+      EffBlock B{};
+      B.expand = st[0];
+      B.k = st[1];
+      B.stride = j == 0 ? st[2] : 1;
+      B.cin = j == 0 ? st[3] : st[4];
+      B.cout = st[4];
+      B.cexp = B.cin * B.expand;
+      B.csq = B.cin / 4 > 1 ? B.cin / 4 : 1;
+      B.residual = (B.stride == 1 && B.cin == B.cout);
+      const std::string bp = p + std::to_string(si + 1) + "." + std::to_string(j) + ".block.";
+      int i = 0;
+      if (B.expand != 1) {
+        CHK(fold_bn(h, bp + "0.0", bp + "0.1", B.cexp, B.cin, &w, &b));
+        CHK(up_bf16(h, &B.e.w, w));
+        CHK(up_f32(h, &B.e.b, b));
+        B.e.out = B.cexp;
+        B.e.in = B.cin;
+        i = 1;
+      }
+      CHK(fold_bn(h, bp + std::to_string(i) + ".0", bp + std::to_string(i) + ".1", B.cexp, (size_t)B.k * B.k, &w, &b));
+      CHK(up_f32(h, &B.wd, w));
+      CHK(up_f32(h, &B.bd, b));
+      const std::string se = bp + std::to_string(i + 1) + ".";
+      CHK(load_f32(h, &B.w1, se + "fc1.weight", (size_t)B.csq * B.cexp));
+      CHK(load_f32(h, &B.b1, se + "fc1.bias", B.csq));
+      CHK(load_f32(h, &B.w2, se + "fc2.weight", (size_t)B.cexp * B.csq));
+      CHK(load_f32(h, &B.b2, se + "fc2.bias", B.cexp));
+      CHK(fold_bn(h, bp + std::to_string(i + 2) + ".0", bp + std::to_string(i + 2) + ".1", B.cout, B.cexp, &w, &b));
+      CHK(up_bf16(h, &B.p.w, w));
+      CHK(up_f32(h, &B.p.b, b));
+      B.p.out = B.cout;
+      B.p.in = B.cexp;
+      h->e_blocks.push_back(B);
+    }
+  }
+  CHK(fold_bn(h, p + "8.0", p + "8.1", 1280, 320, &w, &b));
+  CHK(up_bf16(h, &h->e_head.w, w));
+  CHK(up_f32(h, &h->e_head.b, b));
+  h->e_head.out = 1280;
+  h->e_head.in = 320;
+  CHK(load_f32(h, &h->e_cls_w, "efficientnet.classifier.1.weight", 2 * 1280));
+  CHK(load_f32(h, &h->e_cls_b, "efficientnet.classifier.1.bias", 2));
+  return 0;
+}
+
+int finalize_clip_layers(mmf_handle* h, EncLayer* layers, const std::string& base, int H, int I) {
+  for (int i = 0; i < 12; ++i) {
+    const std::string l = base + std::to_string(i) + ".";
+    EncLayer& L = layers[i];
+    CHK(load_qkv(h, &L.qkv, l + "self_attn.q_proj", l + "self_attn.k_proj", l + "self_attn.v_proj", H));
+    CHK(load_lin(h, &L.o, l + "self_attn.out_proj", H, H, true));
+    CHK(load_ln(h, &L.ln1, l + "layer_norm1", H));
+    CHK(load_lin(h, &L.fc1, l + "mlp.fc1", I, H, true));
+    CHK(load_lin(h, &L.fc2, l + "mlp.fc2", H, I, true));
+    CHK(load_ln(h, &L.ln2, l + "layer_norm2", H));
+  }
+  return 0;
+}
+
+int finalize_clip_vision(mmf_handle* h) {
+  const std::string p = "clip.vision_model.";
+  {
+    GET(w, p + "embeddings.patch_embedding.weight", (size_t)768 * 3072);
+    CHK(up_bf16(h, &h->v_patch_w, w->f));  // [768][3*32*32] = (c, ky, kx) columns
+  }
+  CHK(load_f32(h, &h->v_cls, p + "embeddings.class_embedding", 768));
+  CHK(load_f32(h, &h->v_pos, p + "embeddings.position_embedding.weight", 50 * 768));
+  CHK(load_ln(h, &h->v_pre, p + "pre_layrnorm", 768));
+  CHK(finalize_clip_layers(h, h->v_layers, p + "encoder.layers.", 768, 3072));
+  CHK(load_ln(h, &h->v_post, p + "post_layernorm", 768));
+  GET(pw, "clip.visual_projection.weight", (size_t)512 * 768);
+  return up_bf16(h, &h->v_proj, pw->f);
+}
+
+int finalize_clip_text(mmf_handle* h) {
+  const std::string p = "clip.text_model.";
+  CHK(load_f32(h, &h->t_tok, p + "embeddings.token_embedding.weight", (size_t)49408 * 512));
+  CHK(load_f32(h, &h->t_pos, p + "embeddings.position_embedding.weight", 77 * 512));
+  CHK(finalize_clip_layers(h, h->t_layers, p + "encoder.layers.", 512, 2048));
+  CHK(load_ln(h, &h->t_final, p + "final_layer_norm", 512));
+  GET(pw, "clip.text_projection.weight", (size_t)512 * 512);
+  return up_bf16(h, &h->t_proj, pw->f);
+}
+
+int finalize_fusion(mmf_handle* h) {
+  CHK(load_f32(h, &h->f_w0, "fusion_layer.0.weight", 64 * 5));
+  CHK(load_f32(h, &h->f_b0, "fusion_layer.0.bias", 64));
+  CHK(load_f32(h, &h->f_w3, "fusion_layer.3.weight", 32 * 64));
+  CHK(load_f32(h, &h->f_b3, "fusion_layer.3.bias", 32));
+  CHK(load_f32(h, &h->f_w5, "fusion_layer.5.weight", 2 * 32));
+  return load_f32(h, &h->f_b5, "fusion_layer.5.bias", 2);
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward sequences
+// ---------------------------------------------------------------------------------------------
+GemmArgs gemm_args(const bf16_t* A, int lda, const Lin16& l, int M) {
+  GemmArgs g{};
+  g.A = A;
+  g.lda = lda;
+  g.W = l.w;
+  g.ldw = l.in;
+  g.bias = l.b;
+  g.M = M;
+  g.N = l.out;
+  g.K = l.in;
+  g.ldc = l.out;
+  g.ldr = l.out;
+  return g;
+}
+
+int gemm(mmf_handle* h, const GemmArgs& g, hipStream_t s) {
+  const double M = g.M, N = g.N, K = g.K;
+  const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
+  ProfScope ps(h, s, gemm_config(g), 2.0 * M * N * K, 2.0 * (M * K + N * K) + M * N * out_b);
+  HIPCHK(launch_gemm(g, s));
+  return 0;
+}
+
+int attn(mmf_handle* h, const bf16_t* qkv, int ld, const int32_t* mask, bf16_t* out, int ldo, int B, int L, int H,
+         int causal, hipStream_t s) {
+  ProfScope ps(h, s, PK_ATTN, 4.0 * B * H * (double)L * L * 64, (double)B * L * H * 64 * 2 * 4);
+  HIPCHK(launch_attention(qkv, ld, mask, out, ldo, B, L, H, causal, s));
+  return 0;
+}
+
+int lnorm(mmf_handle* h, const float* x, int ldx, const LNp& p, float* y32, int ldy32, bf16_t* y16, int ldy16,
+          int rows, int C, hipStream_t s) {
+  ProfScope ps(h, s, PK_LN, 8.0 * rows * C, (double)rows * C * (4 + (y32 ? 4 : 0) + (y16 ? 2 : 0)));
+  HIPCHK(launch_layernorm(x, ldx, nullptr, 0, p.g, p.b, 1e-5f, y32, ldy32, y16, ldy16, rows, C, s));
+  return 0;
+}
+
+int check_cap(mmf_handle* h, int B, int Lr, int Lc) {
+  if (B <= 0) return fail(MMF_EINVAL, "batch must be > 0 (got %d)", B);
+  if (B > h->cap_b || Lr > h->cap_lr || Lc > h->cap_lc)
+    return fail(MMF_EINVAL, "shape B=%d Lr=%d Lc=%d exceeds reserved B=%d Lr=%d Lc=%d (call mmf_reserve)", B, Lr, Lc,
+                h->cap_b, h->cap_lr, h->cap_lc);
+  return 0;
+}
+
+int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
+             float* scores, int score_stride, hipStream_t s) {
+  Workspace& w = h->ws;
+  const int M = B * L;
+  {
+    ProfScope ps(h, s, PK_EMBED, 10.0 * M * 768, (double)M * 768 * (4 + 4 + 4 + 2));
+    HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, w.r_x,
+                                w.r_xb, B, L, 768, 1, s));
+  }
+  for (int i = 0; i < 12; ++i) {
+    const EncLayer& Ly = h->r_layers[i];
+    GemmArgs g = gemm_args(w.r_xb, 768, Ly.qkv, M);
+    g.c16 = w.r_qkv;
+    CHK(gemm(h, g, s));
+    CHK(attn(h, w.r_qkv, 2304, mask, w.r_ctx, 768, B, L, 12, 0, s));
+    g = gemm_args(w.r_ctx, 768, Ly.o, M);
+    g.res32 = w.r_x;
+    g.c32 = w.r_y;
+    CHK(gemm(h, g, s));
+    CHK(lnorm(h, w.r_y, 768, Ly.ln1, w.r_x, 768, w.r_xb, 768, M, 768, s));
+    g = gemm_args(w.r_xb, 768, Ly.fc1, M);
+    g.act = 1;  // GELU-erf
+    g.c16 = w.r_h;
+    CHK(gemm(h, g, s));
+    g = gemm_args(w.r_h, 3072, Ly.fc2, M);
+    g.res32 = w.r_x;
+    g.c32 = w.r_y;
+    CHK(gemm(h, g, s));
+    CHK(lnorm(h, w.r_y, 768, Ly.ln2, w.r_x, 768, w.r_xb, 768, M, 768, s));
+  }
+  ProfScope ps(h, s, PK_HEADS, 2.0 * B * 2 * (768 * 256 + 256 * 2), (double)B * 768 * 4 + 2 * 768 * 256 * 4);
+  HIPCHK(launch_text_heads(w.r_x, L * 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,
+                           h->h_b2m, ai, mi, scores, score_stride, B, s));
+  return 0;
+}
+
+// pre-LN CLIP encoder over x (fp32 residual, in place) with xb = LN1_0(x) already computed
+int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, bf16_t* xb, bf16_t* qkv,
+                     bf16_t* ctx, bf16_t* hid, const int32_t* mask, int causal, int B, int L, hipStream_t s) {
+  const int M = B * L;
+  for (int i = 0; i < 12; ++i) {
+    const EncLayer& Ly = layers[i];
+    GemmArgs g = gemm_args(xb, H, Ly.qkv, M);
+    g.c16 = qkv;
+    CHK(gemm(h, g, s));
+    CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
+    g = gemm_args(ctx, H, Ly.o, M);
+    g.res32 = x;
+    g.c32 = x;
+    CHK(gemm(h, g, s));
+    CHK(lnorm(h, x, H, Ly.ln2, nullptr, 0, xb, H, M, H, s));
+    g = gemm_args(xb, H, Ly.fc1, M);
+    g.act = 2;  // quick_gelu
+    g.c16 = hid;
+    CHK(gemm(h, g, s));
+    g = gemm_args(hid, I, Ly.fc2, M);
+    g.res32 = x;
+    g.c32 = x;
+    CHK(gemm(h, g, s));
+    if (i + 1 < 12) {
+      const EncLayer& Nx = layers[i + 1];
+      CHK(lnorm(h, x, H, Nx.ln1, nullptr, 0, xb, H, M, H, s));
+    }
+  }
+  return 0;
+}
+
+int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStream_t s) {
+  Workspace& w = h->ws;
+  {
+    ProfScope ps(h, s, PK_IM2COL, 2.0 * B * 49 * 3072, (double)B * 49 * 3072 * (1 + 2));
+    HIPCHK(launch_clip_im2col(img, w.v_col, B, s));
+  }
+  Lin16 pe;
+  pe.w = h->v_patch_w;
+  pe.out = 768;
+  pe.in = 3072;
+  GemmArgs g = gemm_args(w.v_col, 3072, pe, B * 49);
+  g.c32 = w.v_patch;
+  CHK(gemm(h, g, s));
+  {
+    ProfScope ps(h, s, PK_EMBED, 16.0 * B * 50 * 768, (double)B * 50 * 768 * (4 + 4 + 2));
+    HIPCHK(launch_clip_vision_assemble(w.v_patch, h->v_cls, h->v_pos, h->v_pre.g, h->v_pre.b, h->v_layers[0].ln1.g,
+                                       h->v_layers[0].ln1.b, 1e-5f, w.v_x, w.v_xb, B, s));
+  }
+  CHK(run_clip_encoder(h, h->v_layers, 768, 3072, 12, w.v_x, w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50, s));
+  HIPCHK(launch_gather_ln(w.v_x, nullptr, 50, h->v_post.g, h->v_post.b, 1e-5f, w.v_cls, nullptr, B, 768, s));
+  Lin16 pj;
+  pj.w = h->v_proj;
+  pj.out = 512;
+  pj.in = 768;
+  g = gemm_args(w.v_cls, 768, pj, B);
+  g.c32 = emb;
+  CHK(gemm(h, g, s));
+  HIPCHK(launch_l2norm(emb, B, 512, s));
+  return 0;
+}
+
+int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* emb, hipStream_t s) {
+  Workspace& w = h->ws;
+  {
+    ProfScope ps(h, s, PK_EMBED, 10.0 * B * L * 512, (double)B * L * 512 * (4 + 4 + 4 + 2));
+    HIPCHK(launch_clip_text_embed(ids, h->t_tok, h->t_pos, h->t_layers[0].ln1.g, h->t_layers[0].ln1.b, 1e-5f, w.t_x,
+                                  w.t_xb, B, L, 512, s));
+  }
+  CHK(run_clip_encoder(h, h->t_layers, 512, 2048, 8, w.t_x, w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, s));
+  HIPCHK(launch_eos_index(ids, w.t_eos, B, L, h->eos_id, s));
+  HIPCHK(launch_gather_ln(w.t_x, w.t_eos, L, h->t_final.g, h->t_final.b, 1e-5f, w.t_pool, nullptr, B, 512, s));
+  Lin16 pj;
+  pj.w = h->t_proj;
+  pj.out = 512;
+  pj.in = 512;
+  GemmArgs g = gemm_args(w.t_pool, 512, pj, B);
+  g.c32 = emb;
+  CHK(gemm(h, g, s));
+  HIPCHK(launch_l2norm(emb, B, 512, s));
+  return 0;
+}
+
+int run_effnet(mmf_handle* h, const uint8_t* img, int B, float* logits, float* score, int score_stride,
+               hipStream_t s) {
+  Workspace& w = h->ws;
+  bf16_t* cur = w.e_a;
+  bf16_t* nxt = w.e_b;
+  {
+    ProfScope ps(h, s, PK_STEM, 2.0 * B * 112 * 112 * 32 * 27, (double)B * (224 * 224 * 3 + 112 * 112 * 32 * 2));
+    HIPCHK(launch_effnet_stem(img, h->e_stem_w, h->e_stem_b, cur, B, s));
+  }
+  int H = 112, W = 112;
+  for (const EffBlock& b : h->e_blocks) {
+    const bf16_t* src = cur;
+    if (b.expand != 1) {
+      GemmArgs g = gemm_args(cur, b.cin, b.e, B * H * W);
+      g.act = 3;  // SiLU
+      g.c16 = w.e_exp;
+      CHK(gemm(h, g, s));
+      src = w.e_exp;
+    }
+    int nch = 0;
+    const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
+    {
+      ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k,
+                   (double)B * b.cexp * 2 * ((double)H * W + (double)Ho * Wo));
+      HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s));
+    }
+    ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, (double)B * b.cexp * 4 * (nch + 1));
+    HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s));
+    GemmArgs g = gemm_args(w.e_dw, b.cexp, b.p, B * Ho * Wo);
+    g.ascale = w.e_scale;
+    g.rows_per_batch = Ho * Wo;
+    if (b.residual) g.res16 = cur;
+    g.c16 = nxt;
+    CHK(gemm(h, g, s));
+    bf16_t* t = cur;
+    cur = nxt;
+    nxt = t;
+    H = Ho;
+    W = Wo;
+  }
+  GemmArgs g = gemm_args(cur, 320, h->e_head, B * H * W);
+  g.act = 3;
+  g.c16 = w.e_exp;
+  CHK(gemm(h, g, s));
+  ProfScope ps(h, s, PK_GAP, (double)B * H * W * 1280 + 4.0 * B * 1280, (double)B * H * W * 1280 * 2);
+  HIPCHK(launch_gap_classifier(w.e_exp, H * W, 1280, h->e_cls_w, h->e_cls_b, logits, score, score_stride, B, s));
+  return 0;
+}
+
+int ensure_sims(mmf_handle* h) {
+  if (!h->vault_n || !h->cap_b) return 0;
+  if (h->ws.s_cap_n >= h->vault_n) return 0;
+  void* p;
+  CHK(dev_alloc(h, &p, (size_t)h->cap_b * h->vault_n * sizeof(float), true));
+  h->ws.s_sims = (float*)p;
+  h->ws.s_cap_n = h->vault_n;
+  return 0;
+}
+
+}  // namespace
+
+// =============================================================================================
+extern "C" {
+
+const char* mmf_last_error(void) { return g_err.c_str(); }
+const char* mmf_version(void) { return "mmf_hip 0.1.0 gfx950"; }
+
+int mmf_create(int device, mmf_handle** out) {
+  if (!out) return fail(MMF_EINVAL, "out is NULL");
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(MMF_EINVAL, "device %d out of range (%d devices)", device, n);
+  HIPCHK(hipSetDevice(device));
+  mmf_handle* h = new (std::nothrow) mmf_handle();
+  if (!h) return fail(MMF_ENOMEM, "out of host memory");
+  h->device = device;
+  *out = h;
+  g_err.clear();
+  return 0;
+}
+
+void mmf_destroy(mmf_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  delete h;
+}
+
+int mmf_load_tensor(mmf_handle* h, const char* name, int dtype, int ndim, const int64_t* shape, const void* data) {
+  if (!h || !name || (!data && ndim > 0) || ndim < 0 || ndim > 8) return fail(MMF_EINVAL, "bad argument");
+  HostT t;
+  size_t n = 1;
+  for (int i = 0; i < ndim; ++i) {
+    if (shape[i] < 0) return fail(MMF_EINVAL, "negative dim in '%s'", name);
+    t.shape.push_back(shape[i]);
+    n *= (size_t)shape[i];
+  }
+  if (dtype == MMF_DTYPE_I64) return 0;  // integer buffers (num_batches_tracked) carry no arithmetic
+  if (dtype != MMF_DTYPE_F32) return fail(MMF_EINVAL, "unsupported dtype %d for '%s'", dtype, name);
+  t.f.resize(n);
+  if (n) std::memcpy(t.f.data(), data, n * sizeof(float));
+  h->staged[name] = std::move(t);
+  return 0;
+}
+
+int mmf_finalize(mmf_handle* h, int clip_eos_token_id) {
+  if (!h) return fail(MMF_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  h->eos_id = clip_eos_token_id;
+  int ready = h->ready & 32;
+  std::string missing;
+  auto attempt = [&](int bit, const char* probe, int (*fn)(mmf_handle*)) -> int {
+    if (!has(h, probe)) return 0;
+    int r = fn(h);
+    if (r) return r;
+    ready |= bit;
+    return 0;
+  };
+  CHK(attempt(1, "roberta.embeddings.word_embeddings.weight", finalize_text));
+  CHK(attempt(2, "efficientnet.features.0.0.weight", finalize_effnet));
+  CHK(attempt(4, "clip.vision_model.embeddings.patch_embedding.weight", finalize_clip_vision));
+  CHK(attempt(8, "clip.text_model.embeddings.token_embedding.weight", finalize_clip_text));
+  CHK(attempt(16, "fusion_layer.0.weight", finalize_fusion));
+  h->ready = ready;
+  h->staged.clear();
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
+int mmf_ready(mmf_handle* h) { return h ? h->ready : 0; }
+
+int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
+  if (!h || B <= 0 || Lr <= 0 || Lr > 512 || Lc <= 0 || Lc > 77)
+    return fail(MMF_EINVAL, "mmf_reserve: bad shape B=%d Lr=%d Lc=%d", B, Lr, Lc);
+  if (Lr > 128) return fail(MMF_EINVAL, "mmf_reserve: RoBERTa length %d > 128 not supported yet", Lr);
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  for (void* p : h->ws_allocs) (void)hipFree(p);
+  h->ws_allocs.clear();
+  h->ws = Workspace();
+  h->cap_b = h->cap_lr = h->cap_lc = 0;
+  Workspace& w = h->ws;
+  auto A = [&](void** p, size_t bytes) { return dev_alloc(h, p, bytes, true); };
+  const size_t Mr = (size_t)B * Lr, Mv = (size_t)B * 50, Mt = (size_t)B * Lc;
+  CHK(A((void**)&w.r_x, Mr * 768 * 4));
+  CHK(A((void**)&w.r_y, Mr * 768 * 4));
+  CHK(A((void**)&w.r_xb, Mr * 768 * 2));
+  CHK(A((void**)&w.r_qkv, Mr * 2304 * 2));
+  CHK(A((void**)&w.r_ctx, Mr * 768 * 2));
+  CHK(A((void**)&w.r_h, Mr * 3072 * 2));
+  CHK(A((void**)&w.v_col, (size_t)B * 49 * 3072 * 2));
+  CHK(A((void**)&w.v_patch, (size_t)B * 49 * 768 * 4));
+  CHK(A((void**)&w.v_x, Mv * 768 * 4));
+  CHK(A((void**)&w.v_xb, Mv * 768 * 2));
+  CHK(A((void**)&w.v_qkv, Mv * 2304 * 2));
+  CHK(A((void**)&w.v_ctx, Mv * 768 * 2));
+  CHK(A((void**)&w.v_h, Mv * 3072 * 2));
+  CHK(A((void**)&w.v_cls, (size_t)B * 768 * 2));
+  CHK(A((void**)&w.v_emb, (size_t)B * 512 * 4));
+  CHK(A((void**)&w.t_x, Mt * 512 * 4));
+  CHK(A((void**)&w.t_xb, Mt * 512 * 2));
+  CHK(A((void**)&w.t_qkv, Mt * 1536 * 2));
+  CHK(A((void**)&w.t_ctx, Mt * 512 * 2));
+  CHK(A((void**)&w.t_h, Mt * 2048 * 2));
+  CHK(A((void**)&w.t_pool, (size_t)B * 512 * 2));
+  CHK(A((void**)&w.t_emb, (size_t)B * 512 * 4));
+  CHK(A((void**)&w.t_eos, (size_t)B * 4));
+  // EfficientNet activation sizes per image
+  size_t max_io = 112 * 112 * 32, max_exp = 0, max_dw = 0, max_pool = 0, max_c = 1280;
+  {
+    int H = 112;
+    for (int si = 0; si < 7; ++si)
+      for (int j = 0; j < kStages[si][5]; ++j) {
+        const int e = kStages[si][0], st = j == 0 ? kStages[si][2] : 1;
+        const int cin = j == 0 ? kStages[si][3] : kStages[si][4], cout = kStages[si][4], cexp = cin * e;
+        const int Ho = (H - 1) / st + 1;
+        max_exp = std::max(max_exp, (size_t)H * H * cexp);
+        max_dw = std::max(max_dw, (size_t)Ho * Ho * cexp);
+        max_io = std::max(max_io, (size_t)Ho * Ho * cout);
+        max_pool = std::max(max_pool, (size_t)dwconv_nchunks(H, H, cexp, st) * cexp);
+        H = Ho;
+      }
+    max_exp = std::max(max_exp, (size_t)7 * 7 * 1280);
+  }
+  CHK(A((void**)&w.e_a, (size_t)B * max_io * 2));
+  CHK(A((void**)&w.e_b, (size_t)B * max_io * 2));
+  CHK(A((void**)&w.e_exp, (size_t)B * max_exp * 2));
+  CHK(A((void**)&w.e_dw, (size_t)B * max_dw * 2));
+  CHK(A((void**)&w.e_pool, (size_t)B * max_pool * 4));
+  CHK(A((void**)&w.e_scale, (size_t)B * max_c * 4));
+  h->cap_b = B;
+  h->cap_lr = Lr;
+  h->cap_lc = Lc;
+  CHK(ensure_sims(h));
+  return 0;
+}
+
+int mmf_text_forward(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
+                     float* scores2, void* stream) {
+  if (!h || !ids || !mask) return fail(MMF_EINVAL, "null argument");
+  if (!(h->ready & 1)) return fail(MMF_EINVAL, "text model (RoBERTa + heads) not loaded");
+  if (L > 128) return fail(MMF_EINVAL, "RoBERTa length %d > 128 not supported yet", L);
+  CHK(check_cap(h, B, L, 1));
+  HIPCHK(hipSetDevice(h->device));
+  return run_text(h, ids, mask, B, L, ai, mi, scores2, 2, (hipStream_t)stream);
+}
+
+int mmf_effnet_forward(mmf_handle* h, const uint8_t* img, int B, float* logits, float* score, void* stream) {
+  if (!h || !img) return fail(MMF_EINVAL, "null argument");
+  if (!(h->ready & 2)) return fail(MMF_EINVAL, "EfficientNet not loaded");
+  CHK(check_cap(h, B, 1, 1));
+  HIPCHK(hipSetDevice(h->device));
+  return run_effnet(h, img, B, logits, score, 1, (hipStream_t)stream);
+}
+
+int mmf_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, void* stream) {
+  if (!h || !img || !emb) return fail(MMF_EINVAL, "null argument");
+  if (!(h->ready & 4)) return fail(MMF_EINVAL, "CLIP vision tower not loaded");
+  CHK(check_cap(h, B, 1, 1));
+  HIPCHK(hipSetDevice(h->device));
+  return run_clip_image(h, img, B, emb, (hipStream_t)stream);
+}
+
+int mmf_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* emb, void* stream) {
+  if (!h || !ids || !mask || !emb) return fail(MMF_EINVAL, "null argument");
+  if (!(h->ready & 8)) return fail(MMF_EINVAL, "CLIP text tower not loaded");
+  if (L > 77) return fail(MMF_EINVAL, "CLIP text length %d > 77", L);
+  CHK(check_cap(h, B, 1, L));
+  HIPCHK(hipSetDevice(h->device));
+  return run_clip_text(h, ids, mask, B, L, emb, (hipStream_t)stream);
+}
+
+int mmf_set_vault(mmf_handle* h, const float* V, int N, int D) {
+  if (!h || !V || N <= 0 || D != 512) return fail(MMF_EINVAL, "mmf_set_vault: need N > 0 rows of D = 512");
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<float> u((size_t)N * D);
+  for (int i = 0; i < N; ++i) {
+    double s = 0;
+    for (int d = 0; d < D; ++d) s += (double)V[(size_t)i * D + d] * V[(size_t)i * D + d];
+    const float nrm = (float)std::sqrt(s);
+    for (int d = 0; d < D; ++d) u[(size_t)i * D + d] = V[(size_t)i * D + d] / nrm;
+  }
+  CHK(up_f32(h, &h->vault, u));
+  h->vault_n = N;
+  h->vault_title = nullptr;
+  h->ready |= 32;
+  h->ws.s_cap_n = 0;
+  return ensure_sims(h);
+}
+
+int mmf_set_vault_titles(mmf_handle* h, const int32_t* ids, const int32_t* mask, int N, int L, void* stream) {
+  if (!h || !ids || !mask) return fail(MMF_EINVAL, "null argument");
+  if (!(h->ready & 32) || N != h->vault_n) return fail(MMF_EINVAL, "set the vault (N=%d) first", h->vault_n);
+  if (!(h->ready & 8)) return fail(MMF_EINVAL, "CLIP text tower not loaded");
+  if (L > h->cap_lc || h->cap_b <= 0) return fail(MMF_EINVAL, "reserve CLIP length >= %d first", L);
+  HIPCHK(hipSetDevice(h->device));
+  float* t;
+  CHK(dev_alloc(h, (void**)&t, (size_t)N * 512 * 4));
+  hipStream_t s = (hipStream_t)stream;
+  for (int i = 0; i < N; i += h->cap_b) {
+    const int n = std::min(h->cap_b, N - i);
+    CHK(run_clip_text(h, ids + (size_t)i * L, mask + (size_t)i * L, n, L, t + (size_t)i * 512, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  h->vault_title = t;
+  return 0;
+}
+
+int mmf_vault_topk(mmf_handle* h, const float* q, int B, int k, float thresh, float* sims, int32_t* idx, float* disc,
+                   const float* temb, float* tsim, void* stream) {
+  if (!h || !q) return fail(MMF_EINVAL, "null argument");
+  if (!(h->ready & 32)) return fail(MMF_EINVAL, "vault not loaded");
+  if (k < 1 || k > 8) return fail(MMF_EINVAL, "top_k must be in [1, 8]");
+  CHK(check_cap(h, B, 1, 1));
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(launch_vault_sims(q, h->vault, h->ws.s_sims, B, h->vault_n, 512, s));
+  HIPCHK(launch_vault_topk(h->ws.s_sims, B, h->vault_n, k, thresh, sims, idx, disc, 1, temb, h->vault_title, 512,
+                           tsim, s));
+  return 0;
+}
+
+int mmf_fusion(mmf_handle* h, const float* x5, int B, float* probs, int32_t* verdict, float* conf, int32_t* rule,
+               void* stream) {
+  if (!h || !x5 || !probs || B <= 0) return fail(MMF_EINVAL, "bad argument");
+  if (!(h->ready & 16)) return fail(MMF_EINVAL, "fusion layer not loaded");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(launch_fusion(x5, h->f_w0, h->f_b0, h->f_w3, h->f_b3, h->f_w5, h->f_b5, probs, verdict, conf, rule, B,
+                       (hipStream_t)stream));
+  return 0;
+}
+
+int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_mask, int Lr, const int32_t* clip_ids,
+                      const int32_t* clip_mask, int Lc, const uint8_t* img_eff, const uint8_t* img_clip, int B,
+                      float* scores5, float* text_sim, float* probs2, int32_t* verdict, float* conf, int32_t* rule,
+                      float* top_sims, int32_t* top_idx, void* stream) {
+  if (!h || !rob_ids || !rob_mask || !clip_ids || !clip_mask || !img_eff || !scores5 || !probs2)
+    return fail(MMF_EINVAL, "null argument");
+  if ((h->ready & 31) != 31) return fail(MMF_EINVAL, "not all models loaded (ready mask %d)", h->ready);
+  if (Lr > 128 || Lc > 77) return fail(MMF_EINVAL, "lengths Lr=%d (<=128) Lc=%d (<=77)", Lr, Lc);
+  CHK(check_cap(h, B, Lr, Lc));
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (!img_clip) img_clip = img_eff;
+  Workspace& w = h->ws;
+  CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, s));
+  CHK(run_effnet(h, img_eff, B, nullptr, scores5 + 2, 5, s));
+  CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
+  CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, s));
+  HIPCHK(launch_rowdot(w.v_emb, w.t_emb, scores5 + 3, 5, B, 512, s));
+  if (h->ready & 32) {
+    ProfScope ps(h, s, PK_VAULT, 2.0 * B * h->vault_n * 512, (double)h->vault_n * 512 * 4 + (double)B * h->vault_n * 8);
+    HIPCHK(launch_vault_sims(w.v_emb, h->vault, w.s_sims, B, h->vault_n, 512, s));
+    HIPCHK(launch_vault_topk(w.s_sims, B, h->vault_n, 5, 0.85f, top_sims, top_idx, scores5 + 4, 5, w.t_emb,
+                             h->vault_title, 512, text_sim, s));
+  } else {
+    HIPCHK(launch_fill_strided(scores5 + 4, 5, B, 0.f, s));
+    if (text_sim) HIPCHK(hipMemsetAsync(text_sim, 0, (size_t)B * 4, s));
+    if (top_sims) HIPCHK(hipMemsetAsync(top_sims, 0, (size_t)B * 5 * 4, s));
+    if (top_idx) HIPCHK(hipMemsetAsync(top_idx, 0xff, (size_t)B * 5 * 4, s));
+  }
+  ProfScope ps(h, s, PK_FUSION, 2.0 * B * (5 * 64 + 64 * 32 + 32 * 2), (double)B * (5 + 2 + 3) * 4);
+  HIPCHK(launch_fusion(scores5, h->f_w0, h->f_b0, h->f_w3, h->f_b3, h->f_w5, h->f_b5, probs2, verdict, conf, rule, B,
+                       s));
+  return 0;
+}
+
+int mmf_profile_begin(mmf_handle* h) {
+  if (!h) return fail(MMF_EINVAL, "null handle");
+  h->prof = true;
+  h->prof_recs.clear();
+  h->ev_used = 0;
+  return 0;
+}
+
+int mmf_profile_end(mmf_handle* h, int max_kinds, int* counts, double* ms, double* flops, double* bytes) {
+  if (!h || max_kinds < PK_COUNT || !counts || !ms || !flops || !bytes)
+    return fail(MMF_EINVAL, "mmf_profile_end needs arrays of >= %d kinds", (int)PK_COUNT);
+  h->prof = false;
+  for (int k = 0; k < max_kinds; ++k) {
+    counts[k] = 0;
+    ms[k] = flops[k] = bytes[k] = 0.0;
+  }
+  if (!h->prof_recs.empty()) HIPCHK(hipEventSynchronize(h->ev_pool[h->prof_recs.back().ev + 1]));
+  for (const auto& r : h->prof_recs) {
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, h->ev_pool[r.ev], h->ev_pool[r.ev + 1]));
+    counts[r.kind] += 1;
+    ms[r.kind] += t;
+    flops[r.kind] += r.flops;
+    bytes[r.kind] += r.bytes;
+  }
+  h->prof_recs.clear();
+  h->ev_used = 0;
+  return PK_COUNT;
+}
+
+const char* mmf_profile_kind_name(int kind) { return prof_kind_name(kind); }
+
+int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual, float* c32,
+                  void* c16, int ldc, int M, int N, int K, int act, void* stream) {
+  GemmArgs g{};
+  g.A = (const bf16_t*)A;
+  g.lda = lda;
+  g.W = (const bf16_t*)W;
+  g.ldw = ldw;
+  g.bias = bias;
+  g.res32 = residual;
+  g.ldr = ldc;
+  g.c32 = c32;
+  g.c16 = (bf16_t*)c16;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.act = act;
+  if (!A || !W || (!c32 && !c16)) return fail(MMF_EINVAL, "null argument");
+  hipError_t e = launch_gemm(g, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MMF_EIO, "gemm: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int mmf_attention_bf16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,
+                       void* stream) {
+  if (!qkv || !out) return fail(MMF_EINVAL, "null argument");
+  hipError_t e = launch_attention((const bf16_t*)qkv, 3 * H * 64, mask, (bf16_t*)out, H * 64, B, L, H, causal,
+                                  (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MMF_EIO, "attention: %s", hipGetErrorString(e));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,49 @@
+// Device-side helpers shared by the gfx950 kernels of libmmf_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;  // raw bf16 storage
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MMF_DEV __device__ __forceinline__
+
+MMF_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+MMF_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 on gfx950 (RNE, NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+MMF_DEV uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+MMF_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+MMF_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+MMF_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+MMF_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// activations (fp32)
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QUICK_GELU = 2, ACT_SILU = 3, ACT_RELU = 4 };
+MMF_DEV float act_apply(float x, int act) {
+  switch (act) {
+    case ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));  // GELU-erf
+    case ACT_QUICK_GELU: return x / (1.0f + __expf(-1.702f * x));              // x*sigmoid(1.702x)
+    case ACT_SILU: return x / (1.0f + __expf(-x));
+    case ACT_RELU: return fmaxf(x, 0.0f);
+    default: return x;
+  }
+}
+
+MMF_DEV f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+MMF_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }

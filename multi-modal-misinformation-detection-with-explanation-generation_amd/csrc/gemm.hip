@@ -1,0 +1,200 @@
+// bf16 MFMA GEMM for gfx950: C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ residual), fp32 accumulate.
+//
+// Used for every dense contraction of the hot path: RoBERTa / CLIP QKV, out-proj, FFN (SURVEY.md
+// §2.1), the CLIP patch embedding (im2col GEMM), the CLIP projections and the EfficientNet 1x1
+// convolutions (BatchNorm folded into W/bias; SE excitation folded into the A load).
+//
+// Design (CDNA4, 64-wide waves):
+//  * 256 threads = 4 waves in a WGM x WGN grid; each wave owns a (BM/WGM) x (BN/WGN) output block
+//    of 16x16 tiles computed with v_mfma_f32_16x16x32_bf16.
+//  * Operands are "swapped" (MFMA A-operand = W rows, B-operand = A rows) so that each lane ends
+//    with 4 CONSECUTIVE output columns of one row -> 16-B fp32 / 8-B bf16 epilogue stores and
+//    vector bias/residual loads.
+//  * BK = 64: LDS tiles [rows][64] bf16 (128-B rows) with an XOR swizzle (16-B chunk ^= row & 7)
+//    that makes the 16-lane ds_read_b128 fragment reads conflict-free; double-buffered, register
+//    staged (next tile's global loads issued before the MFMAs, written to LDS after them).
+//  * XCD-aware bijective block remap so consecutive tiles of one row panel share an XCD's L2.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+template <int BM, int BN, int WGM, int WGN>
+struct Cfg {
+  static constexpr int TM = BM / WGM, TN = BN / WGN;
+  static constexpr int MI = TM / 16, NI = TN / 16;
+  static constexpr int XC = BM * 8 / 256;  // 16-B chunks per thread, A tile
+  static constexpr int WC = BN * 8 / 256;  // 16-B chunks per thread, W tile
+  static_assert(WGM * WGN == 4, "4 waves");
+  static_assert(MI >= 1 && NI >= 1, "tile");
+  static_assert(XC >= 1 && WC >= 1, "chunking");
+};
+
+MMF_DEV int swz(int row, int kc) { return row * BK + ((kc ^ (row & 7)) << 3); }
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) {
+  using C = Cfg<BM, BN, WGM, WGN>;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
+  auto Xs = [&](int buf) { return lds + buf * (BM + BN) * BK; };
+  auto Ws = [&](int buf) { return lds + buf * (BM + BN) * BK + BM * BK; };
+
+  // XCD-aware bijective remap of the 1-D grid
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = wgid / tilesN, tn = wgid - tm * tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int M = g.M, N = g.N, K = g.K;
+  const int nk = (K + BK - 1) / BK;
+
+  uint4 xr[C::XC], wr[C::WC];
+
+  auto load_regs = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < C::XC; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, kc = c & 7;
+      const int m = m0 + row, k = k0 + kc * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (m < M && k < K) {
+        v = *reinterpret_cast<const uint4*>(g.A + (size_t)m * g.lda + k);
+        if (g.ascale) {
+          const float* s = g.ascale + (size_t)(m / g.rows_per_batch) * K + k;
+          const float4 s0 = *reinterpret_cast<const float4*>(s);
+          const float4 s1 = *reinterpret_cast<const float4*>(s + 4);
+          v.x = pack2bf(lo_bf(v.x) * s0.x, hi_bf(v.x) * s0.y);
+          v.y = pack2bf(lo_bf(v.y) * s0.z, hi_bf(v.y) * s0.w);
+          v.z = pack2bf(lo_bf(v.z) * s1.x, hi_bf(v.z) * s1.y);
+          v.w = pack2bf(lo_bf(v.w) * s1.z, hi_bf(v.w) * s1.w);
+        }
+      }
+      xr[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < C::WC; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, kc = c & 7;
+      const int n = n0 + row, k = k0 + kc * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n < N && k < K) v = *reinterpret_cast<const uint4*>(g.W + (size_t)n * g.ldw + k);
+      wr[i] = v;
+    }
+  };
+  auto store_lds = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < C::XC; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<uint4*>(Xs(buf) + swz(c >> 3, c & 7)) = xr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < C::WC; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<uint4*>(Ws(buf) + swz(c >> 3, c & 7)) = wr[i];
+    }
+  };
+
+  f32x4 acc[C::NI][C::MI];
+#pragma unroll
+  for (int i = 0; i < C::NI; ++i)
+#pragma unroll
+    for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_regs(0);
+  store_lds(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load_regs(kt + 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 wf[C::NI], xf[C::MI];
+#pragma unroll
+      for (int i = 0; i < C::NI; ++i) {
+        const int row = wn * C::TN + i * 16 + fr;
+        wf[i] = as_bf16x8(*reinterpret_cast<const uint4*>(Ws(buf) + swz(row, ks * 4 + fg)));
+      }
+#pragma unroll
+      for (int j = 0; j < C::MI; ++j) {
+        const int row = wm * C::TM + j * 16 + fr;
+        xf[j] = as_bf16x8(*reinterpret_cast<const uint4*>(Xs(buf) + swz(row, ks * 4 + fg)));
+      }
+#pragma unroll
+      for (int i = 0; i < C::NI; ++i)
+#pragma unroll
+        for (int j = 0; j < C::MI; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) store_lds(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[m][n..n+3]
+#pragma unroll
+  for (int j = 0; j < C::MI; ++j) {
+    const int m = m0 + wm * C::TM + j * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i) {
+      const int n = n0 + wn * C::TN + i * 16 + fg * 4;
+      if (n >= N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.bias) {
+        const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (g.act) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = act_apply(v[t], g.act);
+      }
+      if (g.res32) {
+        const float4 rr = *reinterpret_cast<const float4*>(g.res32 + (size_t)m * g.ldr + n);
+        v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+      } else if (g.res16) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(g.res16 + (size_t)m * g.ldr + n);
+        v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
+      }
+      if (g.c32) *reinterpret_cast<float4*>(g.c32 + (size_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+      if (g.c16)
+        *reinterpret_cast<uint2*>(g.c16 + (size_t)m * g.ldc + n) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t run(const GemmArgs& a, hipStream_t s) {
+  const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN), dim3(256), 0, s, a, tilesN);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int gemm_config(const GemmArgs& a) {
+  if (a.N <= 32) return 0;
+  if (a.N <= 64) return 1;
+  if (a.M <= 512) return 2;  // skinny-M (projections, M = batch)
+  return 3;
+}
+
+const char* gemm_config_name(int c) {
+  static const char* names[] = {"gemm_bf16<256,32,4,1>", "gemm_bf16<256,64,4,1>", "gemm_bf16<64,128,1,4>",
+                                "gemm_bf16<128,128,2,2>"};
+  return (c >= 0 && c < 4) ? names[c] : "gemm_bf16<?>";
+}
+
+hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return hipSuccess;
+  if ((a.K & 7) || (a.N & 3) || (a.lda & 7) || (a.ldw & 7) || (a.ldc & 3)) return hipErrorInvalidValue;
+  switch (gemm_config(a)) {
+    case 0: return run<256, 32, 4, 1>(a, s);
+    case 1: return run<256, 64, 4, 1>(a, s);
+    case 2: return run<64, 128, 1, 4>(a, s);
+    default: return run<128, 128, 2, 2>(a, s);
+  }
+}

@@ -1,0 +1,88 @@
+// Host-side launchers of the gfx950 kernels (implemented in *.hip).  All enqueue on `stream`
+// and return hipError_t of the launch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+
+struct GemmArgs {
+  const bf16_t* A;  int lda;     // activations [M][K] bf16
+  const bf16_t* W;  int ldw;     // weights [N][K] bf16 (PyTorch Linear layout)
+  const float* bias;             // [N] or null
+  const float* res32;            // fp32 residual [M][N] (ldr) or null
+  const bf16_t* res16;           // bf16 residual [M][N] (ldr) or null
+  int ldr;
+  float* c32;                    // fp32 out [M][N] (ldc) or null
+  bf16_t* c16;                   // bf16 out [M][N] (ldc) or null
+  int ldc;
+  const float* ascale;           // per-(batch, k) fp32 scale of A (SE excitation) or null
+  int rows_per_batch;            // rows of A per batch item when ascale != null
+  int M, N, K, act;
+};
+hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
+int gemm_config(const GemmArgs& a);          // which tile instantiation launch_gemm picks (0..3)
+const char* gemm_config_name(int c);
+
+// LayerNorm over rows of width C (multiple of 256): y = LN(x [+ add]) * g + b.
+// x/add fp32 with row strides; writes fp32 y32 and/or bf16 y16.
+hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd, const float* g, const float* b,
+                            float eps, float* y32, int ldy32, bf16_t* y16, int ldy16, int rows, int C,
+                            hipStream_t s);
+
+// Fused multi-head attention, head_dim 64, L <= 128: qkv bf16 [B*L][ldqkv] with q at col h*64,
+// k at D + h*64, v at 2D + h*64 (D = H*64); mask int32 [B][L] (1 keep) or null; out bf16 [B*L][ldo].
+hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, bf16_t* out, int ldo, int B,
+                            int L, int H, int causal, hipStream_t s);
+
+// RoBERTa embeddings + LayerNorm -> x fp32 [B*L][H], xb bf16 [B*L][H]
+hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
+                                const float* g, const float* b, float eps, float* x, bf16_t* xb, int B, int L,
+                                int H, int pad_id, hipStream_t s);
+// CLIP text embeddings (tok + pos) -> x fp32, then LN1 of layer 0 -> xb bf16
+hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
+                                  const float* b, float eps, float* x, bf16_t* xb, int B, int L, int H,
+                                  hipStream_t s);
+// CLIP patch im2col with normalisation: img uint8 [B,224,224,3] -> A bf16 [B*49][3072]
+hipError_t launch_clip_im2col(const uint8_t* img, bf16_t* A, int B, hipStream_t s);
+// CLIP vision: x = preLN(cat(cls, patches) + pos) -> x fp32 [B*50][768], xb = LN1(x) bf16
+hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
+                                       const float* pre_g, const float* pre_b, const float* ln1_g,
+                                       const float* ln1_b, float eps, float* x, bf16_t* xb, int B,
+                                       hipStream_t s);
+// EOS index per row (first == eos_id, or argmax when eos_id == 2)
+hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int eos_id, hipStream_t s);
+// gather rows: out bf16 [B][C] = LN(x[row_index(b)]) where row_index = b*L + (idx ? idx[b] : 0)
+hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const float* g, const float* b, float eps,
+                            bf16_t* out, float* out32, int B, int C, hipStream_t s);
+// L2-normalise rows of fp32 [B][C] in place (C multiple of 64)
+hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s);
+// two 768->256->2 heads (fp32) from CLS rows x[b*L*768]; writes logits and softmax[:,1] scores
+hipError_t launch_text_heads(const float* x, int row_stride, const float* w1a, const float* b1a,
+                             const float* w2a, const float* b2a, const float* w1m, const float* b1m,
+                             const float* w2m, const float* b2m, float* ai_logits, float* mi_logits,
+                             float* scores, int score_stride, int B, hipStream_t s);
+// fusion MLP 5->64->32->2 (+ verdict, confidence, explanation rule)
+hipError_t launch_fusion(const float* x5, const float* w0, const float* b0, const float* w3, const float* b3,
+                         const float* w5, const float* b5, float* probs, int32_t* verdict, float* conf,
+                         int32_t* rule, int B, hipStream_t s);
+// cosine of unit rows: out[b*ostride] = dot(a[b], c[b])
+hipError_t launch_rowdot(const float* a, const float* c, float* out, int ostride, int B, int C, hipStream_t s);
+// vault: S[B][N] = Q[B][D] . V[N][D]^T (fp32)
+hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s);
+hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, float* sims, int32_t* idx,
+                             float* disc, int disc_stride, const float* text_emb, const float* title_emb, int D,
+                             float* text_sim, hipStream_t s);
+
+// EfficientNet-B0 pieces (NHWC bf16 activations)
+hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, bf16_t* out, int B,
+                              hipStream_t s);
+hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part,
+                         int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s);
+hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
+                     const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s);
+hipError_t launch_gap_classifier(const bf16_t* x, int HW, int C, const float* w, const float* b, float* logits,
+                                 float* score, int score_stride, int B, hipStream_t s);
+hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);
+// number of pool-partial chunks launch_dwconv uses for an output of Ho x Wo with C channels
+int dwconv_nchunks(int H, int W, int C, int stride);

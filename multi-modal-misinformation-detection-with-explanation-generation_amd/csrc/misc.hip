@@ -1,0 +1,294 @@
+// Small fp32 kernels at the ends of the path: the RoBERTa dual heads, the FusionJudge MLP with
+// verdict / explanation rule, cosine rows, and the Truth-Vault search (similarities + top-k).
+// These are latency/L2-bound: they run in exact fp32 like the reference.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// misinfo_forensics.py:57-69, 97-98, 342-347: two Linear(768,256)-ReLU-Linear(256,2) heads on the
+// CLS row, softmax[:, 1].  Block = 4 rows; thread j = hidden unit j; W1 stored transposed [768][256]
+// so a k-step reads one coalesced 1-KB row.
+__global__ __launch_bounds__(256) void text_heads_kernel(const float* x, int row_stride, const float* w1a,
+                                                         const float* b1a, const float* w2a, const float* b2a,
+                                                         const float* w1m, const float* b1m, const float* w2m,
+                                                         const float* b2m, float* ai_logits, float* mi_logits,
+                                                         float* scores, int score_stride, int B) {
+  __shared__ float xs[4][768];
+  __shared__ float red[4][4][4];  // [wave][row][head*2+o]
+  const int tid = threadIdx.x, r0 = blockIdx.x * 4;
+  for (int i = tid; i < 4 * 768; i += 256) {
+    const int r = i / 768, c = i % 768;
+    xs[r][c] = (r0 + r < B) ? x[(size_t)(r0 + r) * row_stride + c] : 0.f;
+  }
+  __syncthreads();
+  float part[4][4];
+#pragma unroll
+  for (int head = 0; head < 2; ++head) {
+    const float* w1 = head ? w1m : w1a;
+    const float* b1 = head ? b1m : b1a;
+    const float* w2 = head ? w2m : w2a;
+    float hsum[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 768; ++k) {
+      const float w = w1[(size_t)k * 256 + tid];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hsum[r] = fmaf(w, xs[r][k], hsum[r]);
+    }
+    const float w20 = w2[tid], w21 = w2[256 + tid], bb = b1[tid];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float hv = fmaxf(hsum[r] + bb, 0.f);
+      part[r][head * 2 + 0] = hv * w20;
+      part[r][head * 2 + 1] = hv * w21;
+    }
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const float v = wave_sum(part[r][o]);
+      if (lane == 0) red[wave][r][o] = v;
+    }
+  __syncthreads();
+  if (tid < 4 && r0 + tid < B) {
+    const int r = tid, row = r0 + r;
+    float l[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) l[o] = red[0][r][o] + red[1][r][o] + red[2][r][o] + red[3][r][o];
+    l[0] += b2a[0]; l[1] += b2a[1]; l[2] += b2m[0]; l[3] += b2m[1];
+    if (ai_logits) { ai_logits[row * 2] = l[0]; ai_logits[row * 2 + 1] = l[1]; }
+    if (mi_logits) { mi_logits[row * 2] = l[2]; mi_logits[row * 2 + 1] = l[3]; }
+    if (scores) {
+      // softmax(l)[1] = exp(l1 - m) / (exp(l0 - m) + exp(l1 - m))
+      const float ma = fmaxf(l[0], l[1]), mm = fmaxf(l[2], l[3]);
+      const float ea0 = expf(l[0] - ma), ea1 = expf(l[1] - ma), em0 = expf(l[2] - mm), em1 = expf(l[3] - mm);
+      scores[(size_t)row * score_stride] = ea1 / (ea0 + ea1);
+      scores[(size_t)row * score_stride + 1] = em1 / (em0 + em1);
+    }
+  }
+}
+
+// misinfo_forensics.py:575-615 (fusion_verdict) + 742-765 (fallback explanation rule cascade)
+__global__ __launch_bounds__(256) void fusion_kernel(const float* x5, const float* w0, const float* b0,
+                                                     const float* w3, const float* b3, const float* w5,
+                                                     const float* b5, float* probs, int32_t* verdict, float* conf,
+                                                     int32_t* rule, int B) {
+  __shared__ float sw0[64 * 5], sb0[64], sw3[32 * 64], sb3[32], sw5[64], sb5[2];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 320; i += 256) sw0[i] = w0[i];
+  for (int i = tid; i < 2048; i += 256) sw3[i] = w3[i];
+  if (tid < 64) { sb0[tid] = b0[tid]; sw5[tid] = w5[tid]; }
+  if (tid < 32) sb3[tid] = b3[tid];
+  if (tid < 2) sb5[tid] = b5[tid];
+  __syncthreads();
+  const int row = blockIdx.x * 256 + tid;
+  if (row >= B) return;
+  float x[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) x[i] = x5[(size_t)row * 5 + i];
+  float h1[64];
+#pragma unroll
+  for (int o = 0; o < 64; ++o) {
+    float a = sb0[o];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) a = fmaf(sw0[o * 5 + i], x[i], a);
+    h1[o] = fmaxf(a, 0.f);
+  }
+  float l0 = sb5[0], l1 = sb5[1];
+#pragma unroll 4
+  for (int o = 0; o < 32; ++o) {
+    float a = sb3[o];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) a = fmaf(sw3[o * 64 + i], h1[i], a);
+    a = fmaxf(a, 0.f);
+    l0 = fmaf(sw5[o], a, l0);
+    l1 = fmaf(sw5[32 + o], a, l1);
+  }
+  const float m = fmaxf(l0, l1);
+  const float e0 = expf(l0 - m), e1 = expf(l1 - m);
+  const float p0 = e0 / (e0 + e1), p1 = e1 / (e0 + e1);
+  probs[(size_t)row * 2] = p0;
+  probs[(size_t)row * 2 + 1] = p1;
+  const int v = p1 > 0.5f ? 1 : 0;
+  if (verdict) verdict[row] = v;
+  if (conf) conf[row] = v ? p1 : p0;
+  if (rule) {
+    int rr = 5;
+    if (x[4] > 0.7f) rr = 0;
+    else if (x[2] > 0.7f) rr = 1;
+    else if (x[0] > 0.7f) rr = 2;
+    else if (x[1] > 0.7f) rr = 3;
+    else if (x[3] < 0.3f) rr = 4;
+    rule[row] = rr;
+  }
+}
+
+__global__ __launch_bounds__(256) void rowdot_kernel(const float* a, const float* c, float* out, int ostride, int B,
+                                                     int C) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  float s = 0.f;
+  for (int i = lane; i < C; i += 64) s = fmaf(a[(size_t)row * C + i], c[(size_t)row * C + i], s);
+  s = wave_sum(s);
+  if (lane == 0) out[(size_t)row * ostride] = s;
+}
+
+// S[B][N] = Q[B][D] . V[N][D]^T, fp32 (misinfo_forensics.py:446).  Tile 16 queries x 64 rows.
+__global__ __launch_bounds__(256) void vault_sims_kernel(const float* q, const float* v, float* S, int B, int N,
+                                                         int D) {
+  __shared__ float qs[16][33];
+  __shared__ float vs[64][33];
+  const int tid = threadIdx.x, tq = tid >> 4, tv = tid & 15;
+  const int q0 = blockIdx.y * 16, v0 = blockIdx.x * 64;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < D; k0 += 32) {
+    for (int i = tid; i < 16 * 32; i += 256) {
+      const int r = i >> 5, c = i & 31;
+      qs[r][c] = (q0 + r < B) ? q[(size_t)(q0 + r) * D + k0 + c] : 0.f;
+    }
+    for (int i = tid; i < 64 * 32; i += 256) {
+      const int r = i >> 5, c = i & 31;
+      vs[r][c] = (v0 + r < N) ? v[(size_t)(v0 + r) * D + k0 + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const float a = qs[tq][k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(a, vs[tv + 16 * j][k], acc[j]);
+    }
+    __syncthreads();
+  }
+  if (q0 + tq < B) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (v0 + tv + 16 * j < N) S[(size_t)(q0 + tq) * N + v0 + tv + 16 * j] = acc[j];
+  }
+}
+
+// (value desc, index desc) order, i.e. numpy argsort()[-k:][::-1] for distinct values
+MMF_DEV bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia > ib); }
+
+template <int K>
+__global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, int N, float thresh, float* sims,
+                                                         int32_t* idx, float* disc, int disc_stride,
+                                                         const float* temb, const float* title, int D,
+                                                         float* tsim) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  float tv[K];
+  int ti[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) { tv[i] = -INFINITY; ti[i] = -1; }
+  const float* s = S + (size_t)row * N;
+  for (int j = lane; j < N; j += 64) {
+    float v = s[j];
+    int vi = j;
+    if (better(v, vi, tv[K - 1], ti[K - 1])) {
+      tv[K - 1] = v; ti[K - 1] = vi;
+#pragma unroll
+      for (int i = K - 1; i > 0; --i) {
+        if (better(tv[i], ti[i], tv[i - 1], ti[i - 1])) {
+          const float a = tv[i]; tv[i] = tv[i - 1]; tv[i - 1] = a;
+          const int b = ti[i]; ti[i] = ti[i - 1]; ti[i - 1] = b;
+        }
+      }
+    }
+  }
+  float outv[K];
+  int outi[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    float bv = tv[0];
+    int bi = ti[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    outv[t] = bv; outi[t] = bi;
+    if (ti[0] == bi) {  // pop the head of the winning lane
+#pragma unroll
+      for (int i = 0; i < K - 1; ++i) { tv[i] = tv[i + 1]; ti[i] = ti[i + 1]; }
+      tv[K - 1] = -INFINITY; ti[K - 1] = -1;
+    }
+  }
+  const bool hit = outv[0] > thresh;
+  if (lane == 0) {
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      if (sims) sims[(size_t)row * K + t] = outv[t];
+      if (idx) idx[(size_t)row * K + t] = outi[t];
+    }
+    if (disc) disc[(size_t)row * disc_stride] = hit ? outv[0] : 0.f;
+  }
+  if (tsim) {
+    float d = 0.f;
+    if (hit && temb && title) {
+      for (int c = lane; c < D; c += 64) d = fmaf(temb[(size_t)row * D + c], title[(size_t)outi[0] * D + c], d);
+      d = wave_sum(d);
+    }
+    if (lane == 0) tsim[row] = d;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_text_heads(const float* x, int row_stride, const float* w1a, const float* b1a, const float* w2a,
+                             const float* b2a, const float* w1m, const float* b1m, const float* w2m,
+                             const float* b2m, float* ai_logits, float* mi_logits, float* scores, int score_stride,
+                             int B, hipStream_t s) {
+  hipLaunchKernelGGL(text_heads_kernel, dim3((B + 3) / 4), dim3(256), 0, s, x, row_stride, w1a, b1a, w2a, b2a, w1m,
+                     b1m, w2m, b2m, ai_logits, mi_logits, scores, score_stride, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_fusion(const float* x5, const float* w0, const float* b0, const float* w3, const float* b3,
+                         const float* w5, const float* b5, float* probs, int32_t* verdict, float* conf,
+                         int32_t* rule, int B, hipStream_t s) {
+  hipLaunchKernelGGL(fusion_kernel, dim3((B + 255) / 256), dim3(256), 0, s, x5, w0, b0, w3, b3, w5, b5, probs,
+                     verdict, conf, rule, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_rowdot(const float* a, const float* c, float* out, int ostride, int B, int C, hipStream_t s) {
+  hipLaunchKernelGGL(rowdot_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a, c, out, ostride, B, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s) {
+  if (D & 31) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(vault_sims_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, float* sims, int32_t* idx,
+                             float* disc, int disc_stride, const float* text_emb, const float* title_emb, int D,
+                             float* text_sim, hipStream_t s) {
+  const dim3 grid((B + 3) / 4), blk(256);
+#define TOPK_CASE(KK)                                                                                          \
+  case KK:                                                                                                     \
+    hipLaunchKernelGGL(vault_topk_kernel<KK>, grid, blk, 0, s, S, B, N, thresh, sims, idx, disc, disc_stride, \
+                       text_emb, title_emb, D, text_sim);                                                      \
+    break;
+  switch (k) {
+    TOPK_CASE(1) TOPK_CASE(2) TOPK_CASE(3) TOPK_CASE(4) TOPK_CASE(5) TOPK_CASE(6) TOPK_CASE(7) TOPK_CASE(8)
+    default: return hipErrorInvalidValue;
+  }
+#undef TOPK_CASE
+  return hipGetLastError();
+}
+
+namespace {
+__global__ void fill_strided_kernel(float* p, int stride, int B, float v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) p[(size_t)i * stride] = v;
+}
+}  // namespace
+
+hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s) {
+  hipLaunchKernelGGL(fill_strided_kernel, dim3((B + 255) / 256), dim3(256), 0, s, p, stride, B, v);
+  return hipGetLastError();
+}

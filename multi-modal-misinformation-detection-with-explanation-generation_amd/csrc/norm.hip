@@ -1,0 +1,280 @@
+// Row-wise kernels: LayerNorm, embeddings (+LN), CLIP patch im2col, EOS pooling, L2 norm.
+// One 64-lane wave per row of width C in {512, 768}: every lane holds C/256 float4 in registers,
+// so a row is read once, reduced with DPP/shuffle trees and written once (fp32 residual stream
+// and/or bf16 GEMM operand).  Variance is the two-pass mean((x-mean)^2) in fp32 like torch.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+template <int NV>
+MMF_DEV void ln_row(float4 (&v)[NV], const float* g, const float* b, float eps, int C, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += v[i].x + v[i].y + v[i].z + v[i].w;
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i].x -= mean; v[i].y -= mean; v[i].z -= mean; v[i].w -= mean;
+    q += v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    const float4 gg = *reinterpret_cast<const float4*>(g + c);
+    const float4 bb = *reinterpret_cast<const float4*>(b + c);
+    v[i].x = v[i].x * rstd * gg.x + bb.x;
+    v[i].y = v[i].y * rstd * gg.y + bb.y;
+    v[i].z = v[i].z * rstd * gg.z + bb.z;
+    v[i].w = v[i].w * rstd * gg.w + bb.w;
+  }
+}
+
+template <int NV>
+MMF_DEV void load_row(float4 (&v)[NV], const float* x, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const float4*>(x + (i * 64 + lane) * 4);
+}
+template <int NV>
+MMF_DEV void add_row(float4 (&v)[NV], const float* x, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float4 a = *reinterpret_cast<const float4*>(x + (i * 64 + lane) * 4);
+    v[i].x += a.x; v[i].y += a.y; v[i].z += a.z; v[i].w += a.w;
+  }
+}
+template <int NV>
+MMF_DEV void store_row(const float4 (&v)[NV], float* y32, bf16_t* y16, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (y32) *reinterpret_cast<float4*>(y32 + c) = v[i];
+    if (y16) *reinterpret_cast<uint2*>(y16 + c) = make_uint2(pack2bf(v[i].x, v[i].y), pack2bf(v[i].z, v[i].w));
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx, const float* add, int ldadd,
+                                                        const float* g, const float* b, float eps, float* y32,
+                                                        int ldy32, bf16_t* y16, int ldy16, int rows) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float4 v[NV];
+  load_row<NV>(v, x + (size_t)row * ldx, lane);
+  if (add) add_row<NV>(v, add + (size_t)row * ldadd, lane);
+  ln_row<NV>(v, g, b, eps, NV * 256, lane);
+  store_row<NV>(v, y32 ? y32 + (size_t)row * ldy32 : nullptr, y16 ? y16 + (size_t)row * ldy16 : nullptr, lane);
+}
+
+// RoBERTa: position ids = cumsum(ids != pad) * (ids != pad) + pad (TF roberta:142-155);
+// x = LN(word[id] + type[0] + pos[pid]).  One block per sequence.
+template <int NV>
+__global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, const float* word, const float* pos,
+                                                            const float* type0, const float* g, const float* b,
+                                                            float eps, float* x, bf16_t* xb, int L, int pad) {
+  __shared__ int s_ids[512];
+  __shared__ int s_pos[512];
+  const int bi = blockIdx.x, tid = threadIdx.x;
+  for (int t = tid; t < L; t += 256) s_ids[t] = ids[(size_t)bi * L + t];
+  __syncthreads();
+  if (tid < 64) {  // wave-level inclusive scan of the non-pad flags, 64 positions per step
+    int carry = 0;
+    for (int base = 0; base < L; base += 64) {
+      const int t = base + tid;
+      int f = (t < L && s_ids[t] != pad) ? 1 : 0;
+      int v = f;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int n = __shfl_up(v, o, 64);
+        if (tid >= o) v += n;
+      }
+      if (t < L) s_pos[t] = f ? (carry + v + pad) : pad;
+      carry += __shfl(v, 63, 64);
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  constexpr int C = NV * 256;
+  for (int t = wave; t < L; t += 4) {
+    float4 v[NV];
+    load_row<NV>(v, word + (size_t)s_ids[t] * C, lane);
+    add_row<NV>(v, type0, lane);
+    add_row<NV>(v, pos + (size_t)s_pos[t] * C, lane);
+    ln_row<NV>(v, g, b, eps, C, lane);
+    const size_t r = (size_t)bi * L + t;
+    store_row<NV>(v, x + r * C, xb + r * C, lane);
+  }
+}
+
+// CLIP text: x = tok[id] + pos[t] (fp32 residual stream); xb = LN1_layer0(x) (bf16)
+template <int NV>
+__global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids, const float* tok, const float* pos,
+                                                              const float* g, const float* b, float eps, float* x,
+                                                              bf16_t* xb, int rows, int L) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  constexpr int C = NV * 256;
+  const int t = row % L;
+  float4 v[NV];
+  load_row<NV>(v, tok + (size_t)ids[row] * C, lane);
+  add_row<NV>(v, pos + (size_t)t * C, lane);
+  store_row<NV>(v, x + (size_t)row * C, nullptr, lane);
+  ln_row<NV>(v, g, b, eps, C, lane);
+  store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
+}
+
+// CLIP patch embedding operand: A[b*49 + p][c*1024 + ky*32 + kx] = (img/255 - mean_c)/std_c
+__global__ __launch_bounds__(256) void clip_im2col_kernel(const uint8_t* img, bf16_t* A, int B) {
+  const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)B * 49 * 384;
+  if (gid >= total) return;
+  const int g = gid % 384;
+  const size_t rowp = gid / 384;
+  const int p = rowp % 49, bi = rowp / 49;
+  const int c = g >> 7, ky = (g & 127) >> 2, kx0 = (g & 3) * 8;
+  const int y = (p / 7) * 32 + ky, x0 = (p % 7) * 32 + kx0;
+  const float mean = c == 0 ? 0.48145466f : (c == 1 ? 0.4578275f : 0.40821073f);
+  const float istd = 1.0f / (c == 0 ? 0.26862954f : (c == 1 ? 0.26130258f : 0.27577711f));
+  const uint8_t* src = img + (((size_t)bi * 224 + y) * 224 + x0) * 3 + c;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = ((float)src[j * 3] * (1.0f / 255.0f) - mean) * istd;
+  *reinterpret_cast<uint4*>(A + rowp * 3072 + g * 8) =
+      make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+}
+
+// CLIP vision: e = (t==0 ? class_emb : patch[b*49+t-1]) + pos[t]; x = pre_LN(e); xb = LN1(x)
+__global__ __launch_bounds__(256) void clip_vision_assemble_kernel(const float* patches, const float* cls,
+                                                                   const float* pos, const float* pg,
+                                                                   const float* pb, const float* g1,
+                                                                   const float* b1, float eps, float* x,
+                                                                   bf16_t* xb, int rows) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  constexpr int NV = 3, C = 768;
+  const int t = row % 50, bi = row / 50;
+  float4 v[NV];
+  if (t == 0) load_row<NV>(v, cls, lane);
+  else load_row<NV>(v, patches + ((size_t)bi * 49 + t - 1) * C, lane);
+  add_row<NV>(v, pos + (size_t)t * C, lane);
+  ln_row<NV>(v, pg, pb, eps, C, lane);
+  store_row<NV>(v, x + (size_t)row * C, nullptr, lane);
+  ln_row<NV>(v, g1, b1, eps, C, lane);
+  store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
+}
+
+__global__ void eos_index_kernel(const int32_t* ids, int32_t* out, int B, int L, int eos) {
+  const int bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= B) return;
+  const int32_t* r = ids + (size_t)bi * L;
+  int best = 0;
+  if (eos == 2) {  // legacy configs: argmax(ids) (first maximal position)
+    int mv = r[0];
+    for (int t = 1; t < L; ++t)
+      if (r[t] > mv) { mv = r[t]; best = t; }
+  } else {
+    for (int t = 0; t < L; ++t)
+      if (r[t] == eos) { best = t; break; }
+  }
+  out[bi] = best;
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void gather_ln_kernel(const float* x, const int32_t* idx, int L, const float* g,
+                                                        const float* b, float eps, bf16_t* out, float* out32,
+                                                        int B) {
+  const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (bi >= B) return;
+  constexpr int C = NV * 256;
+  const size_t row = (size_t)bi * L + (idx ? idx[bi] : 0);
+  float4 v[NV];
+  load_row<NV>(v, x + row * C, lane);
+  ln_row<NV>(v, g, b, eps, C, lane);
+  store_row<NV>(v, out32 ? out32 + (size_t)bi * C : nullptr, out ? out + (size_t)bi * C : nullptr, lane);
+}
+
+__global__ __launch_bounds__(256) void l2norm_kernel(float* x, int B, int C) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  float* r = x + (size_t)row * C;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += r[c] * r[c];
+  const float inv = 1.0f / sqrtf(wave_sum(s));
+  for (int c = lane; c < C; c += 64) r[c] *= inv;
+}
+
+}  // namespace
+
+hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd, const float* g, const float* b,
+                            float eps, float* y32, int ldy32, bf16_t* y16, int ldy16, int rows, int C,
+                            hipStream_t s) {
+  const dim3 grid((rows + 3) / 4);
+  if (C == 768)
+    hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, x, ldx, add, ldadd, g, b, eps, y32, ldy32, y16,
+                       ldy16, rows);
+  else if (C == 512)
+    hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, x, ldx, add, ldadd, g, b, eps, y32, ldy32, y16,
+                       ldy16, rows);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
+                                const float* g, const float* b, float eps, float* x, bf16_t* xb, int B, int L,
+                                int H, int pad_id, hipStream_t s) {
+  if (H != 768 || L > 512) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, x, xb, L,
+                     pad_id);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
+                                  const float* b, float eps, float* x, bf16_t* xb, int B, int L, int H,
+                                  hipStream_t s) {
+  if (H != 512) return hipErrorInvalidValue;
+  const int rows = B * L;
+  hipLaunchKernelGGL(clip_text_embed_kernel<2>, dim3((rows + 3) / 4), dim3(256), 0, s, ids, tok, pos, g, b, eps, x,
+                     xb, rows, L);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_im2col(const uint8_t* img, bf16_t* A, int B, hipStream_t s) {
+  const size_t total = (size_t)B * 49 * 384;
+  hipLaunchKernelGGL(clip_im2col_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, img, A, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
+                                       const float* pre_g, const float* pre_b, const float* ln1_g,
+                                       const float* ln1_b, float eps, float* x, bf16_t* xb, int B,
+                                       hipStream_t s) {
+  const int rows = B * 50;
+  hipLaunchKernelGGL(clip_vision_assemble_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, patches, cls, pos, pre_g,
+                     pre_b, ln1_g, ln1_b, eps, x, xb, rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int eos_id, hipStream_t s) {
+  hipLaunchKernelGGL(eos_index_kernel, dim3((B + 255) / 256), dim3(256), 0, s, ids, out, B, L, eos_id);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const float* g, const float* b, float eps,
+                            bf16_t* out, float* out32, int B, int C, hipStream_t s) {
+  const dim3 grid((B + 3) / 4);
+  if (C == 768)
+    hipLaunchKernelGGL(gather_ln_kernel<3>, grid, dim3(256), 0, s, x, idx, L, g, b, eps, out, out32, B);
+  else if (C == 512)
+    hipLaunchKernelGGL(gather_ln_kernel<2>, grid, dim3(256), 0, s, x, idx, L, g, b, eps, out, out32, B);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s) {
+  hipLaunchKernelGGL(l2norm_kernel, dim3((B + 3) / 4), dim3(256), 0, s, x, B, C);
+  return hipGetLastError();
+}

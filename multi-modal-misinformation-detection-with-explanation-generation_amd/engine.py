@@ -1,0 +1,176 @@
+"""Per-device engine: owns one libmmf_hip handle (weights, workspaces, Truth-Vault) and exposes
+the five signals as batched tensor calls on torch device tensors (torch = device memory and
+streams only; all arithmetic runs in the HIP kernels of libmmf_hip.so)."""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import hip
+from .hip import check, ptr, stream_ptr
+
+SCORE_KEYS = ("ai_score", "misinfo_score", "deepfake_score", "clip_similarity", "vault_discrepancy")
+
+
+def _as_np(v) -> np.ndarray:
+    if isinstance(v, torch.Tensor):
+        v = v.detach().cpu()
+        return v.numpy() if v.dtype == torch.int64 else v.float().numpy()
+    return np.asarray(v)
+
+
+class Engine:
+    """MI355X replica of the MisinfoForensics models on one device."""
+
+    def __init__(self, device: int = 0, detector_state=None, clip_state=None, eos_token_id: int = 49407,
+                 max_batch: int = 256, max_text_len: int = 128, max_clip_len: int = 77):
+        self.lib = hip.load()
+        self.device = torch.device("cuda", device)
+        torch.cuda.set_device(self.device)
+        h = ctypes.c_void_p()
+        check(self.lib.mmf_create(device, ctypes.byref(h)), "mmf_create")
+        self.h = h
+        self.eos_token_id = eos_token_id
+        if detector_state is not None:
+            self.load_state(detector_state, "")
+        if clip_state is not None:
+            self.load_state(clip_state, "clip.")
+        self.finalize()
+        self.reserve(max_batch, max_text_len, max_clip_len)
+        self.vault_n = 0
+
+    # ------------------------------------------------------------------ weights
+    def load_state(self, state: Dict, prefix: str = "") -> None:
+        for name, v in state.items():
+            a = _as_np(v)
+            if a.dtype == np.int64:
+                dt = 1
+            else:
+                a = np.ascontiguousarray(a, dtype=np.float32)
+                dt = 0
+            shape = (ctypes.c_int64 * max(1, a.ndim))(*a.shape)
+            check(self.lib.mmf_load_tensor(self.h, (prefix + name).encode(), dt, a.ndim, shape,
+                                           a.ctypes.data_as(ctypes.c_void_p)), f"load {prefix + name}")
+
+    def finalize(self) -> None:
+        check(self.lib.mmf_finalize(self.h, int(self.eos_token_id)), "mmf_finalize")
+
+    @property
+    def ready(self) -> int:
+        return self.lib.mmf_ready(self.h)
+
+    def reserve(self, max_batch: int, max_text_len: int = 128, max_clip_len: int = 77) -> None:
+        check(self.lib.mmf_reserve(self.h, max_batch, max_text_len, max_clip_len), "mmf_reserve")
+        self.max_batch, self.max_text_len, self.max_clip_len = max_batch, max_text_len, max_clip_len
+
+    # ------------------------------------------------------------------ vault
+    def set_vault(self, embeddings: np.ndarray, title_ids=None, title_mask=None) -> None:
+        v = np.ascontiguousarray(_as_np(embeddings), dtype=np.float32)
+        check(self.lib.mmf_set_vault(self.h, v.ctypes.data_as(ctypes.c_void_p), v.shape[0], v.shape[1]),
+              "mmf_set_vault")
+        self.vault_n = v.shape[0]
+        if title_ids is not None:
+            ids = self._i32(title_ids)
+            mask = self._i32(title_mask)
+            check(self.lib.mmf_set_vault_titles(self.h, ptr(ids), ptr(mask), ids.shape[0], ids.shape[1],
+                                                stream_ptr()), "mmf_set_vault_titles")
+
+    # ------------------------------------------------------------------ helpers
+    def _i32(self, x) -> torch.Tensor:
+        t = torch.as_tensor(x)
+        return t.to(self.device, torch.int32).contiguous()
+
+    def _u8(self, x) -> torch.Tensor:
+        t = torch.as_tensor(x)
+        assert t.dtype == torch.uint8 and t.dim() == 4 and tuple(t.shape[1:]) == (224, 224, 3), \
+            f"images must be uint8 [B,224,224,3], got {tuple(t.shape)} {t.dtype}"
+        return t.to(self.device).contiguous()
+
+    def _f32(self, *shape) -> torch.Tensor:
+        return torch.empty(shape, dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ signals
+    def text_forward(self, ids, mask):
+        ids, mask = self._i32(ids), self._i32(mask)
+        B, L = ids.shape
+        ai, mi, sc = self._f32(B, 2), self._f32(B, 2), self._f32(B, 2)
+        check(self.lib.mmf_text_forward(self.h, ptr(ids), ptr(mask), B, L, ptr(ai), ptr(mi), ptr(sc),
+                                        stream_ptr()), "mmf_text_forward")
+        return ai, mi, sc
+
+    def effnet_forward(self, img):
+        img = self._u8(img)
+        B = img.shape[0]
+        lg, sc = self._f32(B, 2), self._f32(B)
+        check(self.lib.mmf_effnet_forward(self.h, ptr(img), B, ptr(lg), ptr(sc), stream_ptr()), "mmf_effnet_forward")
+        return lg, sc
+
+    def clip_image(self, img):
+        img = self._u8(img)
+        e = self._f32(img.shape[0], 512)
+        check(self.lib.mmf_clip_image(self.h, ptr(img), img.shape[0], ptr(e), stream_ptr()), "mmf_clip_image")
+        return e
+
+    def clip_text(self, ids, mask):
+        ids, mask = self._i32(ids), self._i32(mask)
+        e = self._f32(ids.shape[0], 512)
+        check(self.lib.mmf_clip_text(self.h, ptr(ids), ptr(mask), ids.shape[0], ids.shape[1], ptr(e),
+                                     stream_ptr()), "mmf_clip_text")
+        return e
+
+    def vault_topk(self, q_unit: torch.Tensor, k: int = 5, thresh: float = 0.85, text_emb=None):
+        q = q_unit.contiguous()
+        B = q.shape[0]
+        sims, idx = self._f32(B, k), torch.empty((B, k), dtype=torch.int32, device=self.device)
+        disc, tsim = self._f32(B), self._f32(B)
+        check(self.lib.mmf_vault_topk(self.h, ptr(q), B, k, float(thresh), ptr(sims), ptr(idx), ptr(disc),
+                                      ptr(text_emb), ptr(tsim), stream_ptr()), "mmf_vault_topk")
+        return sims, idx, disc, tsim
+
+    def fusion(self, x5):
+        x5 = torch.as_tensor(x5, dtype=torch.float32).to(self.device).contiguous()
+        B = x5.shape[0]
+        probs, conf = self._f32(B, 2), self._f32(B)
+        verdict = torch.empty(B, dtype=torch.int32, device=self.device)
+        rule = torch.empty(B, dtype=torch.int32, device=self.device)
+        check(self.lib.mmf_fusion(self.h, ptr(x5), B, ptr(probs), ptr(verdict), ptr(conf), ptr(rule), stream_ptr()),
+              "mmf_fusion")
+        return probs, verdict, conf, rule
+
+    def analyze_batch(self, rob_ids, rob_mask, clip_ids, clip_mask, img, img_clip=None,
+                      out: Optional[dict] = None) -> dict:
+        """Text+image pairs through all five signals + fusion (misinfo_forensics.py:767-927)."""
+        rob_ids, rob_mask = self._i32(rob_ids), self._i32(rob_mask)
+        clip_ids, clip_mask = self._i32(clip_ids), self._i32(clip_mask)
+        img = self._u8(img)
+        img_clip = self._u8(img_clip) if img_clip is not None else None
+        B = rob_ids.shape[0]
+        if out is None:
+            out = self.alloc_outputs(B)
+        check(self.lib.mmf_analyze_batch(
+            self.h, ptr(rob_ids), ptr(rob_mask), rob_ids.shape[1], ptr(clip_ids), ptr(clip_mask), clip_ids.shape[1],
+            ptr(img), ptr(img_clip), B, ptr(out["scores"]), ptr(out["text_similarity"]), ptr(out["probs"]),
+            ptr(out["verdict"]), ptr(out["confidence"]), ptr(out["rule"]), ptr(out["top_sims"]),
+            ptr(out["top_idx"]), stream_ptr()), "mmf_analyze_batch")
+        return out
+
+    def alloc_outputs(self, B: int) -> dict:
+        d = self.device
+        return {"scores": self._f32(B, 5), "text_similarity": self._f32(B), "probs": self._f32(B, 2),
+                "verdict": torch.empty(B, dtype=torch.int32, device=d), "confidence": self._f32(B),
+                "rule": torch.empty(B, dtype=torch.int32, device=d), "top_sims": self._f32(B, 5),
+                "top_idx": torch.empty((B, 5), dtype=torch.int32, device=d)}
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.mmf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

@@ -1,0 +1,94 @@
+"""End-to-end parity of the HIP path (through the C-ABI) against the reference-generated golden
+fixtures and the fp32 CPU oracle.  Tolerance (BASELINE.json north_star): the 5-score vector and
+the fusion probabilities within 1e-3 of the fp32 reference; verdicts equal."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-3
+
+
+@pytest.fixture(scope="module")
+def engine(det_sd, clip_sd, golden, golden_inputs):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from mmf_amd.engine import Engine
+    eng = Engine(0, det_sd, clip_sd, eos_token_id=golden_inputs["eos"], max_batch=256)
+    assert eng.ready == 31
+    gi = golden_inputs
+    tmask = np.zeros((2170, 77), np.int32)
+    for j, t in enumerate(gi["title_ids"]):
+        tmask[j, :len(t)] = 1
+    eng.set_vault(gi["vault"], golden["title_clip_ids"], tmask)
+    assert eng.ready == 63
+    return eng
+
+
+def _sm1(lg):
+    return torch.softmax(torch.as_tensor(lg, dtype=torch.float32), 1)[:, 1].numpy()
+
+
+def test_text_signals(engine, golden):
+    ai, mi, sc = engine.text_forward(golden["rob_ids"], golden["rob_mask"])
+    torch.cuda.synchronize()
+    sc = sc.cpu().numpy()
+    np.testing.assert_allclose(sc[:, 0], _sm1(golden["ai_logits"]), atol=TOL)
+    np.testing.assert_allclose(sc[:, 1], _sm1(golden["misinfo_logits"]), atol=TOL)
+    np.testing.assert_allclose(ai.cpu().numpy(), golden["ai_logits"], atol=5e-3)
+
+
+def test_effnet_signal(engine, golden, golden_inputs):
+    lg, sc = engine.effnet_forward(golden_inputs["imgs"])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(sc.cpu().numpy(), _sm1(golden["effnet_logits"]), atol=TOL)
+
+
+def test_clip_embeddings(engine, golden, golden_inputs):
+    ie = engine.clip_image(golden_inputs["imgs"]).cpu().numpy()
+    te = engine.clip_text(golden["clip_ids"], golden["clip_mask"]).cpu().numpy()
+    # unit vectors: compare directions
+    assert (ie * golden["clip_image_embeds"]).sum(1).min() > 1 - 1e-4
+    assert (te * golden["clip_text_embeds"]).sum(1).min() > 1 - 1e-4
+    np.testing.assert_allclose((ie * te).sum(1), golden["clip_similarity"], atol=TOL)
+
+
+def test_analyze_batch_vs_golden(engine, golden, golden_inputs):
+    out = engine.analyze_batch(golden["rob_ids"], golden["rob_mask"], golden["clip_ids"], golden["clip_mask"],
+                               golden_inputs["imgs"])
+    torch.cuda.synchronize()
+    o = {k: v.cpu().numpy() for k, v in out.items()}
+    np.testing.assert_allclose(o["scores"], golden["scores"], atol=TOL)
+    np.testing.assert_allclose(o["probs"], golden["fusion_probs"], atol=TOL)
+    np.testing.assert_array_equal(o["verdict"], (golden["fusion_probs"][:, 1] > 0.5).astype(np.int32))
+    np.testing.assert_array_equal(o["top_idx"], golden["vault_top_idx"])
+    np.testing.assert_allclose(o["top_sims"], golden["vault_top_sim"], atol=TOL)
+    np.testing.assert_allclose(o["text_similarity"], golden["text_similarity"], atol=TOL)
+
+
+def test_fusion_config1(engine, golden):
+    probs, verdict, conf, rule = engine.fusion(golden["fusion_c1_inputs"])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(probs.cpu().numpy(), golden["fusion_c1_probs"], atol=1e-5)
+    p = golden["fusion_c1_probs"]
+    np.testing.assert_array_equal(verdict.cpu().numpy(), (p[:, 1] > 0.5).astype(np.int32))
+
+
+def test_batch_invariance_full_size(engine, det_sd):
+    """B=256, L=128 (the benchmark workload): every row is bit-identical to the same row run in a
+    batch of 8 -> sharding rows over GPUs cannot change results."""
+    import mmf_amd.synthetic as syn
+    B = 256
+    rid, rm = syn.roberta_ids(B, 128, 5)
+    cid, cm = syn.clip_ids(B, 77, 5)
+    imgs = syn.images(B, 5)
+    full = engine.analyze_batch(rid, rm, cid, cm, imgs)
+    part = engine.analyze_batch(rid[40:48], rm[40:48], cid[40:48], cm[40:48], imgs[40:48])
+    torch.cuda.synchronize()
+    for k in ("scores", "probs", "top_sims", "top_idx", "text_similarity"):
+        a, b = full[k].cpu().numpy(), part[k].cpu().numpy()
+        assert np.isfinite(a).all()
+        np.testing.assert_array_equal(a[40:48], b, err_msg=k)
+    s = full["scores"].cpu().numpy()
+    assert ((s[:, :3] >= 0) & (s[:, :3] <= 1)).all() and (np.abs(s[:, 3]) <= 1 + 1e-5).all()
