@@ -154,14 +154,14 @@ int dev_alloc(mmf_handle* h, void** p, size_t bytes, bool workspace = false) {
 
 // ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
 enum ProfKind {
-  PK_GEMM0 = 0, PK_GEMM1, PK_GEMM2, PK_GEMM3, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
+  PK_GEMM0 = 0, PK_GEMM_LAST = 7, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
   PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
 };
 const char* prof_kind_name(int k) {
-  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, "attention", "layernorm",
-                                        "embed+ln", "clip_im2col", "effnet_stem", "dwconv", "se", "gap_classifier",
-                                        "text_heads", "vault", "fusion"};
-  if (k >= 0 && k < 4) return gemm_config_name(k);
+  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                        "attention", "layernorm", "embed+ln", "clip_im2col", "effnet_stem",
+                                        "dwconv", "se", "gap_classifier", "text_heads", "vault", "fusion"};
+  if (k >= 0 && k <= PK_GEMM_LAST) return gemm_config_name(k);
   return (k >= 0 && k < PK_COUNT) ? names[k] : "?";
 }
 
@@ -345,7 +345,10 @@ int finalize_effnet(mmf_handle* h) {
       const std::string se = bp + std::to_string(i + 1) + ".";
       CHK(load_f32(h, &B.w1, se + "fc1.weight", (size_t)B.csq * B.cexp));
       CHK(load_f32(h, &B.b1, se + "fc1.bias", B.csq));
-      CHK(load_f32(h, &B.w2, se + "fc2.weight", (size_t)B.cexp * B.csq));
+      {
+        GET(w2, se + "fc2.weight", (size_t)B.cexp * B.csq);
+        CHK(up_f32(h, &B.w2, transpose(w2->f, B.cexp, B.csq)));  // [csq][cexp] for coalesced fc2
+      }
       CHK(load_f32(h, &B.b2, se + "fc2.bias", B.cexp));
       CHK(fold_bn(h, bp + std::to_string(i + 2) + ".0", bp + std::to_string(i + 2) + ".1", B.cout, B.cexp, &w, &b));
       CHK(up_bf16(h, &B.p.w, w));

@@ -13,45 +13,55 @@
 
 namespace {
 
+// One thread per output pixel, all 32 channels; weights transposed in LDS to [tap][channel] so
+// every tap is 8 broadcast float4 reads.  ToTensor + Normalize folded into one FMA per input.
 __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* img, const float* w, const float* bias,
                                                    bf16_t* out, int B) {
-  __shared__ float sw[32 * 27];
-  __shared__ float sb[32];
-  for (int i = threadIdx.x; i < 32 * 27; i += 256) sw[i] = w[i];
+  __shared__ __attribute__((aligned(16))) float sw[27 * 32];
+  __shared__ __attribute__((aligned(16))) float sb[32];
+  for (int i = threadIdx.x; i < 32 * 27; i += 256) sw[(i % 27) * 32 + i / 27] = w[i];
   if (threadIdx.x < 32) sb[threadIdx.x] = bias[threadIdx.x];
   __syncthreads();
-  const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= (size_t)B * 112 * 112 * 4) return;
-  const int cg = gid & 3;
-  const size_t pix = gid >> 2;
+  const size_t pix = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (size_t)B * 112 * 112) return;
   const int ox = pix % 112, oy = (pix / 112) % 112, bi = pix / (112 * 112);
-  const float mean[3] = {0.485f, 0.456f, 0.406f};
-  const float stdv[3] = {0.229f, 0.224f, 0.225f};
-  float in[27];
+  // (u/255 - mean)/std == u * (1/(255 std)) + (-mean/std)
+  const float sc[3] = {1.0f / (255.0f * 0.229f), 1.0f / (255.0f * 0.224f), 1.0f / (255.0f * 0.225f)};
+  const float of[3] = {-0.485f / 0.229f, -0.456f / 0.224f, -0.406f / 0.225f};
+  float acc[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) acc[j] = sb[j];
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky) {
     const int iy = oy * 2 - 1 + ky;
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
       const int ix = ox * 2 - 1 + kx;
-      const bool ok = iy >= 0 && iy < 224 && ix >= 0 && ix < 224;
-      const uint8_t* p = img + (((size_t)bi * 224 + (ok ? iy : 0)) * 224 + (ok ? ix : 0)) * 3;
+      if (iy < 0 || iy >= 224 || ix < 0 || ix >= 224) continue;  // zero padding (normalised space)
+      const uint8_t* p = img + (((size_t)bi * 224 + iy) * 224 + ix) * 3;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        in[c * 9 + ky * 3 + kx] = ok ? ((float)p[c] / 255.0f - mean[c]) / stdv[c] : 0.f;
+      for (int c = 0; c < 3; ++c) {
+        const float v = fmaf((float)p[c], sc[c], of[c]);
+        const float4* wr = reinterpret_cast<const float4*>(sw + (c * 9 + ky * 3 + kx) * 32);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float4 ww = wr[q];
+          acc[q * 4 + 0] = fmaf(ww.x, v, acc[q * 4 + 0]);
+          acc[q * 4 + 1] = fmaf(ww.y, v, acc[q * 4 + 1]);
+          acc[q * 4 + 2] = fmaf(ww.z, v, acc[q * 4 + 2]);
+          acc[q * 4 + 3] = fmaf(ww.w, v, acc[q * 4 + 3]);
+        }
+      }
     }
   }
-  float o[8];
+  uint4* dst = reinterpret_cast<uint4*>(out + pix * 32);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int co = cg * 8 + j;
-    float a = sb[co];
+  for (int q = 0; q < 4; ++q) {
+    float o[8];
 #pragma unroll
-    for (int t = 0; t < 27; ++t) a = fmaf(sw[co * 27 + t], in[t], a);
-    o[j] = act_apply(a, ACT_SILU);
+    for (int j = 0; j < 8; ++j) o[j] = act_apply(acc[q * 8 + j], ACT_SILU);
+    dst[q] = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
   }
-  *reinterpret_cast<uint4*>(out + pix * 32 + cg * 8) =
-      make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
 }
 
 // grid (chunks, C/8/CGT, B); block = PL pixel lanes x CGT channel groups of 8
@@ -122,28 +132,37 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* in, const flo
   }
 }
 
+// One block per image.  w2t is fc2's weight transposed to [Csq][C] (packed at load) so every
+// k-step of both matvecs is one coalesced row read; fc1 partial dots are spread over all waves.
 __global__ __launch_bounds__(256) void se_kernel(const float* pool_part, int nchunks, float inv_hw, const float* w1,
-                                                 const float* b1, const float* w2, const float* b2, float* scale,
+                                                 const float* b1, const float* w2t, const float* b2, float* scale,
                                                  int C, int Csq) {
   __shared__ float pooled[1280];
   __shared__ float s1[64];
   const int bi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* pp = pool_part + (size_t)bi * nchunks * C;
   for (int c = tid; c < C; c += 256) {
     float s = 0.f;
-    for (int k = 0; k < nchunks; ++k) s += pool_part[((size_t)bi * nchunks + k) * C + c];
+    for (int k = 0; k < nchunks; ++k) s += pp[(size_t)k * C + c];
     pooled[c] = s * inv_hw;
   }
   __syncthreads();
   for (int o = wave; o < Csq; o += 4) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a = fmaf(w1[(size_t)o * C + c], pooled[c], a);
-    a = wave_sum(a);
+    const float* wr = w1 + (size_t)o * C;
+    float a0 = 0.f, a1 = 0.f;
+    int c = lane;
+    for (; c + 64 < C; c += 128) {
+      a0 = fmaf(wr[c], pooled[c], a0);
+      a1 = fmaf(wr[c + 64], pooled[c + 64], a1);
+    }
+    if (c < C) a0 = fmaf(wr[c], pooled[c], a0);
+    const float a = wave_sum(a0 + a1);
     if (lane == 0) s1[o] = act_apply(a + b1[o], ACT_SILU);
   }
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
     float a = b2[c];
-    for (int j = 0; j < Csq; ++j) a = fmaf(w2[(size_t)c * Csq + j], s1[j], a);
+    for (int j = 0; j < Csq; ++j) a = fmaf(w2t[(size_t)j * C + c], s1[j], a);
     scale[(size_t)bi * C + c] = 1.0f / (1.0f + expf(-a));
   }
 }
@@ -181,7 +200,7 @@ __global__ __launch_bounds__(256) void gap_classifier_kernel(const bf16_t* x, in
 
 hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, bf16_t* out, int B,
                               hipStream_t s) {
-  const size_t total = (size_t)B * 112 * 112 * 4;
+  const size_t total = (size_t)B * 112 * 112;
   hipLaunchKernelGGL(stem_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, img, w, bias, out, B);
   return hipGetLastError();
 }

@@ -166,6 +166,140 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large-tile kernel for the encoder GEMMs (K % 64 == 0): 512 threads = 8 waves, 256-row tiles,
+// operands staged HBM/L2 -> LDS directly with global_load_lds_dwordx4 (no VGPR round trip, no
+// ds_write).  The LDS image keeps the same XOR swizzle as above; because an LDS-DMA writes
+// lane-linearly (base + 16*lane), the swizzle is applied to each lane's SOURCE address instead.
+// Two LDS stages: the next K-tile's DMA is in flight while the current one feeds the MFMAs.
+// ---------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int ROWS>
+MMF_DEV void glds_tile(const bf16_t* __restrict__ G, int ld, int row0, int rowmax, int k0, bf16_t* tile, int wave,
+                       int lane) {
+  constexpr int PER_WAVE = ROWS / 64;  // 1-KB segments (8 rows x 128 B) per wave
+#pragma unroll
+  for (int j = 0; j < PER_WAVE; ++j) {
+    const int seg = wave * PER_WAVE + j;
+    const int r = seg * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (lane >> 3);  // logical chunk stored at physical slot (lane & 7) of row r
+    int grow = row0 + r;
+    grow = grow < rowmax ? grow : rowmax - 1;  // clamped rows are loaded but never stored
+    const bf16_t* src = G + (size_t)grow * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (lds_void_t*)((__attribute__((address_space(3))) bf16_t*)tile + seg * 512),
+                                     16, 0, 0);
+  }
+}
+
+template <int BN, int WGM, int WGN>
+__global__ __launch_bounds__(512) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles) {
+  // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
+  // K-slab of the NEXT tile is DMA'd into the free LDS stage during the current tile's last
+  // K-step, so only the very first tile pays the load latency and each epilogue's stores drain
+  // underneath the next tile's first MFMAs.
+  constexpr int BM = 256;
+  constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
+  constexpr int STAGE = (BM + BN) * BK;
+  static_assert(WGM * WGN == 8, "8 waves");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int M = g.M, N = g.N;
+  const int nk = g.K / BK;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  int t = wgid;
+  if (t >= tiles) return;
+  auto stage = [&](int buf, int tile, int kt) {
+    const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
+    bf16_t* nb = lds + buf * STAGE;
+    glds_tile<BM>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
+    glds_tile<BN>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
+  };
+  stage(0, t, 0);
+  __syncthreads();
+  int cur = 0;
+  for (; t < tiles; t += nwg) {
+    const int tm = t / tilesN, tn = t - tm * tilesN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    f32x4 acc[NI][MI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
+      else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
+      const bf16_t* Xs = lds + cur * STAGE;
+      const bf16_t* Ws = Xs + BM * BK;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 wf[NI], xf[MI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          wf[i] = as_bf16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
+#pragma unroll
+        for (int j = 0; j < MI; ++j)
+          xf[j] = as_bf16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+      }
+      __syncthreads();  // vmcnt(0): next stage landed; all reads of `cur` done before it is refilled
+      cur ^= 1;
+    }
+
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+      const int m = m0 + wm * TM + j * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int n = n0 + wn * TN + i * 16 + fg * 4;
+        if (n >= N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (g.bias) {
+          const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        if (g.act) {
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], g.act);
+        }
+        if (g.res32) {
+          const float4 rr = *reinterpret_cast<const float4*>(g.res32 + (size_t)m * g.ldr + n);
+          v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+        } else if (g.res16) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(g.res16 + (size_t)m * g.ldr + n);
+          v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
+        }
+        if (g.c32) *reinterpret_cast<float4*>(g.c32 + (size_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        if (g.c16)
+          *reinterpret_cast<uint2*>(g.c16 + (size_t)m * g.ldc + n) =
+              make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
+    }
+  }
+}
+
+template <int BN, int WGM, int WGN>
+hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
+  const int tilesM = (a.M + 255) / 256, tilesN = (a.N + BN - 1) / BN;
+  const int tiles = tilesM * tilesN;
+  const int grid = tiles < 256 ? tiles : 256;
+  hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WGM, int WGN>
 hipError_t run(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
@@ -175,17 +309,44 @@ hipError_t run(const GemmArgs& a, hipStream_t s) {
 
 }  // namespace
 
+static int forced_config(const GemmArgs& a) {
+  // MMF_GEMM_CONFIG=<n>: benchmarking override (tools/gemm_bench.py); ignored if inapplicable
+  const char* e = getenv("MMF_GEMM_CONFIG");
+  if (!e || !*e) return -1;
+  const int c = atoi(e);
+  if (c >= 4 && ((a.K % BK) || a.ascale)) return -1;
+  return (c >= 0 && c <= 6) ? c : -1;
+}
+
 int gemm_config(const GemmArgs& a) {
+  const int f = forced_config(a);
+  if (f >= 0) return f;
   if (a.N <= 32) return 0;
   if (a.N <= 64) return 1;
   if (a.M <= 512) return 2;  // skinny-M (projections, M = batch)
+  if ((a.K % BK) == 0 && !a.ascale && a.N >= 128) {
+    // persistent 256-row LDS-DMA tiles: pick the column tile that minimises whole "rounds" of
+    // 256 CUs x per-tile time (wider tiles are more efficient per flop)
+    const long tm = (a.M + 255) / 256;
+    const int bns[3] = {256, 192, 128}, cfg[3] = {4, 6, 5};
+    const double eff[3] = {1.0, 0.97, 0.88};
+    int best = 4;
+    double bc = 1e30;
+    for (int i = 0; i < 3; ++i) {
+      const long tiles = tm * ((a.N + bns[i] - 1) / bns[i]);
+      const double c = (double)((tiles + 255) / 256) * bns[i] / eff[i];
+      if (c < bc) { bc = c; best = cfg[i]; }
+    }
+    return best;
+  }
   return 3;
 }
 
 const char* gemm_config_name(int c) {
-  static const char* names[] = {"gemm_bf16<256,32,4,1>", "gemm_bf16<256,64,4,1>", "gemm_bf16<64,128,1,4>",
-                                "gemm_bf16<128,128,2,2>"};
-  return (c >= 0 && c < 4) ? names[c] : "gemm_bf16<?>";
+  static const char* names[] = {"gemm_bf16<256,32,4,1>",  "gemm_bf16<256,64,4,1>",  "gemm_bf16<64,128,1,4>",
+                                "gemm_bf16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
+                                "gemm_glds<256,192,4,2>"};
+  return (c >= 0 && c < 7) ? names[c] : "gemm_bf16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
@@ -195,6 +356,9 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);
     case 2: return run<64, 128, 1, 4>(a, s);
+    case 4: return run_glds<256, 2, 4>(a, s);
+    case 5: return run_glds<128, 4, 2>(a, s);
+    case 6: return run_glds<192, 4, 2>(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

@@ -103,8 +103,11 @@ def roberta_spec(prefix: str = "") -> "OrderedDict":
 def effnet_spec(prefix: str = "", num_classes: int = 2) -> "OrderedDict":
     d: OrderedDict = OrderedDict()
 
+    # Conv init N(0, (1.3^2)/fan_in): between torchvision's kaiming fan_out init (the random
+    # network collapses to an input-independent output) and He fan_in (chaotic: any rounding is
+    # amplified to O(1e-2) in the deepfake score).  See DESIGN.md "Numerics".
     def conv(name, cout, cin_g, k):
-        d[f"{name}.weight"] = ((cout, cin_g, k, k), ("he", cin_g * k * k))
+        d[f"{name}.weight"] = ((cout, cin_g, k, k), ("he", cin_g * k * k, 1.3))
 
     conv(f"{prefix}features.0.0", EFFNET_STEM, 3, 3)
     _bn(d, f"{prefix}features.0.1", EFFNET_STEM)
@@ -127,7 +130,7 @@ def effnet_spec(prefix: str = "", num_classes: int = 2) -> "OrderedDict":
         _bn(d, f"{p}.{i}.1", b["cout"])
     conv(f"{prefix}features.8.0", EFFNET_LAST, 320, 1)
     _bn(d, f"{prefix}features.8.1", EFFNET_LAST)
-    _lin(d, f"{prefix}classifier.1", num_classes, EFFNET_LAST, 0.02, bstd=0.05)
+    _lin(d, f"{prefix}classifier.1", num_classes, EFFNET_LAST, 0.1, bstd=0.05)
     return d
 
 
@@ -135,9 +138,12 @@ def detector_spec() -> "OrderedDict":
     """Full ``MultiModalMisinfoDetector`` state dict (misinfo_forensics.py:43-108)."""
     d: OrderedDict = OrderedDict()
     d.update(roberta_spec("roberta."))
+    # the heads are plain nn.Linear (misinfo_forensics.py:57-69): PyTorch's default init scale,
+    # U(+-1/sqrt(fan_in)) -> std 1/sqrt(3 fan_in), drawn here as a normal of that std
     for head in ("ai_head", "misinfo_head"):
-        _lin(d, f"{head}.0", 256, ROBERTA["hidden"], 0.05, bstd=0.05)
-        _lin(d, f"{head}.3", 2, 256, 0.05, bstd=0.05)
+        s0, s3 = 1 / math.sqrt(3 * ROBERTA["hidden"]), 1 / math.sqrt(3 * 256)
+        _lin(d, f"{head}.0", 256, ROBERTA["hidden"], s0, bstd=s0)
+        _lin(d, f"{head}.3", 2, 256, s3, bstd=s3)
     d.update(effnet_spec("efficientnet."))
     _lin(d, "fusion_layer.0", 64, 5, 0.5, bstd=0.1)
     _lin(d, "fusion_layer.3", 32, 64, 0.2, bstd=0.1)
@@ -202,8 +208,9 @@ def generate_tensor(name: str, shape: tuple, init: tuple, seed: int = 0) -> np.n
         x = g.standard_normal(n, dtype=np.float32) * np.float32(init[1])
     elif kind == "ones_jitter":
         x = 1.0 + g.standard_normal(n, dtype=np.float32) * np.float32(init[1])
-    elif kind == "he":
-        x = g.standard_normal(n, dtype=np.float32) * np.float32(math.sqrt(2.0 / init[1]))
+    elif kind == "he":  # ("he", fan_in[, gain]) -> N(0, gain^2 / fan_in), default gain sqrt(2)
+        gain = init[2] if len(init) > 2 else math.sqrt(2.0)
+        x = g.standard_normal(n, dtype=np.float32) * np.float32(gain / math.sqrt(init[1]))
     elif kind == "uniform":
         x = g.uniform(init[1], init[2], n).astype(np.float32)
     else:

@@ -35,6 +35,7 @@ def _act(x, act):
     (256, 768, 768, 0, False), (300, 200, 136, 1, True), (1000, 2304, 768, 0, False),
     (4096, 3072, 768, 1, False), (2048, 768, 3072, 0, True), (777, 24, 16, 3, False),
     (5000, 40, 144, 0, True), (12544, 96, 16, 3, False), (64, 512, 512, 0, False), (49 * 3, 1280, 320, 2, False),
+    (3000, 200, 128, 2, True), (2600, 1536, 512, 0, False), (1300, 392, 2048, 4, True),
 ])
 def test_gemm_vs_torch_fp32(lib, M, N, K, act, res):
     import mmf_amd.hip as hip

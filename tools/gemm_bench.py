@@ -1,0 +1,68 @@
+"""Micro-benchmark of libmmf_hip's bf16 GEMM on the encoder shapes of the hot path.
+
+    python tools/gemm_bench.py [--configs 3,4,5] [--iters 20]
+
+Prints TFLOP/s per (shape, tile config) measured with HIP events (torch.cuda.Event on the
+stream the kernel is launched on); MMF_GEMM_CONFIG forces the tile instantiation.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import mmf_amd.hip as hip  # noqa: E402
+
+# (name, M, N, K, act, out) at B=256: RoBERTa L=128, ViT L=50, CLIP text L=77
+SHAPES = [
+    ("rob_qkv", 32768, 2304, 768, 0, "16"), ("rob_o", 32768, 768, 768, 0, "32r"),
+    ("rob_fc1", 32768, 3072, 768, 1, "16"), ("rob_fc2", 32768, 768, 3072, 0, "32r"),
+    ("vit_qkv", 12800, 2304, 768, 0, "16"), ("vit_o", 12800, 768, 768, 0, "32r"),
+    ("vit_fc1", 12800, 3072, 768, 2, "16"), ("vit_fc2", 12800, 768, 3072, 0, "32r"),
+    ("txt_qkv", 19712, 1536, 512, 0, "16"), ("txt_o", 19712, 512, 512, 0, "32r"),
+    ("txt_fc1", 19712, 2048, 512, 2, "16"), ("txt_fc2", 19712, 512, 2048, 0, "32r"),
+    ("patch", 12544, 768, 3072, 0, "32"), ("sq4096", 4096, 4096, 4096, 0, "16"),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="auto,3,4,5,6")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    lib = hip.load()
+    dev = torch.device("cuda")
+    res = []
+    for name, M, N, K, act, out in SHAPES:
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        bias = torch.randn(N, device=dev)
+        c32 = torch.empty(M, N, device=dev) if "32" in out else None
+        c16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if "16" in out else None
+        R = torch.randn(M, N, device=dev) if "r" in out else None
+        row = {"shape": name, "M": M, "N": N, "K": K}
+        for cfg in a.configs.split(","):
+            os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
+
+            def call():
+                hip.check(lib.mmf_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R),
+                                            hip.ptr(c32), hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
+            for _ in range(3):
+                call()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                call()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            row[cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+        os.environ["MMF_GEMM_CONFIG"] = ""
+        res.append(row)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
