@@ -78,6 +78,11 @@ int mmf_text_forward(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
 int mmf_effnet_forward(mmf_handle* h, const uint8_t* img, int B, float* logits, float* deepfake_score,
                        void* stream);
 
+/* Same as mmf_effnet_forward for an already-normalised fp32 NCHW tensor x [B, 3, 224, 224] (the
+ * reference's detector.forward_image(image_tensor) signature, misinfo_forensics.py:102-104). */
+int mmf_effnet_forward_f32(mmf_handle* h, const float* x, int B, float* logits, float* deepfake_score,
+                           void* stream);
+
 /* CLIP image embedding — get_image_features + L2 normalisation (misinfo_forensics.py:395-401,
  * 432-439).  img uint8 [B, 224, 224, 3] (CLIP-preprocessed geometry); emb fp32 [B, 512] unit. */
 int mmf_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb_unit, void* stream);

@@ -583,14 +583,15 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
   return 0;
 }
 
-int run_effnet(mmf_handle* h, const uint8_t* img, int B, float* logits, float* score, int score_stride,
+int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score, int score_stride,
                hipStream_t s) {
   Workspace& w = h->ws;
   bf16_t* cur = w.e_a;
   bf16_t* nxt = w.e_b;
   {
     ProfScope ps(h, s, PK_STEM, 2.0 * B * 112 * 112 * 32 * 27, (double)B * (224 * 224 * 3 + 112 * 112 * 32 * 2));
-    HIPCHK(launch_effnet_stem(img, h->e_stem_w, h->e_stem_b, cur, B, s));
+    if (xf32) HIPCHK(launch_effnet_stem_f32(xf32, h->e_stem_w, h->e_stem_b, cur, B, s));
+    else HIPCHK(launch_effnet_stem(img, h->e_stem_w, h->e_stem_b, cur, B, s));
   }
   int H = 112, W = 112;
   for (const EffBlock& b : h->e_blocks) {
@@ -692,7 +693,7 @@ int mmf_finalize(mmf_handle* h, int clip_eos_token_id) {
   if (!h) return fail(MMF_EINVAL, "null handle");
   HIPCHK(hipSetDevice(h->device));
   h->eos_id = clip_eos_token_id;
-  int ready = h->ready & 32;
+  int ready = h->ready;  // incremental: components not re-staged keep their packed weights
   std::string missing;
   auto attempt = [&](int bit, const char* probe, int (*fn)(mmf_handle*)) -> int {
     if (!has(h, probe)) return 0;
@@ -795,7 +796,15 @@ int mmf_effnet_forward(mmf_handle* h, const uint8_t* img, int B, float* logits, 
   if (!(h->ready & 2)) return fail(MMF_EINVAL, "EfficientNet not loaded");
   CHK(check_cap(h, B, 1, 1));
   HIPCHK(hipSetDevice(h->device));
-  return run_effnet(h, img, B, logits, score, 1, (hipStream_t)stream);
+  return run_effnet(h, img, nullptr, B, logits, score, 1, (hipStream_t)stream);
+}
+
+int mmf_effnet_forward_f32(mmf_handle* h, const float* x, int B, float* logits, float* score, void* stream) {
+  if (!h || !x) return fail(MMF_EINVAL, "null argument");
+  if (!(h->ready & 2)) return fail(MMF_EINVAL, "EfficientNet not loaded");
+  CHK(check_cap(h, B, 1, 1));
+  HIPCHK(hipSetDevice(h->device));
+  return run_effnet(h, nullptr, x, B, logits, score, 1, (hipStream_t)stream);
 }
 
 int mmf_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, void* stream) {
@@ -889,7 +898,7 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   if (!img_clip) img_clip = img_eff;
   Workspace& w = h->ws;
   CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, s));
-  CHK(run_effnet(h, img_eff, B, nullptr, scores5 + 2, 5, s));
+  CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, s));
   CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
   CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, s));
   HIPCHK(launch_rowdot(w.v_emb, w.t_emb, scores5 + 3, 5, B, 512, s));

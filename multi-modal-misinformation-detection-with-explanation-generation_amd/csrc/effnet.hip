@@ -15,8 +15,13 @@ namespace {
 
 // One thread per output pixel, all 32 channels; weights transposed in LDS to [tap][channel] so
 // every tap is 8 broadcast float4 reads.  ToTensor + Normalize folded into one FMA per input.
-__global__ __launch_bounds__(256) void stem_kernel(const uint8_t* img, const float* w, const float* bias,
-                                                   bf16_t* out, int B) {
+// F32 = true: input is an already-normalised fp32 NCHW tensor (detector.forward_image signature,
+// misinfo_forensics.py:102-104) instead of uint8 HWC pixels.
+template <bool F32>
+__global__ __launch_bounds__(256) void stem_kernel(const void* src, const float* w, const float* bias, bf16_t* out,
+                                                   int B) {
+  const uint8_t* img = (const uint8_t*)src;
+  const float* xf = (const float*)src;
   __shared__ __attribute__((aligned(16))) float sw[27 * 32];
   __shared__ __attribute__((aligned(16))) float sb[32];
   for (int i = threadIdx.x; i < 32 * 27; i += 256) sw[(i % 27) * 32 + i / 27] = w[i];
@@ -41,7 +46,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* img, const flo
       const uint8_t* p = img + (((size_t)bi * 224 + iy) * 224 + ix) * 3;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float v = fmaf((float)p[c], sc[c], of[c]);
+        const float v = F32 ? xf[(((size_t)bi * 3 + c) * 224 + iy) * 224 + ix] : fmaf((float)p[c], sc[c], of[c]);
         const float4* wr = reinterpret_cast<const float4*>(sw + (c * 9 + ky * 3 + kx) * 32);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -201,7 +206,16 @@ __global__ __launch_bounds__(256) void gap_classifier_kernel(const bf16_t* x, in
 hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, bf16_t* out, int B,
                               hipStream_t s) {
   const size_t total = (size_t)B * 112 * 112;
-  hipLaunchKernelGGL(stem_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, img, w, bias, out, B);
+  hipLaunchKernelGGL(stem_kernel<false>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const void*)img, w,
+                     bias, out, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_effnet_stem_f32(const float* x, const float* w, const float* bias, bf16_t* out, int B,
+                                  hipStream_t s) {
+  const size_t total = (size_t)B * 112 * 112;
+  hipLaunchKernelGGL(stem_kernel<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const void*)x, w,
+                     bias, out, B);
   return hipGetLastError();
 }
 

@@ -77,6 +77,8 @@ hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, 
 // EfficientNet-B0 pieces (NHWC bf16 activations)
 hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, bf16_t* out, int B,
                               hipStream_t s);
+hipError_t launch_effnet_stem_f32(const float* x_nchw, const float* w, const float* bias, bf16_t* out, int B,
+                                  hipStream_t s);
 hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part,
                          int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s);
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,

@@ -108,6 +108,16 @@ class Engine:
         check(self.lib.mmf_effnet_forward(self.h, ptr(img), B, ptr(lg), ptr(sc), stream_ptr()), "mmf_effnet_forward")
         return lg, sc
 
+    def effnet_forward_f32(self, x):
+        """Normalised fp32 NCHW input (detector.forward_image semantics)."""
+        x = torch.as_tensor(x, dtype=torch.float32).to(self.device).contiguous()
+        assert x.dim() == 4 and tuple(x.shape[1:]) == (3, 224, 224), f"expected [B,3,224,224], got {tuple(x.shape)}"
+        B = x.shape[0]
+        lg, sc = self._f32(B, 2), self._f32(B)
+        check(self.lib.mmf_effnet_forward_f32(self.h, ptr(x), B, ptr(lg), ptr(sc), stream_ptr()),
+              "mmf_effnet_forward_f32")
+        return lg, sc
+
     def clip_image(self, img):
         img = self._u8(img)
         e = self._f32(img.shape[0], 512)

@@ -26,6 +26,7 @@ SIGNATURES = {
     "mmf_reserve": (_I, [_P, _I, _I, _I]),
     "mmf_text_forward": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P]),
     "mmf_effnet_forward": (_I, [_P, _P, _I, _P, _P, _P]),
+    "mmf_effnet_forward_f32": (_I, [_P, _P, _I, _P, _P, _P]),
     "mmf_clip_image": (_I, [_P, _P, _I, _P, _P]),
     "mmf_clip_text": (_I, [_P, _P, _P, _I, _I, _P, _P]),
     "mmf_set_vault": (_I, [_P, _P, _I, _I]),

@@ -1,0 +1,133 @@
+"""Host-side input handling for the drop-in API: image loading/geometry, tokenisation calls and the
+Truth-Vault file format.  Arithmetic (normalisation, every model) stays on the GPU: images cross
+the boundary as uint8 HWC pixels, text as int32 token ids.
+"""
+from __future__ import annotations
+
+import io
+import os
+import pickle
+from typing import List, Optional, Tuple, Union
+
+import numpy as np
+
+try:
+    from PIL import Image
+except Exception:  # noqa: BLE001
+    Image = None
+
+
+def to_pil(image_or_path):
+    """misinfo_forensics.py:255-258 (_to_pil_image)."""
+    if Image is not None and isinstance(image_or_path, Image.Image):
+        return image_or_path.convert("RGB")
+    return Image.open(str(image_or_path)).convert("RGB")
+
+
+def effnet_pixels(img) -> np.ndarray:
+    """EfficientNet geometry (misinfo_forensics.py:249-253): Resize((224, 224)) bilinear on the PIL
+    image (torchvision's PIL path); ToTensor/Normalize happen in the stem kernel."""
+    if img.size != (224, 224):
+        img = img.resize((224, 224), Image.BILINEAR)
+    return np.asarray(img, dtype=np.uint8)
+
+
+def clip_pixels(img) -> np.ndarray:
+    """CLIPImageProcessor geometry: shortest edge -> 224 (bicubic), centre crop 224x224.  Rescale and
+    the OpenAI mean/std normalisation happen in the patch-embedding kernel."""
+    w, h = img.size
+    if (w, h) != (224, 224):
+        short, long_ = (w, h) if w <= h else (h, w)
+        new_long = int(224 * long_ / short)
+        nw, nh = (224, new_long) if w <= h else (new_long, 224)
+        img = img.resize((nw, nh), Image.BICUBIC)
+        top, left = (nh - 224) // 2, (nw - 224) // 2
+        img = img.crop((left, top, left + 224, top + 224))
+    return np.asarray(img, dtype=np.uint8)
+
+
+def pad_ids(seqs: List[List[int]], pad_id: int, length: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+    L = length or max(len(s) for s in seqs)
+    ids = np.full((len(seqs), L), pad_id, dtype=np.int32)
+    mask = np.zeros((len(seqs), L), dtype=np.int32)
+    for i, s in enumerate(seqs):
+        n = min(len(s), L)
+        ids[i, :n] = s[:n]
+        mask[i, :n] = 1
+    return ids, mask
+
+
+def _to_list(x):
+    if hasattr(x, "tolist"):
+        x = x.tolist()
+    return [int(v) for v in x]
+
+
+def tokenize_roberta(tok, text: str) -> List[int]:
+    """analyze_text tokenisation (misinfo_forensics.py:327-333)."""
+    enc = tok(text, return_tensors="pt", max_length=512, truncation=True, padding=True)
+    ids = enc["input_ids"]
+    if (hasattr(ids, "dim") and ids.dim() == 2) or (isinstance(ids, (list, tuple)) and isinstance(ids[0], (list, tuple))):
+        ids = ids[0]
+    return _to_list(ids)
+
+
+def tokenize_clip(proc, texts: List[str], truncation: bool = False) -> List[List[int]]:
+    """CLIPProcessor text tokenisation (misinfo_forensics.py:386-391, 473-478); returns the unpadded
+    id lists (padding ids never influence the causal EOS-pooled embedding)."""
+    kw = dict(text=list(texts), return_tensors="pt", padding=True)
+    if truncation:
+        kw["truncation"] = True
+    enc = proc(**kw)
+    ids, mask = enc["input_ids"], enc["attention_mask"]
+    out = []
+    for i in range(len(texts)):
+        n = int(sum(_to_list(mask[i])))
+        out.append(_to_list(ids[i])[:n])
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Truth-Vault file (train_clip_detective.py:515-581 writes it; misinfo_forensics.py:214-246 reads)
+# ---------------------------------------------------------------------------------------------
+class _SafeUnpickler(pickle.Unpickler):
+    """Only numpy arrays and plain containers: a vault file cannot execute code on load."""
+    _ALLOWED = {
+        ("numpy", "ndarray"), ("numpy", "dtype"), ("numpy.core.multiarray", "_reconstruct"),
+        ("numpy._core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "scalar"),
+        ("numpy._core.multiarray", "scalar"), ("builtins", "dict"), ("builtins", "list"),
+        ("collections", "OrderedDict"), ("numpy", "float32"), ("numpy", "float64"), ("numpy", "int64"),
+    }
+
+    def find_class(self, module, name):
+        if (module, name) in self._ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"vault file references {module}.{name}; only numpy arrays and "
+                                     "plain containers are accepted")
+
+
+def load_vault(path: str):
+    """Returns (embeddings float32 [N, D], metadata list of {title, url, date}) or (None, None)
+    for an unknown format, following misinfo_forensics.py:222-246.  Accepts the reference's
+    pickle (restricted unpickler), .npz, or .json."""
+    if path.endswith(".npz"):
+        d = dict(np.load(path, allow_pickle=False))
+    elif path.endswith(".json"):
+        import json
+        with open(path) as f:
+            d = json.load(f)
+    else:
+        with open(path, "rb") as f:
+            d = _SafeUnpickler(io.BytesIO(f.read())).load()
+    if "embeddings" in d:
+        emb, meta = d["embeddings"], d["metadata"]
+        meta = [dict(m) for m in meta]
+    elif "image_embeddings" in d:
+        emb = d["image_embeddings"]
+        texts = list(d.get("text_contents", []))
+        paths = list(d.get("image_paths", []))
+        meta = [{"title": texts[i] if i < len(texts) else "Unknown",
+                 "url": paths[i] if i < len(paths) else "N/A", "date": "N/A"} for i in range(len(texts))]
+    else:
+        return None, None
+    return np.ascontiguousarray(np.asarray(emb, dtype=np.float32)), meta

@@ -56,37 +56,7 @@ N_VAULT = 2170
 SEED_W, SEED_IN, SEED_VAULT = 0, 1234, 77
 
 
-class TableRobertaTokenizer:
-    def __init__(self, table):
-        self.table = table
-
-    def __call__(self, text, return_tensors="pt", max_length=512, truncation=True, padding=True):
-        ids = list(self.table[text])[:max_length] if truncation else list(self.table[text])
-        t = torch.tensor([ids], dtype=torch.long)
-        return BatchEncoding({"input_ids": t, "attention_mask": torch.ones_like(t)})
-
-
-class TableClipProcessor:
-    def __init__(self, table):
-        self.table = table
-        self.image_processor = CLIPImageProcessor()
-
-    def __call__(self, text=None, images=None, return_tensors="pt", padding=False, truncation=False):
-        out = {}
-        if text is not None:
-            seqs = [list(self.table[s]) for s in text]
-            if truncation:
-                seqs = [s[:77] for s in seqs]
-            L = max(len(s) for s in seqs)
-            ids = torch.full((len(seqs), L), 49407, dtype=torch.long)
-            mask = torch.zeros((len(seqs), L), dtype=torch.long)
-            for i, s in enumerate(seqs):
-                ids[i, :len(s)] = torch.tensor(s)
-                mask[i, :len(s)] = 1
-            out["input_ids"], out["attention_mask"] = ids, mask
-        if images is not None:
-            out["pixel_values"] = self.image_processor(images=images, return_tensors="pt")["pixel_values"]
-        return BatchEncoding(out)
+from tables import TableClipProcessor, TableRobertaTokenizer  # noqa: E402
 
 
 def crc(a: np.ndarray) -> int:

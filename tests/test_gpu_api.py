@@ -1,0 +1,132 @@
+"""The drop-in API on the MI355X against the reference's own analyze() / CLIPSimilarityEngine
+outputs (tests/golden/golden.json, produced by running /root/reference code).  Same inputs: the
+reference's text strings (through the same id tables), PIL images, vault rows and titles."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+
+
+def _tables(golden, gi):
+    rob, clp = {}, {}
+    for i in range(golden["rob_ids"].shape[0]):
+        t = f"sample text {i}"
+        rob[t] = golden["rob_ids"][i, :gi["rob_lens"][i]].tolist()
+        clp[t] = golden["clip_ids"][i, :gi["clip_lens"][i]].tolist()
+    for j, ids in enumerate(gi["title_ids"]):
+        clp[f"Guardian article {j}"] = ids.tolist()
+    return rob, clp
+
+
+@pytest.fixture(scope="module")
+def forensics(golden, golden_inputs, det_sd, clip_sd, tmp_path_factory):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from tables import TableClipProcessor, TableRobertaTokenizer
+    from misinfo_forensics import MisinfoForensics
+    rob, clp = _tables(golden, golden_inputs)
+    mf = MisinfoForensics(fusion_weights="/nonexistent", faiss_index_path="/nonexistent",
+                          roberta_tokenizer=TableRobertaTokenizer(rob), clip_processor=TableClipProcessor(clp),
+                          detector_state=det_sd, clip_state=clip_sd, max_batch=64, verbose=False)
+    mf.set_vault(golden_inputs["vault"], golden_inputs["meta"])
+    return mf
+
+
+def _pil(gi, i):
+    from PIL import Image
+    return Image.fromarray(gi["imgs"][i])
+
+
+def _check(got, ref, tol=TOL):
+    assert got["verdict"] == ref["verdict"] and got["verdict_text"] == ref["verdict_text"]
+    assert abs(got["confidence"] - ref["confidence"]) < tol
+    for k, v in ref["scores"].items():
+        t = 2e-3 if k == "text_similarity" else tol
+        assert abs(got["scores"][k] - v) < t, (k, got["scores"][k], v)
+    assert [m["title"] for m in got["vault_matches"]] == [m["title"] for m in ref["vault_matches"]]
+    for a, b in zip(got["vault_matches"], ref["vault_matches"]):
+        assert abs(a["similarity"] - b["similarity"]) < tol and a["url"] == b["url"] and a["date"] == b["date"]
+    assert got["explanation"] == ref["explanation"]
+
+
+def test_analyze_pairs_match_reference(forensics, golden_json, golden_inputs):
+    for i, ref in enumerate(golden_json["analyze"]):
+        _check(forensics.analyze(text=f"sample text {i}", image_path=_pil(golden_inputs, i), verbose=False), ref)
+
+
+def test_analyze_single_modalities(forensics, golden_json, golden_inputs):
+    for n, i in enumerate((0, 1)):
+        _check(forensics.analyze(text=f"sample text {i}", verbose=False), golden_json["analyze_text_only"][n])
+    for n, i in enumerate((2, 3)):
+        _check(forensics.analyze(image_path=_pil(golden_inputs, i), verbose=False),
+               golden_json["analyze_image_only"][n])
+    with pytest.raises(ValueError) as e:
+        forensics.analyze(verbose=False)
+    assert str(e.value) == golden_json["analyze_no_input_error"]
+
+
+def test_batched_dicts_equal_single(forensics, golden_inputs):
+    texts = [f"sample text {i}" for i in range(8)]
+    batch = forensics.analyze_pairs(texts, [_pil(golden_inputs, i) for i in range(8)])
+    for i in (0, 5):
+        one = forensics.analyze(text=texts[i], image_path=_pil(golden_inputs, i), verbose=False)
+        assert one["verdict"] == batch[i]["verdict"] and one["explanation"] == batch[i]["explanation"]
+
+
+def test_detector_forward_methods(forensics, golden, golden_inputs):
+    from oracle import models as M
+    x = M.effnet_preprocess(torch.as_tensor(golden_inputs["imgs"]))
+    lg = forensics.detector.forward_image(x.cuda()).cpu()
+    np.testing.assert_allclose(torch.softmax(lg, 1)[:, 1].numpy(),
+                               torch.softmax(torch.as_tensor(golden["effnet_logits"]), 1)[:, 1].numpy(), atol=TOL)
+    ai, mi = forensics.detector.forward_text(torch.as_tensor(golden["rob_ids"]).cuda(),
+                                             torch.as_tensor(golden["rob_mask"]).cuda())
+    np.testing.assert_allclose(torch.softmax(ai.cpu(), 1)[:, 1].numpy(),
+                               torch.softmax(torch.as_tensor(golden["ai_logits"]), 1)[:, 1].numpy(), atol=TOL)
+
+
+def test_retrained_fusion_layer_reaches_the_kernel(forensics):
+    det = forensics.detector
+    saved = {k: v.clone() for k, v in det.fusion_layer.state_dict().items()}
+    with torch.no_grad():
+        det.fusion_layer[5].bias.add_(torch.tensor([0.3, -0.3]))
+    s = {"ai_score": 0.4, "misinfo_score": 0.6, "deepfake_score": 0.2, "clip_similarity": 0.1,
+         "vault_discrepancy": 0.0}
+    got = forensics.fusion_verdict(s)
+    det.eval()
+    with torch.no_grad():
+        p = torch.softmax(det.forward_fusion(torch.tensor([[0.4, 0.6, 0.2, 0.1, 0.0]])), 1)[0]
+    assert abs(got["fake_probability"] - p[1].item()) < 1e-5
+    det.fusion_layer.load_state_dict(saved)
+    forensics.detector.sync_fusion(force=True)
+
+
+def test_clip_similarity_engine(golden, golden_json, golden_inputs, clip_sd, tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from tables import TableClipProcessor
+    from clip_similarity_engine import CLIPSimilarityEngine
+    _, clp = _tables(golden, golden_inputs)
+    eng = CLIPSimilarityEngine(threshold=0.25, processor=TableClipProcessor(clp), clip_state=clip_sd)
+    for rec in golden_json["clip_engine"]:
+        i = rec["sample"]
+        p = str(tmp_path / f"img{i}.png")
+        _pil(golden_inputs, i).save(p)
+        sim, label = eng.calculate_similarity(p, f"sample text {i}")
+        assert abs(sim - rec["similarity"]) < TOL and label == rec["label"]
+        r = eng.analyze_with_explanation(p, f"sample text {i}")
+        assert r["label"] == rec["with_explanation"]["label"]
+        assert abs(r["similarity_score"] - rec["with_explanation"]["similarity_score"]) <= 1e-3 + 1e-9
+    errs = golden_json["clip_engine_errors"]
+    with pytest.raises(FileNotFoundError) as e:
+        eng.calculate_similarity("missing.png", "x")
+    assert str(e.value) == errs[0]["msg"]
+    with pytest.raises(ValueError) as e:
+        eng.calculate_similarity(str(tmp_path / "img0.png"), "")
+    assert str(e.value) == errs[1]["msg"]
