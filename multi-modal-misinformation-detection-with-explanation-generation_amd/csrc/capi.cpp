@@ -75,10 +75,11 @@ struct Workspace {
   bf16_t *r_xb = nullptr, *r_qkv = nullptr, *r_ctx = nullptr, *r_h = nullptr;
   // CLIP vision
   bf16_t *v_col = nullptr, *v_xb = nullptr, *v_qkv = nullptr, *v_ctx = nullptr, *v_h = nullptr, *v_cls = nullptr;
-  float *v_patch = nullptr, *v_x = nullptr, *v_emb = nullptr;
+  float *v_patch = nullptr, *v_x = nullptr, *v_emb = nullptr, *v_xc = nullptr;
+  bf16_t* v_ctxc = nullptr;
   // CLIP text
-  bf16_t *t_xb = nullptr, *t_qkv = nullptr, *t_ctx = nullptr, *t_h = nullptr, *t_pool = nullptr;
-  float *t_x = nullptr, *t_emb = nullptr;
+  bf16_t *t_xb = nullptr, *t_qkv = nullptr, *t_ctx = nullptr, *t_h = nullptr, *t_pool = nullptr, *t_ctxc = nullptr;
+  float *t_x = nullptr, *t_emb = nullptr, *t_xc = nullptr;
   int32_t* t_eos = nullptr;
   // EfficientNet
   bf16_t *e_a = nullptr, *e_b = nullptr, *e_exp = nullptr, *e_dw = nullptr;
@@ -134,11 +135,20 @@ struct mmf_handle {
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> ev_pool;
   int ev_used = 0;
+  // fork/join streams of mmf_analyze_batch (text, effnet, clip-text towers beside the caller's)
+  hipStream_t tower[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
+  int concurrent = 1;
 
   ~mmf_handle() {
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : ws_allocs) (void)hipFree(p);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < 3; ++i) {
+      if (tower[i]) (void)hipStreamDestroy(tower[i]);
+      if (join_ev[i]) (void)hipEventDestroy(join_ev[i]);
+    }
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
   }
 };
 
@@ -479,30 +489,41 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
     g.c16 = w.r_qkv;
     CHK(gemm(h, g, s));
     CHK(attn(h, w.r_qkv, 2304, mask, w.r_ctx, 768, B, L, 12, 0, s));
-    g = gemm_args(w.r_ctx, 768, Ly.o, M);
+    // last layer: only the CLS row feeds the heads (misinfo_forensics.py:95), so the rows below
+    // run on B compact CLS rows (strided A / residual reads) instead of B*L rows
+    const bool last = (i == 11);
+    const int Mr = last ? B : M;            // rows after the attention
+    const int rs = last ? L * 768 : 768;    // row stride of ctx / residual stream at this point
+    g = gemm_args(w.r_ctx, rs, Ly.o, Mr);
     g.res32 = w.r_x;
+    g.ldr = rs;
     g.c32 = w.r_y;
     CHK(gemm(h, g, s));
-    CHK(lnorm(h, w.r_y, 768, Ly.ln1, w.r_x, 768, w.r_xb, 768, M, 768, s));
-    g = gemm_args(w.r_xb, 768, Ly.fc1, M);
+    CHK(lnorm(h, w.r_y, 768, Ly.ln1, last ? w.r_y : w.r_x, 768, w.r_xb, 768, Mr, 768, s));
+    g = gemm_args(w.r_xb, 768, Ly.fc1, Mr);
     g.act = 1;  // GELU-erf
     g.c16 = w.r_h;
     CHK(gemm(h, g, s));
-    g = gemm_args(w.r_h, 3072, Ly.fc2, M);
-    g.res32 = w.r_x;
-    g.c32 = w.r_y;
+    g = gemm_args(w.r_h, 3072, Ly.fc2, Mr);
+    g.res32 = last ? w.r_y : w.r_x;
+    g.c32 = last ? w.r_x : w.r_y;
     CHK(gemm(h, g, s));
-    CHK(lnorm(h, w.r_y, 768, Ly.ln2, w.r_x, 768, w.r_xb, 768, M, 768, s));
+    CHK(lnorm(h, last ? w.r_x : w.r_y, 768, Ly.ln2, w.r_x, 768, w.r_xb, 768, Mr, 768, s));
   }
+  // w.r_x now holds the B final CLS rows, compact
   ProfScope ps(h, s, PK_HEADS, 2.0 * B * 2 * (768 * 256 + 256 * 2), (double)B * 768 * 4 + 2 * 768 * 256 * 4);
-  HIPCHK(launch_text_heads(w.r_x, L * 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,
+  HIPCHK(launch_text_heads(w.r_x, 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,
                            h->h_b2m, ai, mi, scores, score_stride, B, s));
   return 0;
 }
 
 // pre-LN CLIP encoder over x (fp32 residual, in place) with xb = LN1_0(x) already computed
+// Only one row per sequence is consumed after the last layer (CLS for the ViT, EOS for the text
+// tower: TF clip:561-582, 650-651): the last layer's out-proj / MLP run on those B rows, gathered
+// into compact buffers (xc fp32, ctxc bf16); on return xc holds them (before the final LN).
 int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, bf16_t* xb, bf16_t* qkv,
-                     bf16_t* ctx, bf16_t* hid, const int32_t* mask, int causal, int B, int L, hipStream_t s) {
+                     bf16_t* ctx, bf16_t* hid, const int32_t* mask, int causal, int B, int L,
+                     const int32_t* last_rows, float* xc, bf16_t* ctxc, hipStream_t s) {
   const int M = B * L;
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = layers[i];
@@ -510,6 +531,23 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
     g.c16 = qkv;
     CHK(gemm(h, g, s));
     CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
+    if (i == 11) {
+      HIPCHK(launch_gather_rows2(ctx, x, last_rows, L, H, ctxc, xc, B, s));
+      g = gemm_args(ctxc, H, Ly.o, B);
+      g.res32 = xc;
+      g.c32 = xc;
+      CHK(gemm(h, g, s));
+      CHK(lnorm(h, xc, H, Ly.ln2, nullptr, 0, xb, H, B, H, s));
+      g = gemm_args(xb, H, Ly.fc1, B);
+      g.act = 2;  // quick_gelu
+      g.c16 = hid;
+      CHK(gemm(h, g, s));
+      g = gemm_args(hid, I, Ly.fc2, B);
+      g.res32 = xc;
+      g.c32 = xc;
+      CHK(gemm(h, g, s));
+      break;
+    }
     g = gemm_args(ctx, H, Ly.o, M);
     g.res32 = x;
     g.c32 = x;
@@ -549,8 +587,9 @@ int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStre
     HIPCHK(launch_clip_vision_assemble(w.v_patch, h->v_cls, h->v_pos, h->v_pre.g, h->v_pre.b, h->v_layers[0].ln1.g,
                                        h->v_layers[0].ln1.b, 1e-5f, w.v_x, w.v_xb, B, s));
   }
-  CHK(run_clip_encoder(h, h->v_layers, 768, 3072, 12, w.v_x, w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50, s));
-  HIPCHK(launch_gather_ln(w.v_x, nullptr, 50, h->v_post.g, h->v_post.b, 1e-5f, w.v_cls, nullptr, B, 768, s));
+  CHK(run_clip_encoder(h, h->v_layers, 768, 3072, 12, w.v_x, w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50,
+                       nullptr, w.v_xc, w.v_ctxc, s));
+  HIPCHK(launch_gather_ln(w.v_xc, nullptr, 1, h->v_post.g, h->v_post.b, 1e-5f, w.v_cls, nullptr, B, 768, s));
   Lin16 pj;
   pj.w = h->v_proj;
   pj.out = 512;
@@ -569,9 +608,10 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
     HIPCHK(launch_clip_text_embed(ids, h->t_tok, h->t_pos, h->t_layers[0].ln1.g, h->t_layers[0].ln1.b, 1e-5f, w.t_x,
                                   w.t_xb, B, L, 512, s));
   }
-  CHK(run_clip_encoder(h, h->t_layers, 512, 2048, 8, w.t_x, w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, s));
   HIPCHK(launch_eos_index(ids, w.t_eos, B, L, h->eos_id, s));
-  HIPCHK(launch_gather_ln(w.t_x, w.t_eos, L, h->t_final.g, h->t_final.b, 1e-5f, w.t_pool, nullptr, B, 512, s));
+  CHK(run_clip_encoder(h, h->t_layers, 512, 2048, 8, w.t_x, w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, w.t_eos,
+                       w.t_xc, w.t_ctxc, s));
+  HIPCHK(launch_gather_ln(w.t_xc, nullptr, 1, h->t_final.g, h->t_final.b, 1e-5f, w.t_pool, nullptr, B, 512, s));
   Lin16 pj;
   pj.w = h->t_proj;
   pj.out = 512;
@@ -660,6 +700,8 @@ int mmf_create(int device, mmf_handle** out) {
   mmf_handle* h = new (std::nothrow) mmf_handle();
   if (!h) return fail(MMF_ENOMEM, "out of host memory");
   h->device = device;
+  const char* conc = getenv("MMF_CONCURRENT");  // MMF_CONCURRENT=0: run the towers on one stream
+  h->concurrent = !(conc && conc[0] == '0');
   *out = h;
   g_err.clear();
   return 0;
@@ -751,6 +793,10 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   CHK(A((void**)&w.t_pool, (size_t)B * 512 * 2));
   CHK(A((void**)&w.t_emb, (size_t)B * 512 * 4));
   CHK(A((void**)&w.t_eos, (size_t)B * 4));
+  CHK(A((void**)&w.v_xc, (size_t)B * 768 * 4));
+  CHK(A((void**)&w.v_ctxc, (size_t)B * 768 * 2));
+  CHK(A((void**)&w.t_xc, (size_t)B * 512 * 4));
+  CHK(A((void**)&w.t_ctxc, (size_t)B * 512 * 2));
   // EfficientNet activation sizes per image
   size_t max_io = 112 * 112 * 32, max_exp = 0, max_dw = 0, max_pool = 0, max_c = 1280;
   {
@@ -897,10 +943,34 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   hipStream_t s = (hipStream_t)stream;
   if (!img_clip) img_clip = img_eff;
   Workspace& w = h->ws;
-  CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, s));
-  CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, s));
+  // the per-kernel profiling pass runs the towers sequentially so event intervals are clean
+  const int concurrent = h->concurrent && !h->prof;
+  if (concurrent && !h->tower[0]) {
+    for (int i = 0; i < 3; ++i) {
+      HIPCHK(hipStreamCreateWithFlags(&h->tower[i], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
+    }
+    HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+  }
+  // fork: the four towers only share read-only inputs and write disjoint workspaces/outputs
+  hipStream_t st_text = s, st_eff = s, st_ctxt = s;
+  if (concurrent) {
+    HIPCHK(hipEventRecord(h->fork_ev, s));
+    for (int i = 0; i < 3; ++i) HIPCHK(hipStreamWaitEvent(h->tower[i], h->fork_ev, 0));
+    st_text = h->tower[0];
+    st_eff = h->tower[1];
+    st_ctxt = h->tower[2];
+  }
+  CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
+  CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
+  CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
   CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
-  CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, s));
+  if (concurrent) {
+    for (int i = 0; i < 3; ++i) {
+      HIPCHK(hipEventRecord(h->join_ev[i], h->tower[i]));
+      HIPCHK(hipStreamWaitEvent(s, h->join_ev[i], 0));
+    }
+  }
   HIPCHK(launch_rowdot(w.v_emb, w.t_emb, scores5 + 3, 5, B, 512, s));
   if (h->ready & 32) {
     ProfScope ps(h, s, PK_VAULT, 2.0 * B * h->vault_n * 512, (double)h->vault_n * 512 * 4 + (double)B * h->vault_n * 8);

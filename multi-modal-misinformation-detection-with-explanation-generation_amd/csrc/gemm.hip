@@ -193,7 +193,7 @@ MMF_DEV void glds_tile(const bf16_t* __restrict__ G, int ld, int row0, int rowma
   }
 }
 
-template <int BN, int WGM, int WGN>
+template <int BN, int WGM, int WGN, int ACT>
 __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
   // K-slab of the NEXT tile is DMA'd into the free LDS stage during the current tile's last
@@ -258,6 +258,47 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmArgs g, int tilesN, 
       cur ^= 1;
     }
 
+    // epilogue per fragment; the activation is a compile-time parameter (no per-element branch)
+    if (g.c16 && !g.c32 && !g.res32 && !g.res16) {
+      // bf16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
+      // fragment of each pair so every lane stores 16 contiguous bytes (half the store issues)
+#pragma unroll
+      for (int j = 0; j < MI; ++j) {
+        const int m = m0 + wm * TM + j * 16 + fr;
+#pragma unroll
+        for (int i = 0; i < NI; i += 2) {
+          uint2 pk[2];
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int n = min(n0 + wn * TN + (i + h2) * 16 + fg * 4, N - 4);
+            float v[4] = {acc[i + h2][j][0], acc[i + h2][j][1], acc[i + h2][j][2], acc[i + h2][j][3]};
+            if (g.bias) {
+              const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
+              v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+            }
+            if (ACT != ACT_NONE) {
+#pragma unroll
+              for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
+            }
+            pk[h2] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+          }
+          const bool odd = fg & 1;
+          const uint2 send = odd ? pk[0] : pk[1];
+          uint2 recv;
+          recv.x = __shfl_xor(send.x, 16, 64);
+          recv.y = __shfl_xor(send.y, 16, 64);
+          // even fg: cols (16i + 4fg) .. +7 of fragment i; odd fg: cols (16(i+1) + 4(fg-1)) .. +7
+          const int n8 = n0 + wn * TN + (odd ? (i + 1) * 16 + (fg - 1) * 4 : i * 16 + fg * 4);
+          const uint4 o = odd ? make_uint4(recv.x, recv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, recv.x, recv.y);
+          if (m < M) {
+            bf16_t* dst = g.c16 + (size_t)m * g.ldc + n8;
+            if (n8 + 8 <= N) *reinterpret_cast<uint4*>(dst) = o;
+            else if (n8 < N) *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y);
+          }
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < MI; ++j) {
       const int m = m0 + wm * TM + j * 16 + fr;
@@ -271,9 +312,9 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmArgs g, int tilesN, 
           const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
           v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
         }
-        if (g.act) {
+        if (ACT != ACT_NONE) {
 #pragma unroll
-          for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], g.act);
+          for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
         }
         if (g.res32) {
           const float4 rr = *reinterpret_cast<const float4*>(g.res32 + (size_t)m * g.ldr + n);
@@ -296,7 +337,26 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + 255) / 256, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
   const int grid = tiles < 256 ? tiles : 256;
-  hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+  switch (a.act) {
+    case ACT_GELU:
+      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_GELU>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+      break;
+    case ACT_QUICK_GELU:
+      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_QUICK_GELU>), dim3(grid), dim3(512), 0, s, a, tilesN,
+                         tiles);
+      break;
+    case ACT_NONE:
+      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_NONE>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+      break;
+    case ACT_SILU:
+      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_SILU>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+      break;
+    case ACT_RELU:
+      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_RELU>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

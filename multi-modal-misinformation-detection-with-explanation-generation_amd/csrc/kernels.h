@@ -55,6 +55,9 @@ hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int 
 // gather rows: out bf16 [B][C] = LN(x[row_index(b)]) where row_index = b*L + (idx ? idx[b] : 0)
 hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const float* g, const float* b, float eps,
                             bf16_t* out, float* out32, int B, int C, hipStream_t s);
+// compact copies of rows b*L + (idx ? idx[b] : 0) of a bf16 and an fp32 [.,C] buffer
+hipError_t launch_gather_rows2(const bf16_t* a16, const float* a32, const int32_t* idx, int L, int C, bf16_t* o16,
+                               float* o32, int B, hipStream_t s);
 // L2-normalise rows of fp32 [B][C] in place (C multiple of 64)
 hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s);
 // two 768->256->2 heads (fp32) from CLS rows x[b*L*768]; writes logits and softmax[:,1] scores

@@ -195,6 +195,18 @@ __global__ __launch_bounds__(256) void gather_ln_kernel(const float* x, const in
   store_row<NV>(v, out32 ? out32 + (size_t)bi * C : nullptr, out ? out + (size_t)bi * C : nullptr, lane);
 }
 
+// rows b*L + (idx ? idx[b] : 0) of a bf16 [.,C] and an fp32 [.,C] buffer -> compact [B,C] copies
+__global__ __launch_bounds__(256) void gather_rows2_kernel(const bf16_t* a16, const float* a32, const int32_t* idx,
+                                                           int L, int C, bf16_t* o16, float* o32, int B) {
+  const int bi = blockIdx.x;
+  if (bi >= B) return;
+  const size_t row = (size_t)bi * L + (idx ? idx[bi] : 0);
+  for (int c = threadIdx.x * 4; c < C; c += 256 * 4) {
+    *reinterpret_cast<uint2*>(o16 + (size_t)bi * C + c) = *reinterpret_cast<const uint2*>(a16 + row * C + c);
+    *reinterpret_cast<float4*>(o32 + (size_t)bi * C + c) = *reinterpret_cast<const float4*>(a32 + row * C + c);
+  }
+}
+
 __global__ __launch_bounds__(256) void l2norm_kernel(float* x, int B, int C) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
@@ -271,6 +283,13 @@ hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const flo
     hipLaunchKernelGGL(gather_ln_kernel<2>, grid, dim3(256), 0, s, x, idx, L, g, b, eps, out, out32, B);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows2(const bf16_t* a16, const float* a32, const int32_t* idx, int L, int C, bf16_t* o16,
+                               float* o32, int B, hipStream_t s) {
+  if (C & 3) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_rows2_kernel, dim3(B), dim3(256), 0, s, a16, a32, idx, L, C, o16, o32, B);
   return hipGetLastError();
 }
 

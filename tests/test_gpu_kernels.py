@@ -61,6 +61,28 @@ def test_gemm_vs_torch_fp32(lib, M, N, K, act, res):
     assert ((c16.cpu().float() - ref).abs() <= ref.abs() * 2 ** -7 + 1e-5 * scale).all()
 
 
+@pytest.mark.parametrize("M,N,K,act", [(1000, 200, 128, 1), (2048, 2304, 768, 0), (777, 392, 512, 2),
+                                       (4096, 3072, 768, 1), (300, 136, 64, 0)])
+def test_gemm_bf16_only_output(lib, M, N, K, act):
+    """bf16-only epilogue (paired 16-B stores across lanes l, l^16), incl. column tails."""
+    import mmf_amd.hip as hip
+    g = torch.Generator().manual_seed(M + 3 * N)
+    A = _bf16(torch.randn(M, K, generator=g))
+    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
+    bias = torch.randn(N, generator=g)
+    ref = _act(A.float() @ W.float().T + bias, act)
+    dev = torch.device("cuda")
+    c16 = torch.full((M, N + 8), 7.0, device=dev, dtype=torch.bfloat16)  # ldc = N + 8: canary columns
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)  # keep the device buffers alive across the call
+    hip.check(lib.mmf_gemm_bf16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), None,
+                                None, c16.data_ptr(), N + 8, M, N, K, act, hip.stream_ptr()))
+    torch.cuda.synchronize()
+    out = c16.cpu().float()
+    scale = ref.abs().max().item()
+    assert ((out[:, :N] - ref).abs() <= ref.abs() * 2 ** -7 + 1e-5 * scale).all()
+    assert (out[:, N:] == 7.0).all(), "wrote past N"
+
+
 def _attn_ref(qkv, mask, B, L, H, causal):
     D = H * 64
     x = qkv.float().view(B, L, 3, H, 64)
@@ -92,7 +114,8 @@ def test_attention_vs_torch_fp32(lib, B, L, H, causal, masked):
     dev = torch.device("cuda")
     out = torch.empty(B * L, H * 64, device=dev, dtype=torch.bfloat16)
     md = mask.to(dev, torch.int32) if mask is not None else None
-    hip.check(lib.mmf_attention_bf16(qkv.to(dev).data_ptr(), hip.ptr(md), out.data_ptr(), B, L, H, causal,
+    qkv_d = qkv.to(dev)
+    hip.check(lib.mmf_attention_bf16(qkv_d.data_ptr(), hip.ptr(md), out.data_ptr(), B, L, H, causal,
                                      hip.stream_ptr()))
     torch.cuda.synchronize()
     got = out.cpu().float()
