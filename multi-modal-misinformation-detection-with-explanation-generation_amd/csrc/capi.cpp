@@ -164,11 +164,11 @@ int dev_alloc(mmf_handle* h, void** p, size_t bytes, bool workspace = false) {
 
 // ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
 enum ProfKind {
-  PK_GEMM0 = 0, PK_GEMM_LAST = 7, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
+  PK_GEMM0 = 0, PK_GEMM_LAST = 8, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
   PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
 };
 const char* prof_kind_name(int k) {
-  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                         "attention", "layernorm", "embed+ln", "clip_im2col", "effnet_stem",
                                         "dwconv", "se", "gap_classifier", "text_heads", "vault", "fusion"};
   if (k >= 0 && k <= PK_GEMM_LAST) return gemm_config_name(k);

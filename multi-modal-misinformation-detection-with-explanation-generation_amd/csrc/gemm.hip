@@ -175,10 +175,11 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-template <int ROWS>
+template <int ROWS, int NW>
 MMF_DEV void glds_tile(const bf16_t* __restrict__ G, int ld, int row0, int rowmax, int k0, bf16_t* tile, int wave,
                        int lane) {
-  constexpr int PER_WAVE = ROWS / 64;  // 1-KB segments (8 rows x 128 B) per wave
+  constexpr int PER_WAVE = ROWS / (8 * NW);  // 1-KB segments (8 rows x 128 B) per wave
+  static_assert(PER_WAVE * 8 * NW == ROWS, "rows must split evenly over the waves");
 #pragma unroll
   for (int j = 0; j < PER_WAVE; ++j) {
     const int seg = wave * PER_WAVE + j;
@@ -193,16 +194,18 @@ MMF_DEV void glds_tile(const bf16_t* __restrict__ G, int ld, int row0, int rowma
   }
 }
 
-template <int BN, int WGM, int WGN, int ACT>
-__global__ __launch_bounds__(512) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles) {
+template <int BM, int BN, int WGM, int WGN, int ACT>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
   // K-slab of the NEXT tile is DMA'd into the free LDS stage during the current tile's last
   // K-step, so only the very first tile pays the load latency and each epilogue's stores drain
   // underneath the next tile's first MFMAs.
-  constexpr int BM = 256;
+  // BM = 128 variants use 4 waves and <= 80 KB of LDS so TWO workgroups share a CU: one's
+  // epilogue (stores) then overlaps the other's MFMA main loop.
+  constexpr int NW = WGM * WGN;
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int STAGE = (BM + BN) * BK;
-  static_assert(WGM * WGN == 8, "8 waves");
+  static_assert(NW == 8 || NW == 4, "4 or 8 waves");
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
 
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -220,8 +223,8 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmArgs g, int tilesN, 
   auto stage = [&](int buf, int tile, int kt) {
     const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
     bf16_t* nb = lds + buf * STAGE;
-    glds_tile<BM>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
-    glds_tile<BN>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
+    glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
+    glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
   };
   stage(0, t, 0);
   __syncthreads();
@@ -332,31 +335,27 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmArgs g, int tilesN, 
   }
 }
 
-template <int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN>
 hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
-  const int tilesM = (a.M + 255) / 256, tilesN = (a.N + BN - 1) / BN;
+  const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
-  const int grid = tiles < 256 ? tiles : 256;
+  const int per_cu = (BM == 128) ? 2 : 1;  // co-resident workgroups per CU (LDS / VGPR budget)
+  const int grid = tiles < 256 * per_cu ? tiles : 256 * per_cu;
+  const dim3 blk(64 * WGM * WGN);
+#define MMF_GLDS_CASE(ACT)                                                                                  \
+  case ACT:                                                                                                 \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT>), dim3(grid), blk, 0, s, a, tilesN, tiles); \
+    break;
   switch (a.act) {
-    case ACT_GELU:
-      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_GELU>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
-      break;
-    case ACT_QUICK_GELU:
-      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_QUICK_GELU>), dim3(grid), dim3(512), 0, s, a, tilesN,
-                         tiles);
-      break;
-    case ACT_NONE:
-      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_NONE>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
-      break;
-    case ACT_SILU:
-      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_SILU>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
-      break;
-    case ACT_RELU:
-      hipLaunchKernelGGL((gemm_glds_kernel<BN, WGM, WGN, ACT_RELU>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
-      break;
+    MMF_GLDS_CASE(ACT_NONE)
+    MMF_GLDS_CASE(ACT_GELU)
+    MMF_GLDS_CASE(ACT_QUICK_GELU)
+    MMF_GLDS_CASE(ACT_SILU)
+    MMF_GLDS_CASE(ACT_RELU)
     default:
       return hipErrorInvalidValue;
   }
+#undef MMF_GLDS_CASE
   return hipGetLastError();
 }
 
@@ -375,7 +374,7 @@ static int forced_config(const GemmArgs& a) {
   if (!e || !*e) return -1;
   const int c = atoi(e);
   if (c >= 4 && ((a.K % BK) || a.ascale)) return -1;
-  return (c >= 0 && c <= 6) ? c : -1;
+  return (c >= 0 && c <= 8) ? c : -1;
 }
 
 int gemm_config(const GemmArgs& a) {
@@ -405,8 +404,8 @@ int gemm_config(const GemmArgs& a) {
 const char* gemm_config_name(int c) {
   static const char* names[] = {"gemm_bf16<256,32,4,1>",  "gemm_bf16<256,64,4,1>",  "gemm_bf16<64,128,1,4>",
                                 "gemm_bf16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
-                                "gemm_glds<256,192,4,2>"};
-  return (c >= 0 && c < 7) ? names[c] : "gemm_bf16<?>";
+                                "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>"};
+  return (c >= 0 && c < 9) ? names[c] : "gemm_bf16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
@@ -416,9 +415,11 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);
     case 2: return run<64, 128, 1, 4>(a, s);
-    case 4: return run_glds<256, 2, 4>(a, s);
-    case 5: return run_glds<128, 4, 2>(a, s);
-    case 6: return run_glds<192, 4, 2>(a, s);
+    case 4: return run_glds<256, 256, 2, 4>(a, s);
+    case 5: return run_glds<256, 128, 4, 2>(a, s);
+    case 6: return run_glds<256, 192, 4, 2>(a, s);
+    case 7: return run_glds<128, 192, 2, 2>(a, s);
+    case 8: return run_glds<128, 128, 2, 2>(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

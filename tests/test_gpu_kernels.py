@@ -83,6 +83,37 @@ def test_gemm_bf16_only_output(lib, M, N, K, act):
     assert (out[:, N:] == 7.0).all(), "wrote past N"
 
 
+@pytest.mark.parametrize("cfg", [3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("M,N,K,act,res", [(1000, 2304, 768, 1, False), (777, 392, 512, 0, True),
+                                           (130, 136, 64, 2, False)])
+def test_gemm_forced_configs(lib, monkeypatch, cfg, M, N, K, act, res):
+    """Every tile instantiation (MMF_GEMM_CONFIG override) on ragged M/N, both epilogues."""
+    import mmf_amd.hip as hip
+    monkeypatch.setenv("MMF_GEMM_CONFIG", str(cfg))
+    g = torch.Generator().manual_seed(cfg * 1000 + M)
+    A = _bf16(torch.randn(M, K, generator=g))
+    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g) if res else None
+    ref = _act(A.float() @ W.float().T + bias, act)
+    if res:
+        ref = ref + R
+    dev = torch.device("cuda")
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    Rd = torch.nn.functional.pad(R, (0, 8)).to(dev) if res else None  # residual shares ldc = N + 8
+    c16 = torch.full((M, N + 8), 7.0, device=dev, dtype=torch.bfloat16)
+    c32 = torch.empty(M, N + 8, device=dev) if res else None
+    hip.check(lib.mmf_gemm_bf16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), hip.ptr(c32),
+                                c16.data_ptr(), N + 8, M, N, K, act, hip.stream_ptr()))
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    out = c16.cpu().float()
+    assert ((out[:, :N] - ref).abs() <= ref.abs() * 2 ** -7 + 1e-5 * scale).all()
+    assert (out[:, N:] == 7.0).all(), "wrote past N"
+    if res:
+        assert (c32.cpu()[:, :N] - ref).abs().max().item() / scale < 2e-5
+
+
 def _attn_ref(qkv, mask, B, L, H, causal):
     D = H * 64
     x = qkv.float().view(B, L, 3, H, 64)

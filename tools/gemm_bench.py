@@ -31,7 +31,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="auto,3,4,5,6")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--noout", action="store_true", help="also time each shape with no epilogue stores")
+    ap.add_argument("--kscale", default="", help="comma list of K multipliers to time (fixed-cost probe)")
     a = ap.parse_args()
+    global SHAPES
+    if a.kscale:
+        SHAPES = [(f"{n}_k{m}", M, N, K * int(m), act, out) for n, M, N, K, act, out in SHAPES
+                  for m in a.kscale.split(",")]
     lib = hip.load()
     dev = torch.device("cuda")
     res = []
@@ -59,6 +65,21 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
             row[cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+        if a.noout:
+            def call():
+                hip.check(lib.mmf_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None, None, None, N,
+                                            M, N, K, 0, hip.stream_ptr()))
+            for cfg in a.configs.split(","):
+                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
+                call()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    call()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                row["noout_" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
         os.environ["MMF_GEMM_CONFIG"] = ""
         res.append(row)
         print(json.dumps(row), flush=True)
