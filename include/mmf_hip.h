@@ -139,6 +139,12 @@ const char* mmf_profile_kind_name(int kind);
 int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual,
                   float* c32, void* c16, int ldc, int M, int N, int K, int act, void* stream);
 
+/* The same with the EfficientNet operands of the 1x1 convolutions: bf16 residual res16 [M,N] (ldc)
+ * and a per-(image, k) fp32 scale ascale [M / rows_per_batch, K] applied to A (SE excitation). */
+int mmf_gemm_bf16_ex(const void* A, int lda, const void* W, int ldw, const float* bias, const void* res16,
+                     const float* ascale, int rows_per_batch, void* c16, int ldc, int M, int N, int K, int act,
+                     void* stream);
+
 /* Low-level attention op for tests: qkv bf16 [B*L, 3*H*64] (q|k|v), mask int32 [B,L] or NULL,
  * causal 0/1 -> out bf16 [B*L, H*64]. */
 int mmf_attention_bf16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,

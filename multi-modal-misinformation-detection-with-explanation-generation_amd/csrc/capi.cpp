@@ -164,11 +164,11 @@ int dev_alloc(mmf_handle* h, void** p, size_t bytes, bool workspace = false) {
 
 // ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
 enum ProfKind {
-  PK_GEMM0 = 0, PK_GEMM_LAST = 8, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
+  PK_GEMM0 = 0, PK_GEMM_LAST = 9, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
   PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
 };
 const char* prof_kind_name(int k) {
-  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                         "attention", "layernorm", "embed+ln", "clip_im2col", "effnet_stem",
                                         "dwconv", "se", "gap_classifier", "text_heads", "vault", "fusion"};
   if (k >= 0 && k <= PK_GEMM_LAST) return gemm_config_name(k);
@@ -1039,6 +1039,32 @@ int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* b
   g.K = K;
   g.act = act;
   if (!A || !W || (!c32 && !c16)) return fail(MMF_EINVAL, "null argument");
+  hipError_t e = launch_gemm(g, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MMF_EIO, "gemm: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int mmf_gemm_bf16_ex(const void* A, int lda, const void* W, int ldw, const float* bias, const void* res16,
+                     const float* ascale, int rows_per_batch, void* c16, int ldc, int M, int N, int K, int act,
+                     void* stream) {
+  GemmArgs g{};
+  g.A = (const bf16_t*)A;
+  g.lda = lda;
+  g.W = (const bf16_t*)W;
+  g.ldw = ldw;
+  g.bias = bias;
+  g.res16 = (const bf16_t*)res16;
+  g.ldr = ldc;
+  g.ascale = ascale;
+  g.rows_per_batch = rows_per_batch;
+  g.c16 = (bf16_t*)c16;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.act = act;
+  if (!A || !W || !c16) return fail(MMF_EINVAL, "null argument");
+  if (ascale && rows_per_batch <= 0) return fail(MMF_EINVAL, "rows_per_batch must be > 0 with ascale");
   hipError_t e = launch_gemm(g, (hipStream_t)stream);
   if (e != hipSuccess) return fail(MMF_EIO, "gemm: %s", hipGetErrorString(e));
   return 0;

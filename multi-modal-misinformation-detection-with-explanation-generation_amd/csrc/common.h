@@ -69,3 +69,34 @@ MMF_DEV f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 }
 
 MMF_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+
+// Raw buffer access (CDNA SRSRC): 32-bit byte offsets with hardware bounds checking -- loads at
+// offsets >= `bytes` return 0 and such stores are dropped, so null operands (bytes = 0) and
+// ragged tile edges need no branches.  Descriptors must be built from wave-uniform values.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kOOB = 0x80000000u;  // an offset past every buffer the launchers allow
+MMF_DEV rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? (int)bytes : 0, 0x00020000);
+}
+MMF_DEV float4 buf_load_f4(rsrc_t r, uint32_t off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+MMF_DEV uint2 buf_load_u2(rsrc_t r, uint32_t off) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_uint2(v.x, v.y);
+}
+MMF_DEV void buf_store_f4(rsrc_t r, uint32_t off, float4 v) {
+  const u32x4 w = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+}
+MMF_DEV void buf_store_u4(rsrc_t r, uint32_t off, uint4 v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+}
+MMF_DEV void buf_store_u2(rsrc_t r, uint32_t off, uint2 v) {
+  const u32x2 w = {v.x, v.y};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, off, 0, 0);
+}

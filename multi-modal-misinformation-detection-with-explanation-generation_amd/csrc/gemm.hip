@@ -14,6 +14,8 @@
 //    that makes the 16-lane ds_read_b128 fragment reads conflict-free; double-buffered, register
 //    staged (next tile's global loads issued before the MFMAs, written to LDS after them).
 //  * XCD-aware bijective block remap so consecutive tiles of one row panel share an XCD's L2.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -217,6 +219,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, i
   const int M = g.M, N = g.N;
   const int nk = g.K / BK;
   const int fr = lane & 15, fg = lane >> 4;
+  const bool has_res = g.res32 || g.res16;
+  const bool full8 = (N & 7) == 0;
+  // byte extents of the epilogue operands (run_glds keeps them, and every offset formed below
+  // for a row < M + BM, under 2^31)
+  const uint32_t out_elems = (uint32_t)(M - 1) * g.ldc + N;
+  const rsrc_t rbias = make_rsrc(g.bias, (uint32_t)N * 4u);
+  const rsrc_t rres = make_rsrc(g.res32 ? (const void*)g.res32 : (const void*)g.res16,
+                                ((uint32_t)(M - 1) * g.ldr + N) * (g.res32 ? 4u : 2u));
+  const rsrc_t rc32 = make_rsrc(g.c32, out_elems * 4u);
+  const rsrc_t rc16 = make_rsrc(g.c16, out_elems * 2u);
 
   int t = wgid;
   if (t >= tiles) return;
@@ -237,6 +249,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, i
     for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 bias_r[NI];  // this lane's epilogue bias columns, fetched under the K loop
+#pragma unroll
+    for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
 
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
@@ -261,24 +276,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, i
       cur ^= 1;
     }
 
-    // epilogue per fragment; the activation is a compile-time parameter (no per-element branch)
-    if (g.c16 && !g.c32 && !g.res32 && !g.res16) {
+    // Epilogue.  The activation is a compile-time parameter (no per-element branch).  All traffic
+    // is raw-buffer: out-of-range rows/columns read 0 / drop their stores, so there is no divergent
+    // branch and no load that has to wait on the stores issued before it -- bias columns were
+    // fetched at tile start and residual rows are loaded one fragment row AHEAD of the stores (one
+    // vmcnt counter covers loads and stores in issue order).
+    if (!has_res && !g.c32) {
       // bf16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
       // fragment of each pair so every lane stores 16 contiguous bytes (half the store issues)
 #pragma unroll
       for (int j = 0; j < MI; ++j) {
-        const int m = m0 + wm * TM + j * 16 + fr;
+        const uint32_t m = m0 + wm * TM + j * 16 + fr;
 #pragma unroll
         for (int i = 0; i < NI; i += 2) {
           uint2 pk[2];
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2) {
-            const int n = min(n0 + wn * TN + (i + h2) * 16 + fg * 4, N - 4);
-            float v[4] = {acc[i + h2][j][0], acc[i + h2][j][1], acc[i + h2][j][2], acc[i + h2][j][3]};
-            if (g.bias) {
-              const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
-              v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-            }
+            float v[4] = {acc[i + h2][j][0] + bias_r[i + h2].x, acc[i + h2][j][1] + bias_r[i + h2].y,
+                          acc[i + h2][j][2] + bias_r[i + h2].z, acc[i + h2][j][3] + bias_r[i + h2].w};
             if (ACT != ACT_NONE) {
 #pragma unroll
               for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
@@ -293,45 +308,59 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, i
           // even fg: cols (16i + 4fg) .. +7 of fragment i; odd fg: cols (16(i+1) + 4(fg-1)) .. +7
           const int n8 = n0 + wn * TN + (odd ? (i + 1) * 16 + (fg - 1) * 4 : i * 16 + fg * 4);
           const uint4 o = odd ? make_uint4(recv.x, recv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, recv.x, recv.y);
-          if (m < M) {
-            bf16_t* dst = g.c16 + (size_t)m * g.ldc + n8;
-            if (n8 + 8 <= N) *reinterpret_cast<uint4*>(dst) = o;
-            else if (n8 < N) *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y);
+          const uint32_t off = (m * (uint32_t)g.ldc + n8) * 2u;
+          if (full8) {
+            buf_store_u4(rc16, n8 < N ? off : kOOB, o);
+          } else {  // N % 8 == 4: the last group of a row holds only 4 valid columns
+            buf_store_u4(rc16, n8 + 8 <= N ? off : kOOB, o);
+            buf_store_u2(rc16, (n8 + 8 > N && n8 < N) ? off : kOOB, make_uint2(o.x, o.y));
           }
         }
       }
       continue;
     }
+    // general epilogue, instantiated per residual dtype so that no load sits under a branch
+    auto epilogue = [&](auto res_is_f32) {
+      constexpr bool R32 = decltype(res_is_f32)::value;
+      float4 rcur[NI], rnext[NI];
+      auto load_res = [&](float4* r, int j) {
+        const uint32_t m = m0 + wm * TM + j * 16 + fr;
 #pragma unroll
-    for (int j = 0; j < MI; ++j) {
-      const int m = m0 + wm * TM + j * 16 + fr;
-      if (m >= M) continue;
+        for (int i = 0; i < NI; ++i) {
+          const uint32_t e = m * (uint32_t)g.ldr + (n0 + wn * TN + i * 16 + fg * 4);
+          if constexpr (R32) {
+            r[i] = buf_load_f4(rres, e * 4u);
+          } else {
+            const uint2 rr = buf_load_u2(rres, e * 2u);  // zeros when there is no residual
+            r[i] = make_float4(lo_bf(rr.x), hi_bf(rr.x), lo_bf(rr.y), hi_bf(rr.y));
+          }
+        }
+      };
+      load_res(rcur, 0);
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int n = n0 + wn * TN + i * 16 + fg * 4;
-        if (n >= N) continue;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (g.bias) {
-          const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
-          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-        }
-        if (ACT != ACT_NONE) {
+      for (int j = 0; j < MI; ++j) {
+        if (j + 1 < MI) load_res(rnext, j + 1);
+        const uint32_t m = m0 + wm * TM + j * 16 + fr;
 #pragma unroll
-          for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
+        for (int i = 0; i < NI; ++i) {
+          const int n = n0 + wn * TN + i * 16 + fg * 4;
+          float v[4] = {acc[i][j][0] + bias_r[i].x, acc[i][j][1] + bias_r[i].y, acc[i][j][2] + bias_r[i].z,
+                        acc[i][j][3] + bias_r[i].w};
+          if (ACT != ACT_NONE) {
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
+          }
+          v[0] += rcur[i].x; v[1] += rcur[i].y; v[2] += rcur[i].z; v[3] += rcur[i].w;
+          const uint32_t e = n < N ? m * (uint32_t)g.ldc + n : (kOOB >> 2);
+          if (g.c32) buf_store_f4(rc32, e * 4u, make_float4(v[0], v[1], v[2], v[3]));
+          if (g.c16) buf_store_u2(rc16, e * 2u, make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3])));
         }
-        if (g.res32) {
-          const float4 rr = *reinterpret_cast<const float4*>(g.res32 + (size_t)m * g.ldr + n);
-          v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-        } else if (g.res16) {
-          const uint2 rr = *reinterpret_cast<const uint2*>(g.res16 + (size_t)m * g.ldr + n);
-          v[0] += lo_bf(rr.x); v[1] += hi_bf(rr.x); v[2] += lo_bf(rr.y); v[3] += hi_bf(rr.y);
-        }
-        if (g.c32) *reinterpret_cast<float4*>(g.c32 + (size_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
-        if (g.c16)
-          *reinterpret_cast<uint2*>(g.c16 + (size_t)m * g.ldc + n) =
-              make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+#pragma unroll
+        for (int i = 0; i < NI; ++i) rcur[i] = rnext[i];
       }
-    }
+    };
+    if (g.res32) epilogue(std::true_type{});
+    else epilogue(std::false_type{});
   }
 }
 
@@ -368,22 +397,31 @@ hipError_t run(const GemmArgs& a, hipStream_t s) {
 
 }  // namespace
 
+// The LDS-DMA kernel addresses its epilogue operands with 32-bit raw-buffer byte offsets.
+static bool glds_ok(const GemmArgs& a) {
+  const size_t lim = (size_t)1 << 31;
+  const size_t rows = (size_t)a.M + 256;
+  return (a.K % BK) == 0 && !a.ascale && rows * a.ldc * 4 < lim && rows * (a.ldr > 0 ? a.ldr : 0) * 4 < lim;
+}
+
 static int forced_config(const GemmArgs& a) {
   // MMF_GEMM_CONFIG=<n>: benchmarking override (tools/gemm_bench.py); ignored if inapplicable
   const char* e = getenv("MMF_GEMM_CONFIG");
   if (!e || !*e) return -1;
   const int c = atoi(e);
-  if (c >= 4 && ((a.K % BK) || a.ascale)) return -1;
-  return (c >= 0 && c <= 8) ? c : -1;
+  if (c >= 4 && c <= 8 && !glds_ok(a)) return -1;
+  if (c == 9 && !pw_applicable(a)) return -1;
+  return (c >= 0 && c <= 9) ? c : -1;
 }
 
 int gemm_config(const GemmArgs& a) {
   const int f = forced_config(a);
   if (f >= 0) return f;
+  if (pw_applicable(a)) return 9;  // HBM-bound 1x1 convolutions (pointwise.hip)
   if (a.N <= 32) return 0;
   if (a.N <= 64) return 1;
   if (a.M <= 512) return 2;  // skinny-M (projections, M = batch)
-  if ((a.K % BK) == 0 && !a.ascale && a.N >= 128) {
+  if (glds_ok(a) && a.N >= 128) {
     // persistent 256-row LDS-DMA tiles: pick the column tile that minimises whole "rounds" of
     // 256 CUs x per-tile time (wider tiles are more efficient per flop)
     const long tm = (a.M + 255) / 256;
@@ -404,13 +442,17 @@ int gemm_config(const GemmArgs& a) {
 const char* gemm_config_name(int c) {
   static const char* names[] = {"gemm_bf16<256,32,4,1>",  "gemm_bf16<256,64,4,1>",  "gemm_bf16<64,128,1,4>",
                                 "gemm_bf16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
-                                "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>"};
-  return (c >= 0 && c < 9) ? names[c] : "gemm_bf16<?>";
+                                "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
+                                "pw_conv"};
+  return (c >= 0 && c < 10) ? names[c] : "gemm_bf16<?>";
 }
 
-hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
-  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return hipSuccess;
-  if ((a.K & 7) || (a.N & 3) || (a.lda & 7) || (a.ldw & 7) || (a.ldc & 3)) return hipErrorInvalidValue;
+hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
+  if (a0.M <= 0 || a0.N <= 0 || a0.K <= 0) return hipSuccess;
+  if ((a0.K & 7) || (a0.N & 3) || (a0.lda & 7) || (a0.ldw & 7) || (a0.ldc & 3)) return hipErrorInvalidValue;
+  GemmArgs a = a0;
+  const char* ns = getenv("MMF_GEMM_NOSTORE");  // benchmarking probe: main loop only, no epilogue traffic
+  if (ns && *ns == '1') a.c16 = nullptr, a.c32 = nullptr, a.res32 = nullptr, a.res16 = nullptr;
   switch (gemm_config(a)) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);
@@ -420,6 +462,7 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
     case 6: return run_glds<256, 192, 4, 2>(a, s);
     case 7: return run_glds<128, 192, 2, 2>(a, s);
     case 8: return run_glds<128, 128, 2, 2>(a, s);
+    case 9: return launch_pw(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

@@ -21,8 +21,11 @@ struct GemmArgs {
   int M, N, K, act;
 };
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
-int gemm_config(const GemmArgs& a);          // which tile instantiation launch_gemm picks (0..3)
+int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
 const char* gemm_config_name(int c);
+// streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable
+bool pw_applicable(const GemmArgs& a);
+hipError_t launch_pw(const GemmArgs& a, hipStream_t s);
 
 // LayerNorm over rows of width C (multiple of 256): y = LN(x [+ add]) * g + b.
 // x/add fp32 with row strides; writes fp32 y32 and/or bf16 y16.

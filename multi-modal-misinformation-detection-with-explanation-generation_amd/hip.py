@@ -38,6 +38,7 @@ SIGNATURES = {
     "mmf_profile_end": (_I, [_P, _I, _P, _P, _P, _P]),
     "mmf_profile_kind_name": (ctypes.c_char_p, [_I]),
     "mmf_gemm_bf16":(_I, [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "mmf_gemm_bf16_ex": (_I, [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P]),
     "mmf_attention_bf16": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }
 

@@ -156,3 +156,41 @@ def test_attention_vs_torch_fp32(lib, B, L, H, causal, masked):
     # P is rounded to bf16 before P.V (fp32 accumulate): ~2^-8 relative per term
     assert (got - ref).abs().max().item() < 2e-2
     assert (got - ref).abs().mean().item() < 2e-3
+
+
+# EfficientNet 1x1 convolutions (M = B*H*W pixels): expand (SiLU) and project (SE scale on A,
+# optional bf16 residual); shapes of the real blocks at small batch, plus ragged M / N tails.
+@pytest.mark.parametrize("M,N,K,act,scale,res", [
+    (8 * 3136, 96, 16, 3, False, False), (4 * 3136, 144, 24, 3, False, False), (2 * 784, 240, 40, 3, False, False),
+    (3 * 196, 480, 80, 3, False, False), (3 * 196, 672, 112, 3, False, False), (2 * 12544, 16, 32, 0, True, False),
+    (3 * 3136, 24, 96, 0, True, False), (3 * 3136, 24, 144, 0, True, True), (2 * 784, 40, 240, 0, True, True),
+    (5 * 49, 192, 1152, 0, True, True), (2 * 49, 320, 1152, 0, True, False), (4099, 40, 144, 0, True, True),
+    (2053, 136, 48, 3, False, False),
+])
+def test_gemm_effnet_convs(lib, M, N, K, act, scale, res):
+    import mmf_amd.hip as hip
+    g = torch.Generator().manual_seed(M + N + K)
+    rpb = {8 * 3136: 3136, 4 * 3136: 3136, 3 * 3136: 3136, 2 * 784: 784, 3 * 196: 196, 2 * 12544: 12544,
+           5 * 49: 49, 2 * 49: 49}.get(M, 1000)
+    A = _bf16(torch.randn(M, K, generator=g))
+    W = _bf16(torch.randn(N, K, generator=g) * (2.0 / K) ** 0.5)
+    bias = torch.randn(N, generator=g) * 0.1
+    S = torch.rand((M + rpb - 1) // rpb, K, generator=g) if scale else None
+    R = _bf16(torch.randn(M, N, generator=g)) if res else None
+    Af = A.float()
+    if scale:
+        Af = (Af * S.repeat_interleave(rpb, 0)[:M]).to(torch.bfloat16).float()  # A*s rounded to bf16
+    ref = _act(Af @ W.float().T + bias, act)
+    if res:
+        ref = ref + R.float()
+    dev = torch.device("cuda")
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    Sd = S.to(dev) if scale else None
+    Rd = R.to(dev) if res else None
+    out = torch.full((M, N), 7.0, device=dev, dtype=torch.bfloat16)
+    hip.check(lib.mmf_gemm_bf16_ex(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), hip.ptr(Sd), rpb,
+                                   out.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
+    torch.cuda.synchronize()
+    got = out.cpu().float()
+    scale_ = ref.abs().max().item()
+    assert ((got - ref).abs() <= ref.abs() * 2 ** -7 + 2e-5 * scale_).all()

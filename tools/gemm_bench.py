@@ -27,13 +27,59 @@ SHAPES = [
 ]
 
 
+# EfficientNet-B0 1x1 convolutions at B=256: (name, M, N, K, act, SE scale, bf16 residual, rows/image)
+EFFNET = [
+    ("e2.1", 256 * 12544, 96, 16, 3, 0, 0, 12544), ("e2.2", 256 * 3136, 144, 24, 3, 0, 0, 3136),
+    ("e3.2", 256 * 784, 240, 40, 3, 0, 0, 784), ("e4.2", 256 * 196, 480, 80, 3, 0, 0, 196),
+    ("e5.2", 256 * 196, 672, 112, 3, 0, 0, 196), ("e6.2", 256 * 49, 1152, 192, 3, 0, 0, 49),
+    ("p1", 256 * 12544, 16, 32, 0, 1, 0, 12544), ("p2.1", 256 * 3136, 24, 96, 0, 1, 0, 3136),
+    ("p2.2", 256 * 3136, 24, 144, 0, 1, 1, 3136), ("p3.1", 256 * 784, 40, 144, 0, 1, 0, 784),
+    ("p3.2", 256 * 784, 40, 240, 0, 1, 1, 784), ("p4.2", 256 * 196, 80, 480, 0, 1, 1, 196),
+    ("p5.2", 256 * 196, 112, 672, 0, 1, 1, 196), ("p6.2", 256 * 49, 192, 1152, 0, 1, 1, 49),
+    ("p7", 256 * 49, 320, 1152, 0, 1, 0, 49), ("head", 256 * 49, 1280, 320, 3, 0, 0, 49),
+]
+
+
+def effnet(a, lib, dev):
+    for name, M, N, K, act, sc, rs, rpb in EFFNET:
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        bias = torch.randn(N, device=dev)
+        S = torch.rand(M // rpb, K, device=dev) if sc else None
+        R = torch.randn(M, N, device=dev).to(torch.bfloat16) if rs else None
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        byts = 2.0 * M * (K + N + (N if rs else 0))
+        row = {"shape": name, "M": M, "N": N, "K": K, "MB": round(byts / 1e6, 1)}
+        for cfg in a.configs.split(","):
+            os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
+
+            def call():
+                hip.check(lib.mmf_gemm_bf16_ex(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R),
+                                               hip.ptr(S), rpb, C.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
+            call()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                call()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / a.iters * 1e3
+            row[cfg] = f"{us:.1f}us {byts / us / 1e6:.2f}TB/s"
+        os.environ["MMF_GEMM_CONFIG"] = ""
+        print(json.dumps(row), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="auto,3,4,5,6")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--noout", action="store_true", help="also time each shape with no epilogue stores")
     ap.add_argument("--kscale", default="", help="comma list of K multipliers to time (fixed-cost probe)")
+    ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
     a = ap.parse_args()
+    if a.effnet:
+        effnet(a, hip.load(), torch.device("cuda"))
+        return
     global SHAPES
     if a.kscale:
         SHAPES = [(f"{n}_k{m}", M, N, K * int(m), act, out) for n, M, N, K, act, out in SHAPES
@@ -66,9 +112,7 @@ def main():
             ms = e0.elapsed_time(e1) / a.iters
             row[cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
         if a.noout:
-            def call():
-                hip.check(lib.mmf_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None, None, None, N,
-                                            M, N, K, 0, hip.stream_ptr()))
+            os.environ["MMF_GEMM_NOSTORE"] = "1"
             for cfg in a.configs.split(","):
                 os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
                 call()
@@ -80,6 +124,7 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.iters
                 row["noout_" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+            os.environ["MMF_GEMM_NOSTORE"] = ""
         os.environ["MMF_GEMM_CONFIG"] = ""
         res.append(row)
         print(json.dumps(row), flush=True)
