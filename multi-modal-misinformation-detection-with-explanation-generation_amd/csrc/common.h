@@ -77,6 +77,12 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kOOB = 0x80000000u;  // an offset past every buffer the launchers allow
+// Cache policy of the raw-buffer epilogue stores: sc1 (bit 4).  Interleaved A/B on MI355X
+// (tools/ab_lib.py): 2-13 % faster encoder GEMMs at K <= 768, where every CU's epilogue writes
+// its tile in the same burst; neutral for the streaming 1x1 convolutions.
+#ifndef MMF_STORE_AUX
+#define MMF_STORE_AUX 16
+#endif
 MMF_DEV rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? (int)bytes : 0, 0x00020000);
 }
@@ -90,13 +96,13 @@ MMF_DEV uint2 buf_load_u2(rsrc_t r, uint32_t off) {
 }
 MMF_DEV void buf_store_f4(rsrc_t r, uint32_t off, float4 v) {
   const u32x4 w = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, MMF_STORE_AUX);
 }
 MMF_DEV void buf_store_u4(rsrc_t r, uint32_t off, uint4 v) {
   const u32x4 w = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, MMF_STORE_AUX);
 }
 MMF_DEV void buf_store_u2(rsrc_t r, uint32_t off, uint2 v) {
   const u32x2 w = {v.x, v.y};
-  __builtin_amdgcn_raw_buffer_store_b64(w, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, off, 0, MMF_STORE_AUX);
 }

@@ -69,51 +69,71 @@ __global__ __launch_bounds__(256) void stem_kernel(const void* src, const float*
   }
 }
 
-// grid (chunks, C/8/CGT, B); block = PL pixel lanes x CGT channel groups of 8
-template <int K>
-__global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* in, const float* w, const float* bias,
-                                                     bf16_t* out, float* pool_part, int H, int W, int C,
-                                                     int stride, int CGT, int PL, int pix_per_chunk) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sw = smem;                    // [K*K][CGT*8]
-  float* sb = sw + K * K * CGT * 8;    // [CGT*8]
-  float* red = sb + CGT * 8;           // [PL][CGT*8]
+// Depthwise kxk conv, LDS-tiled: a block owns a T x T output tile of one image and CW channels
+// (CW = 32 or 48, i.e. NG = 4 or 6 groups of 8).  The input tile with its halo
+// ((T-1)S + K)^2 x CW is read from HBM once, coalesced (zero padding written as zeros), and every
+// tap is then served from LDS; weights sit in LDS as [tap][CW] fp32.  Thread (px, g) computes
+// output pixels px, px + PX, ... for channel group g, so the SE pool partial of a channel stays in
+// one thread and is reduced across px in a fixed order (deterministic, no atomics): one partial
+// per (image, tile, channel).
+// grid (tiles_y * tiles_x, C / CW, B); block 256 threads (PX * NG of them active in phase 2)
+template <int K, int S>
+__global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* __restrict__ in, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                     float* __restrict__ pool_part, int H, int W, int C, int CW,
+                                                     int T, int tiles_x) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
+  constexpr int PAD = (K - 1) / 2;
+  const int NG = CW / 8, IT = (T - 1) * S + K;  // input tile edge
   const int tid = threadIdx.x;
-  const int ncw = CGT * 8, c0 = blockIdx.y * ncw;
-  const int bi = blockIdx.z;
-  for (int i = tid; i < K * K * ncw; i += blockDim.x) {
-    const int t = i / ncw, c = i % ncw;
+  const int bi = blockIdx.z, c0 = blockIdx.y * CW;
+  const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
+  const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+  const int oy0 = ty0 * T, ox0 = tx0 * T;
+  bf16_t* tile = (bf16_t*)dw_smem;                       // [IT][IT][CW]
+  float* sw = (float*)(dw_smem + (size_t)IT * IT * CW * 2);  // [K*K][CW]
+  float* sb = sw + K * K * CW;                           // [CW]
+  float* red = sb + CW;                                  // [PX][CW]
+
+  // ---- input tile (+halo) -> LDS ----
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  for (int idx = tid; idx < IT * IT * NG; idx += 256) {
+    const int g = idx % NG, pix = idx / NG;
+    const int ty = pix / IT, tx = pix - ty * IT;
+    const int iy = iy0 + ty, ix = ix0 + tx;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+      v = *reinterpret_cast<const uint4*>(in + (((size_t)bi * H + iy) * W + ix) * C + c0 + g * 8);
+    *reinterpret_cast<uint4*>(tile + (size_t)idx * 8) = v;
+  }
+  for (int i = tid; i < K * K * CW; i += 256) {
+    const int t = i / CW, c = i - t * CW;
     sw[i] = w[(size_t)(c0 + c) * K * K + t];
   }
-  for (int i = tid; i < ncw; i += blockDim.x) sb[i] = bias[c0 + i];
+  for (int i = tid; i < CW; i += 256) sb[i] = bias[c0 + i];
   __syncthreads();
-  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;  // pad = (K-1)/2
-  const int pad = (K - 1) / 2;
-  const int cgl = tid % CGT, pl = tid / CGT;
-  const int cl = cgl * 8;
+
+  const int PX = 256 / NG;
+  const int g = tid % NG, px = tid / NG;
   float psum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int p_begin = blockIdx.x * pix_per_chunk;
-  const int p_end = min(p_begin + pix_per_chunk, Ho * Wo);
-  if (pl < PL) {
-    for (int p = p_begin + pl; p < p_end; p += PL) {
-      const int oy = p / Wo, ox = p - oy * Wo;
+  if (px < PX) {
+    for (int p = px; p < T * T; p += PX) {
+      const int oy = p / T, ox = p - oy * T;
+      if (oy0 + oy >= Ho || ox0 + ox >= Wo) continue;
       float acc[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = sb[cl + j];
+      for (int j = 0; j < 8; ++j) acc[j] = sb[g * 8 + j];
 #pragma unroll
       for (int ky = 0; ky < K; ++ky) {
-        const int iy = oy * stride - pad + ky;
-        if (iy < 0 || iy >= H) continue;
 #pragma unroll
         for (int kx = 0; kx < K; ++kx) {
-          const int ix = ox * stride - pad + kx;
-          if (ix < 0 || ix >= W) continue;
-          const uint4 v = *reinterpret_cast<const uint4*>(in + (((size_t)bi * H + iy) * W + ix) * C + c0 + cl);
-          const float* ww = sw + (ky * K + kx) * ncw + cl;
-          acc[0] = fmaf(lo_bf(v.x), ww[0], acc[0]); acc[1] = fmaf(hi_bf(v.x), ww[1], acc[1]);
-          acc[2] = fmaf(lo_bf(v.y), ww[2], acc[2]); acc[3] = fmaf(hi_bf(v.y), ww[3], acc[3]);
-          acc[4] = fmaf(lo_bf(v.z), ww[4], acc[4]); acc[5] = fmaf(hi_bf(v.z), ww[5], acc[5]);
-          acc[6] = fmaf(lo_bf(v.w), ww[6], acc[6]); acc[7] = fmaf(hi_bf(v.w), ww[7], acc[7]);
+          const uint4 v = *reinterpret_cast<const uint4*>(tile + ((size_t)((oy * S + ky) * IT + ox * S + kx) * NG + g) * 8);
+          const float4 w0 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8);
+          const float4 w1 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8 + 4);
+          acc[0] = fmaf(lo_bf(v.x), w0.x, acc[0]); acc[1] = fmaf(hi_bf(v.x), w0.y, acc[1]);
+          acc[2] = fmaf(lo_bf(v.y), w0.z, acc[2]); acc[3] = fmaf(hi_bf(v.y), w0.w, acc[3]);
+          acc[4] = fmaf(lo_bf(v.z), w1.x, acc[4]); acc[5] = fmaf(hi_bf(v.z), w1.y, acc[5]);
+          acc[6] = fmaf(lo_bf(v.w), w1.z, acc[6]); acc[7] = fmaf(hi_bf(v.w), w1.w, acc[7]);
         }
       }
 #pragma unroll
@@ -121,19 +141,19 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* in, const flo
         acc[j] = act_apply(acc[j], ACT_SILU);
         psum[j] += acc[j];
       }
-      *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy) * Wo + ox) * C + c0 + cl) =
+      *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox) * C + c0 + g * 8) =
           make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]), pack2bf(acc[4], acc[5]),
                      pack2bf(acc[6], acc[7]));
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[pl * ncw + cl + j] = psum[j];
+    for (int j = 0; j < 8; ++j) red[px * CW + g * 8 + j] = psum[j];
   }
   __syncthreads();
-  // fixed-order reduction over pixel lanes -> one partial per (image, chunk, channel)
-  for (int c = tid; c < ncw; c += blockDim.x) {
-    float s = 0.f;
-    for (int q = 0; q < PL; ++q) s += red[q * ncw + c];
-    pool_part[((size_t)bi * gridDim.x + blockIdx.x) * C + c0 + c] = s;
+  // fixed-order reduction over pixel lanes -> one partial per (image, tile, channel)
+  for (int c = tid; c < CW; c += 256) {
+    float sum = 0.f;
+    for (int q = 0; q < PX; ++q) sum += red[q * CW + c];
+    pool_part[((size_t)bi * gridDim.x + blockIdx.x) * C + c0 + c] = sum;
   }
 }
 
@@ -219,39 +239,47 @@ hipError_t launch_effnet_stem_f32(const float* x, const float* w, const float* b
   return hipGetLastError();
 }
 
-static void dw_geometry(int H, int W, int C, int stride, int* CGT_, int* PL_, int* ppc_, int* nchunks_) {
-  const int CG = C / 8;
-  int CGT = 1;
-  for (int cand : {8, 6, 4, 3, 2, 1})
-    if (CG % cand == 0) { CGT = cand; break; }
-  const int PL = 256 / CGT;
+// tile edge: the largest divisor of the output edge up to 16 (stride 1) / 8 (stride 2)
+static void dw_geometry(int H, int W, int C, int stride, int* T_, int* CW_, int* tiles_x_, int* ntiles_) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  const int ppc = PL * 8;  // ~8 output pixels per thread per chunk
-  *CGT_ = CGT; *PL_ = PL; *ppc_ = ppc; *nchunks_ = (Ho * Wo + ppc - 1) / ppc;
+  const int cap = stride == 1 ? 16 : 8;
+  int T = 1;
+  for (int t = cap; t >= 1; --t)
+    if (Ho % t == 0) { T = t; break; }
+  const int tx = (Wo + T - 1) / T, ty = (Ho + T - 1) / T;
+  *T_ = T;
+  *CW_ = (C % 48 == 0) ? 48 : 32;
+  *tiles_x_ = tx;
+  *ntiles_ = tx * ty;
 }
 
 int dwconv_nchunks(int H, int W, int C, int stride) {
-  int a, b, c, n;
-  dw_geometry(H, W, C, stride, &a, &b, &c, &n);
+  int T, CW, tx, n;
+  dw_geometry(H, W, C, stride, &T, &CW, &tx, &n);
   return n;
 }
 
 hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part, int B,
                          int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s) {
-  if (C & 7) return hipErrorInvalidValue;
-  const int CG = C / 8;
-  int CGT, PL, ppc, nchunks;
-  dw_geometry(H, W, C, stride, &CGT, &PL, &ppc, &nchunks);
-  *nchunks_out = nchunks;
-  const size_t smem = (size_t)(k * k * CGT * 8 + CGT * 8 + PL * CGT * 8) * sizeof(float);
-  const dim3 grid(nchunks, CG / CGT, B), blk(PL * CGT);
-  if (k == 3)
-    hipLaunchKernelGGL(dwconv_kernel<3>, grid, blk, smem, s, in, w, bias, out, pool_part, H, W, C, stride, CGT, PL, ppc);
-  else if (k == 5)
-    hipLaunchKernelGGL(dwconv_kernel<5>, grid, blk, smem, s, in, w, bias, out, pool_part, H, W, C, stride, CGT, PL, ppc);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
+  int T, CW, tiles_x, ntiles;
+  dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
+  if (C % CW) return hipErrorInvalidValue;
+  *nchunks_out = ntiles;
+  const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8);
+  const size_t smem = (size_t)IT * IT * CW * 2 + (size_t)(k * k * CW + CW + PX * CW) * 4;
+  const dim3 grid(ntiles, C / CW, B), blk(256);
+#define MMF_DW(KK, SS)                                                                                        \
+  if (k == KK && stride == SS) {                                                                              \
+    hipLaunchKernelGGL((dwconv_kernel<KK, SS>), grid, blk, smem, s, in, w, bias, out, pool_part, H, W, C, CW, \
+                       T, tiles_x);                                                                           \
+    return hipGetLastError();                                                                                 \
+  }
+  MMF_DW(3, 1)
+  MMF_DW(3, 2)
+  MMF_DW(5, 1)
+  MMF_DW(5, 2)
+#undef MMF_DW
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,

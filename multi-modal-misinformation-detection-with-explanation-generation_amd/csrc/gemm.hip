@@ -281,6 +281,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, i
     // branch and no load that has to wait on the stores issued before it -- bias columns were
     // fetched at tile start and residual rows are loaded one fragment row AHEAD of the stores (one
     // vmcnt counter covers loads and stores in issue order).
+    if (!g.c16 && !g.c32) continue;  // nothing to store (MMF_GEMM_NOSTORE probe)
     if (!has_res && !g.c32) {
       // bf16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
       // fragment of each pair so every lane stores 16 contiguous bytes (half the store issues)

@@ -25,6 +25,8 @@ SHAPES = [
     ("txt_fc1", 19712, 2048, 512, 2, "16"), ("txt_fc2", 19712, 512, 2048, 0, "32r"),
     ("patch", 12544, 768, 3072, 0, "32"), ("sq4096", 4096, 4096, 4096, 0, "16"),
 ]
+# one persistent round of 256x256 tiles (256 tiles) at growing K: per-K-step slope vs fixed cost
+ROUND = [("round_k%d" % k, 8192, 2048, k, 0, "16") for k in (256, 512, 768, 1536, 3072, 6144)]
 
 
 # EfficientNet-B0 1x1 convolutions at B=256: (name, M, N, K, act, SE scale, bf16 residual, rows/image)
@@ -76,11 +78,14 @@ def main():
     ap.add_argument("--noout", action="store_true", help="also time each shape with no epilogue stores")
     ap.add_argument("--kscale", default="", help="comma list of K multipliers to time (fixed-cost probe)")
     ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
+    ap.add_argument("--round", action="store_true", help="one 256-tile round at K = 256 .. 6144")
     a = ap.parse_args()
     if a.effnet:
         effnet(a, hip.load(), torch.device("cuda"))
         return
     global SHAPES
+    if a.round:
+        SHAPES = ROUND
     if a.kscale:
         SHAPES = [(f"{n}_k{m}", M, N, K * int(m), act, out) for n, M, N, K, act, out in SHAPES
                   for m in a.kscale.split(",")]

@@ -26,10 +26,17 @@ def main():
     ap.add_argument("--csv", default="")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = list(c.execute("select name, duration, grid_x, workgroup_x from kernels"))
-    steps = sum(1 for r in rows if a.per_step_kernel in r[0]) or 1
+    rows = list(c.execute("select name, duration, grid_x, workgroup_x, start, end from kernels"))
+    marks = sorted(r[5] for r in rows if a.per_step_kernel in r[0])
+    if len(marks) >= 2:
+        # steady-state window: from the end of the first step to the end of the last one, so
+        # set-up work before the first step (vault encoding, warm-up compiles) is excluded
+        rows = [r for r in rows if r[4] >= marks[0] and r[5] <= marks[-1]]
+        steps = len(marks) - 1
+    else:
+        steps = 1
     agg = defaultdict(lambda: [0, 0.0])
-    for name, dur, gx, wx in rows:
+    for name, dur, gx, wx, _, _ in rows:
         key = short(name) + (f" grid={gx // max(wx, 1)}" if a.by_grid else "")
         agg[key][0] += 1
         agg[key][1] += dur / 1e3
