@@ -163,16 +163,23 @@ int dev_alloc(mmf_handle* h, void** p, size_t bytes, bool workspace = false) {
 }
 
 // ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
+// GEMM launches are profiled per (tile instantiation, activation) -- one kernel symbol each, so
+// the numbers line up with a rocprofv3 kernel trace of the same run.
+constexpr int kGemmActs = 5;
 enum ProfKind {
-  PK_GEMM0 = 0, PK_GEMM_LAST = 9, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE, PK_GAP,
-  PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
+  PK_GEMM0 = 0, PK_GEMM_LAST = 10 * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
+  PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
 };
 const char* prof_kind_name(int k) {
-  static const char* names[PK_COUNT] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                        "attention", "layernorm", "embed+ln", "clip_im2col", "effnet_stem",
-                                        "dwconv", "se", "gap_classifier", "text_heads", "vault", "fusion"};
-  if (k >= 0 && k <= PK_GEMM_LAST) return gemm_config_name(k);
-  return (k >= 0 && k < PK_COUNT) ? names[k] : "?";
+  static const char* names[PK_COUNT - PK_ATTN] = {"attention", "layernorm", "embed+ln", "clip_im2col", "effnet_stem",
+                                                  "dwconv", "se", "gap_classifier", "text_heads", "vault", "fusion"};
+  static char gemm_names[PK_GEMM_LAST + 1][64];
+  if (k >= 0 && k <= PK_GEMM_LAST) {
+    if (!gemm_names[k][0])
+      snprintf(gemm_names[k], sizeof(gemm_names[k]), "%s act=%d", gemm_config_name(k / kGemmActs), k % kGemmActs);
+    return gemm_names[k];
+  }
+  return (k >= PK_ATTN && k < PK_COUNT) ? names[k - PK_ATTN] : "?";
 }
 
 struct ProfScope {
@@ -447,7 +454,7 @@ GemmArgs gemm_args(const bf16_t* A, int lda, const Lin16& l, int M) {
 int gemm(mmf_handle* h, const GemmArgs& g, hipStream_t s) {
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
-  ProfScope ps(h, s, gemm_config(g), 2.0 * M * N * K, 2.0 * (M * K + N * K) + M * N * out_b);
+  ProfScope ps(h, s, gemm_config(g) * kGemmActs + g.act, 2.0 * M * N * K, 2.0 * (M * K + N * K) + M * N * out_b);
   HIPCHK(launch_gemm(g, s));
   return 0;
 }

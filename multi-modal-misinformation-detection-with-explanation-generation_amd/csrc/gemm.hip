@@ -196,8 +196,23 @@ MMF_DEV void glds_tile(const bf16_t* __restrict__ G, int ld, int row0, int rowma
   }
 }
 
+// Tile t -> (row panel, column panel).  gm > 0: grouped order -- gm row panels are walked
+// column by column, so the tiles one XCD runs together share A panels and W panels in its L2.
+MMF_DEV void tile_coords(int t, int tilesM, int tilesN, int gm, int& tm, int& tn) {
+  if (gm <= 0) {
+    tm = t / tilesN;
+    tn = t - tm * tilesN;
+    return;
+  }
+  const int per_group = gm * tilesN, group = t / per_group, first_m = group * gm;
+  const int gsz = min(tilesM - first_m, gm), r = t - group * per_group;
+  tm = first_m + r % gsz;
+  tn = r / gsz;
+}
+
 template <int BM, int BN, int WGM, int WGN, int ACT>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles) {
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
+                                                                  int gm) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
   // K-slab of the NEXT tile is DMA'd into the free LDS stage during the current tile's last
   // K-step, so only the very first tile pays the load latency and each epilogue's stores drain
@@ -233,7 +248,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, i
   int t = wgid;
   if (t >= tiles) return;
   auto stage = [&](int buf, int tile, int kt) {
-    const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
+    int tm_, tn_;
+    tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);
     bf16_t* nb = lds + buf * STAGE;
     glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
     glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
@@ -242,7 +258,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_glds_kernel(GemmArgs g, i
   __syncthreads();
   int cur = 0;
   for (; t < tiles; t += nwg) {
-    const int tm = t / tilesN, tn = t - tm * tilesN;
+    int tm, tn;
+    tile_coords(t, tilesM, tilesN, gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     f32x4 acc[NI][MI];
 #pragma unroll
@@ -372,9 +389,12 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int per_cu = (BM == 128) ? 2 : 1;  // co-resident workgroups per CU (LDS / VGPR budget)
   const int grid = tiles < 256 * per_cu ? tiles : 256 * per_cu;
   const dim3 blk(64 * WGM * WGN);
+  const char* gme = getenv("MMF_GEMM_GROUPM");  // tile-order override (tools/ab_env.py)
+  const int gm = (gme && *gme) ? atoi(gme) : 0;
 #define MMF_GLDS_CASE(ACT)                                                                                  \
   case ACT:                                                                                                 \
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT>), dim3(grid), blk, 0, s, a, tilesN, tiles); \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT>), dim3(grid), blk, 0, s, a, tilesN, tiles, tilesM, \
+                       gm);                                                                                      \
     break;
   switch (a.act) {
     MMF_GLDS_CASE(ACT_NONE)

@@ -7,15 +7,20 @@ the op must move) by measured device time, so it is a lower bound on utilisation
 from __future__ import annotations
 
 import ctypes
+import glob
+import json
+import os
+import re
 from typing import Callable, Dict, List
 
 import torch
 
 from .hip import check
 
+PROFILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0
-NK = 32
+NK = 128
 
 
 def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:
@@ -47,6 +52,32 @@ def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:
     return rows
 
 
+def kind_symbol(kind: str) -> str:
+    """Event-profile kind -> kernel symbol as rocprofv3 prints it (GEMM kinds only)."""
+    m = re.match(r"gemm_(glds|bf16)<([\d,]+)> act=(\d)", kind)
+    if not m:
+        return kind
+    dims = m.group(2).split(",")
+    if m.group(1) == "glds":
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3)])}>"
+    return f"gemm_bf16_kernel<{', '.join(dims)}>"
+
+
+def pmc_traffic(symbol: str, path: str | None = None) -> float | None:
+    """HBM bytes per launch of `symbol` from the committed rocprofv3 PMC passes
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    files = [path] if path else sorted(glob.glob(os.path.join(PROFILES, "r*_pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for row in d.get("all_kernels", []):
+            if row["kernel"] == symbol:
+                return float(row["hbm_bytes_per_launch"])
+    return None
+
+
 def kernel_roofline(eng, step: Callable[[], None], steps: int) -> Dict:
     rows = profile_kernels(eng, step, steps)
     dom = rows[0]
@@ -56,7 +87,9 @@ def kernel_roofline(eng, step: Callable[[], None], steps: int) -> Dict:
         ach, peak, unit = dom["gbs"], PEAK_HBM_GBS, "GB/s"
     total = sum(r["ms_per_step"] for r in rows)
     return {"bound": dom["bound"], "kernel": dom["kernel"], "achieved": round(ach, 1), "peak": peak,
-            "unit": unit, "frac": round(ach / peak, 4), "traffic": None,
+            "unit": unit, "frac": round(ach / peak, 4), "traffic": pmc_traffic(kind_symbol(dom["kernel"])),
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
+            "symbol": kind_symbol(dom["kernel"]),
             "avg_launch_us": round(dom["avg_launch_us"], 2),
             "algorithmic_per_launch": round(dom["flops_per_launch"] if dom["bound"] == "mfma"
                                             else dom["bytes_per_launch"], 1),
