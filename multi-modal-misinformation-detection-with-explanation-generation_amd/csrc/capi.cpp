@@ -167,7 +167,7 @@ int dev_alloc(mmf_handle* h, void** p, size_t bytes, bool workspace = false) {
 // the numbers line up with a rocprofv3 kernel trace of the same run.
 constexpr int kGemmActs = 5;
 enum ProfKind {
-  PK_GEMM0 = 0, PK_GEMM_LAST = 10 * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
+  PK_GEMM0 = 0, PK_GEMM_LAST = 13 * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
   PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
 };
 const char* prof_kind_name(int k) {
@@ -473,6 +473,13 @@ int lnorm(mmf_handle* h, const float* x, int ldx, const LNp& p, float* y32, int 
   return 0;
 }
 
+int add_ln(mmf_handle* h, float* x, int ldx, const bf16_t* y, int ldy, const LNp& p, float* s32, float* o32,
+           bf16_t* o16, int ldo, int rows, int C, hipStream_t s) {
+  ProfScope ps(h, s, PK_LN, 9.0 * rows * C, (double)rows * C * (4 + 2 + (s32 ? 4 : 0) + (o32 ? 4 : 0) + 2));
+  HIPCHK(launch_add_ln(x, ldx, y, ldy, p.g, p.b, 1e-5f, s32, o32, o16, ldo, rows, C, s));
+  return 0;
+}
+
 int check_cap(mmf_handle* h, int B, int Lr, int Lc) {
   if (B <= 0) return fail(MMF_EINVAL, "batch must be > 0 (got %d)", B);
   if (B > h->cap_b || Lr > h->cap_lr || Lc > h->cap_lc)
@@ -499,6 +506,25 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
     // last layer: only the CLS row feeds the heads (misinfo_forensics.py:95), so the rows below
     // run on B compact CLS rows (strided A / residual reads) instead of B*L rows
     const bool last = (i == 11);
+    if (!last) {
+      // out-proj and FFN-2 write their bf16 branch output y; the residual add happens in fp32
+      // inside add+LN (y lives in r_h, free until FFN-1, then in r_ctx, free after out-proj)
+      bf16_t* y = w.r_h;
+      g = gemm_args(w.r_ctx, 768, Ly.o, M);
+      g.c16 = y;
+      CHK(gemm(h, g, s));
+      CHK(add_ln(h, w.r_x, 768, y, 768, Ly.ln1, nullptr, w.r_x, w.r_xb, 768, M, 768, s));
+      g = gemm_args(w.r_xb, 768, Ly.fc1, M);
+      g.act = 1;  // GELU-erf
+      g.c16 = w.r_h;
+      CHK(gemm(h, g, s));
+      y = w.r_ctx;
+      g = gemm_args(w.r_h, 3072, Ly.fc2, M);
+      g.c16 = y;
+      CHK(gemm(h, g, s));
+      CHK(add_ln(h, w.r_x, 768, y, 768, Ly.ln2, nullptr, w.r_x, w.r_xb, 768, M, 768, s));
+      continue;
+    }
     const int Mr = last ? B : M;            // rows after the attention
     const int rs = last ? L * 768 : 768;    // row stride of ctx / residual stream at this point
     g = gemm_args(w.r_ctx, rs, Ly.o, Mr);
@@ -555,23 +581,21 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
       CHK(gemm(h, g, s));
       break;
     }
+    // out-proj / FFN-2 write their bf16 branch output y (out-proj into `hid`, free until FFN-1;
+    // FFN-2 into `ctx`, free after out-proj); add+LN adds it to the fp32 residual stream x in place
     g = gemm_args(ctx, H, Ly.o, M);
-    g.res32 = x;
-    g.c32 = x;
+    g.c16 = hid;
     CHK(gemm(h, g, s));
-    CHK(lnorm(h, x, H, Ly.ln2, nullptr, 0, xb, H, M, H, s));
+    CHK(add_ln(h, x, H, hid, H, Ly.ln2, x, nullptr, xb, H, M, H, s));
     g = gemm_args(xb, H, Ly.fc1, M);
     g.act = 2;  // quick_gelu
     g.c16 = hid;
     CHK(gemm(h, g, s));
     g = gemm_args(hid, I, Ly.fc2, M);
-    g.res32 = x;
-    g.c32 = x;
+    g.c16 = ctx;
     CHK(gemm(h, g, s));
-    if (i + 1 < 12) {
-      const EncLayer& Nx = layers[i + 1];
-      CHK(lnorm(h, x, H, Nx.ln1, nullptr, 0, xb, H, M, H, s));
-    }
+    // layer i + 1 < 12 always holds here (layer 11 takes the compact branch above)
+    CHK(add_ln(h, x, H, ctx, H, layers[i + 1].ln1, x, nullptr, xb, H, M, H, s));
   }
   return 0;
 }

@@ -19,6 +19,7 @@ struct GemmArgs {
   const float* ascale;           // per-(batch, k) fp32 scale of A (SE excitation) or null
   int rows_per_batch;            // rows of A per batch item when ascale != null
   int M, N, K, act;
+  int probe;                     // benchmarking probes (0 in production; see gemm.hip)
 };
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
@@ -32,6 +33,11 @@ hipError_t launch_pw(const GemmArgs& a, hipStream_t s);
 hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd, const float* g, const float* b,
                             float eps, float* y32, int ldy32, bf16_t* y16, int ldy16, int rows, int C,
                             hipStream_t s);
+
+// Residual add + LayerNorm: s = x (fp32, row stride ldx) + y (bf16 GEMM output, ldy); optionally
+// s32 = s, o32 = LN(s) (both with stride ldx; may alias x); o16 = LN(s) bf16 (ldo).  C in {512, 768}.
+hipError_t launch_add_ln(const float* x, int ldx, const bf16_t* y, int ldy, const float* g, const float* b, float eps,
+                         float* s32, float* o32, bf16_t* o16, int ldo, int rows, int C, hipStream_t s);
 
 // Fused multi-head attention, head_dim 64, L <= 128: qkv bf16 [B*L][ldqkv] with q at col h*64,
 // k at D + h*64, v at 2D + h*64 (D = H*64); mask int32 [B][L] (1 keep) or null; out bf16 [B*L][ldo].

@@ -68,6 +68,35 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx,
   store_row<NV>(v, y32 ? y32 + (size_t)row * ldy32 : nullptr, y16 ? y16 + (size_t)row * ldy16 : nullptr, lane);
 }
 
+// Residual add + LayerNorm after an out-projection / FFN-2 GEMM whose bf16 output y is the
+// residual branch: s = x + y in fp32 (x = fp32 residual stream), then
+//   pre-LN (CLIP, TF clip:357-385):   s32 = s (the new residual stream), o16 = LN(s)
+//   post-LN (RoBERTa, TF roberta:329-399): o32 = LN(s) (the new residual stream), o16 = LN(s)
+// s32 / o32 may alias x (each wave reads its whole row before writing it).
+template <int NV>
+__global__ __launch_bounds__(256) void add_ln_kernel(const float* x, int ldx, const bf16_t* y, int ldy, const float* g,
+                                                     const float* b, float eps, float* s32, float* o32,
+                                                     bf16_t* o16, int ldo, int rows) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float4 v[NV];
+  uint2 a[NV];
+  const float* xr = x + (size_t)row * ldx;
+  const bf16_t* yr = y + (size_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i] = *reinterpret_cast<const float4*>(xr + (i * 64 + lane) * 4);
+    a[i] = *reinterpret_cast<const uint2*>(yr + (i * 64 + lane) * 4);
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i].x += lo_bf(a[i].x); v[i].y += hi_bf(a[i].x); v[i].z += lo_bf(a[i].y); v[i].w += hi_bf(a[i].y);
+  }
+  if (s32) store_row<NV>(v, s32 + (size_t)row * ldx, nullptr, lane);
+  ln_row<NV>(v, g, b, eps, NV * 256, lane);
+  store_row<NV>(v, o32 ? o32 + (size_t)row * ldx : nullptr, o16 + (size_t)row * ldo, lane);
+}
+
 // RoBERTa: position ids = cumsum(ids != pad) * (ids != pad) + pad (TF roberta:142-155);
 // x = LN(word[id] + type[0] + pos[pid]).  One block per sequence.
 template <int NV>
@@ -229,6 +258,19 @@ hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd
   else if (C == 512)
     hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, x, ldx, add, ldadd, g, b, eps, y32, ldy32, y16,
                        ldy16, rows);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_add_ln(const float* x, int ldx, const bf16_t* y, int ldy, const float* g, const float* b, float eps,
+                         float* s32, float* o32, bf16_t* o16, int ldo, int rows, int C, hipStream_t s) {
+  const dim3 grid((rows + 3) / 4);
+  if (!o16) return hipErrorInvalidValue;
+  if (C == 768)
+    hipLaunchKernelGGL(add_ln_kernel<3>, grid, dim3(256), 0, s, x, ldx, y, ldy, g, b, eps, s32, o32, o16, ldo, rows);
+  else if (C == 512)
+    hipLaunchKernelGGL(add_ln_kernel<2>, grid, dim3(256), 0, s, x, ldx, y, ldy, g, b, eps, s32, o32, o16, ldo, rows);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

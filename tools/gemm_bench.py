@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--kscale", default="", help="comma list of K multipliers to time (fixed-cost probe)")
     ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
     ap.add_argument("--round", action="store_true", help="one 256-tile round at K = 256 .. 6144")
+    ap.add_argument("--nodefer", action="store_true", help="also time each config with MMF_GEMM_DEFER=0")
+    ap.add_argument("--probe", default="", help="MMF_GEMM_PROBE bits for an extra timed pass (1: drop bf16 stores)")
     a = ap.parse_args()
     if a.effnet:
         effnet(a, hip.load(), torch.device("cuda"))
@@ -116,6 +118,34 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
             row[cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+        if a.probe:
+            os.environ["MMF_GEMM_PROBE"] = a.probe
+            for cfg in a.configs.split(","):
+                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
+                call()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    call()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                row["probe_" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+            os.environ["MMF_GEMM_PROBE"] = ""
+        if a.nodefer:
+            os.environ["MMF_GEMM_DEFER"] = "0"
+            for cfg in a.configs.split(","):
+                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
+                call()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    call()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                row["nodefer_" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+            os.environ["MMF_GEMM_DEFER"] = ""
         if a.noout:
             os.environ["MMF_GEMM_NOSTORE"] = "1"
             for cfg in a.configs.split(","):
