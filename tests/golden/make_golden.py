@@ -1,6 +1,7 @@
 """Generate the golden fixtures by running the REFERENCE code itself (build container only).
 
     python tests/golden/make_golden.py            # writes tests/golden/golden.npz + golden.json
+    python tests/golden/make_golden.py --video    # writes tests/golden/golden_video.json
 
 What runs: ``/root/reference/misinfo_forensics.py`` and ``clip_similarity_engine.py`` are
 imported unmodified.  Because the build container has no network, weights or tokenizer
@@ -63,7 +64,8 @@ def crc(a: np.ndarray) -> int:
     return zlib.crc32(np.ascontiguousarray(a).tobytes())
 
 
-def main():
+def setup():
+    """The reference objects and inputs shared by every fixture section."""
     torch.manual_seed(0)
     torch.set_num_threads(max(1, os.cpu_count() or 1))
     tv_stub.install()
@@ -143,6 +145,57 @@ def main():
     mf.efficientnet_transform = tv_stub.Compose([
         tv_stub.Resize((224, 224)), tv_stub.ToTensor(),
         tv_stub.Normalize(mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])])
+    return dict(ref=ref, ref_cse=ref_cse, det=det, clip=clip, clipq=clipq, eos_id=eos_id, proc=proc, pil=pil,
+                texts=texts, imgs=imgs, mf=mf, rob_table=rob_table, clip_table=clip_table, rob_ids=rob_ids,
+                rob_mask=rob_mask, clip_ids=clip_ids, clip_mask=clip_mask, t_ids=t_ids, t_lens=t_lens,
+                raw_img_emb=raw_img_emb, vault_base_crc=vault_base_crc)
+
+
+def video_fixtures(S) -> dict:
+    """analyze_video / analyze(video_path=...) (misinfo_forensics.py:493-573, 812-829) run by the
+    reference against cv2_stub (OpenCV is absent) on the video_fixture.py inputs."""
+    import cv2_stub
+    from video_fixture import ANALYZE_CALLS, VIDEO_CALLS, VIDEOS, bgr_videos, video_vault
+    cv2_stub.install(bgr_videos(S["imgs"]))
+    mf, texts = S["mf"], S["texts"]
+    saved = mf.vault_embeddings
+    mf.vault_embeddings = video_vault(syn.vault(N_VAULT, 512, SEED_VAULT), S["raw_img_emb"])
+    js = {"calls": [], "analyze": [], "errors": {}}
+    for vid, ti, mx, st in VIDEO_CALLS:
+        r = mf.analyze_video(vid, text=texts[ti] if ti is not None else None, max_frames=mx, stride_seconds=st)
+        bf = r.pop("best_frame")
+        r["best_frame_sample"] = (None if bf is None else
+                                  next(i for i in VIDEOS[vid]["frames"] if np.array_equal(np.asarray(bf), S["imgs"][i])))
+        js["calls"].append({"video": vid, "text": ti, "max_frames": mx, "stride_seconds": st, "result": r})
+    for vid, ti in ANALYZE_CALLS:
+        r = mf.analyze(text=texts[ti] if ti is not None else None, video_path=vid, verbose=False)
+        js["analyze"].append({"video": vid, "text": ti, "result": r})
+    for vid in ("v_empty.mp4", "missing.mp4"):
+        try:
+            mf.analyze_video(vid)
+        except RuntimeError as e:
+            js["errors"][vid] = str(e)
+    mf.vault_embeddings = saved
+    return js
+
+
+def main_video():
+    S = setup()
+    js = video_fixtures(S)
+    with open(os.path.join(HERE, "golden_video.json"), "w") as f:
+        json.dump(js, f, indent=1, default=float)
+    print("wrote", os.path.join(HERE, "golden_video.json"))
+
+
+def main():
+    S = setup()
+    globals().update(S)
+    ref, ref_cse, det, clip, clipq, eos_id, proc, pil, texts, imgs, mf = (
+        S["ref"], S["ref_cse"], S["det"], S["clip"], S["clipq"], S["eos_id"], S["proc"], S["pil"], S["texts"],
+        S["imgs"], S["mf"])
+    rob_table, clip_table, rob_ids, rob_mask, clip_ids, clip_mask = (
+        S["rob_table"], S["clip_table"], S["rob_ids"], S["rob_mask"], S["clip_ids"], S["clip_mask"])
+    t_ids, t_lens, raw_img_emb, vault_base_crc = S["t_ids"], S["t_lens"], S["raw_img_emb"], S["vault_base_crc"]
 
     out = {}
     js = {"analyze": [], "analyze_text_only": [], "analyze_image_only": [], "clip_engine": [],
@@ -246,4 +299,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--video" in sys.argv:
+        main_video()
+    else:
+        main()

@@ -112,3 +112,42 @@ def test_api_fails_loudly_without_hip():
         pytest.skip("has a GPU")
     with pytest.raises(RuntimeError, match="HIP device"):
         MisinfoForensics(synthetic_seed=0, device="cpu", verbose=False)
+
+
+def test_video_frame_sampling_matches_reference():
+    """sample_video_frames (misinfo_forensics.py:501-548 sampling) against the frames the reference
+    itself consumed in tests/golden/golden_video.json (best frame + errors), cv2 replaced by the
+    frame-replay stub; and the reference's error without OpenCV."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import cv2_stub
+    import video_fixture as VF
+    import mmf_amd.synthetic as syn
+    from mmf_amd.api import sample_video_frames
+    saved = sys.modules.pop("cv2", None)
+    try:
+        with pytest.raises(RuntimeError) as e:
+            sample_video_frames("v_stride.mp4")
+        assert "opencv-python is required for video analysis" in str(e.value)
+        imgs = syn.images(8, 1234)
+        cv2_stub.install(VF.bgr_videos(imgs))
+        with open(os.path.join(os.path.dirname(__file__), "golden", "golden_video.json")) as f:
+            gv = json.load(f)
+        for c in gv["calls"]:
+            frames = sample_video_frames(c["video"], c["max_frames"], c["stride_seconds"])
+            fps = VF.VIDEOS[c["video"]]["fps"] or 25.0
+            stride = max(1, int(round(fps * max(0.1, c["stride_seconds"]))))
+            want = VF.VIDEOS[c["video"]]["frames"][::stride][:c["max_frames"]]
+            assert len(frames) == len(want)
+            for fr, s in zip(frames, want):
+                assert np.array_equal(np.asarray(fr), imgs[s])
+            assert c["result"]["best_frame_sample"] in want
+        assert sample_video_frames("v_empty.mp4") == []
+        with pytest.raises(RuntimeError) as e:
+            sample_video_frames("missing.mp4")
+        assert str(e.value) == gv["errors"]["missing.mp4"]
+    finally:
+        sys.modules.pop("cv2", None)
+        if saved is not None:
+            sys.modules["cv2"] = saved

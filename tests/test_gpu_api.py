@@ -130,3 +130,88 @@ def test_clip_similarity_engine(golden, golden_json, golden_inputs, clip_sd, tmp
     with pytest.raises(ValueError) as e:
         eng.calculate_similarity(str(tmp_path / "img0.png"), "")
     assert str(e.value) == errs[1]["msg"]
+
+
+def test_analyze_video_matches_reference(forensics, golden, golden_json, golden_inputs):
+    """analyze_video / analyze(video_path=...) (misinfo_forensics.py:493-573, 812-829) against the
+    reference's own results (tests/golden/golden_video.json; OpenCV replaced by the frame-replay
+    stub on both sides).  All frames of a video go through one batched EfficientNet / CLIP /
+    vault pass here; the reference ran 3 single-image passes per frame."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import cv2_stub
+    import video_fixture as VF
+    import mmf_amd.synthetic as syn
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden_video.json")) as f:
+        gv = json.load(f)
+    imgs = golden_inputs["imgs"]
+    cv2_stub.install(VF.bgr_videos(imgs))
+    seeds = golden_json["meta"]["seeds"]
+    forensics.set_vault(VF.video_vault(syn.vault(2170, 512, seeds[2]), golden["clip_image_features_raw"]),
+                        golden_inputs["meta"])
+    try:
+        for c in gv["calls"]:
+            ref = c["result"]
+            got = forensics.analyze_video(c["video"], text=f"sample text {c['text']}" if c["text"] is not None else None,
+                                          max_frames=c["max_frames"], stride_seconds=c["stride_seconds"])
+            for k in ("deepfake_score", "clip_similarity", "vault_discrepancy"):
+                assert abs(got[k] - ref[k]) < TOL, (c, k, got[k], ref[k])
+            assert abs(got["text_similarity"] - ref["text_similarity"]) < 2e-3
+            assert [m["title"] for m in got["vault_matches"]] == [m["title"] for m in ref["vault_matches"]]
+            for a, b in zip(got["vault_matches"], ref["vault_matches"]):
+                assert abs(a["similarity"] - b["similarity"]) < TOL
+            assert np.array_equal(np.asarray(got["best_frame"]), imgs[ref["best_frame_sample"]])
+        for a in gv["analyze"]:
+            got = forensics.analyze(text=f"sample text {a['text']}" if a["text"] is not None else None,
+                                    video_path=a["video"], verbose=False)
+            _check(got, a["result"])
+        for vid, msg in gv["errors"].items():
+            with pytest.raises(RuntimeError) as e:
+                forensics.analyze_video(vid)
+            assert str(e.value) == msg
+    finally:
+        sys.modules.pop("cv2", None)
+        forensics.set_vault(golden_inputs["vault"], golden_inputs["meta"])
+
+
+def test_vault_builder_on_hip(clip_sd, tmp_path):
+    """generate_embeddings_database (train_clip_detective.py:457-607) with the HIP CLIP towers,
+    weights loaded from a CLIPDetective-format checkpoint ('model_state_dict' with 'clip.' keys),
+    against the CPU oracle's normalised embeddings."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from tables import TableClipProcessor
+    from PIL import Image
+    import mmf_amd.synthetic as syn
+    from mmf_amd import io_utils
+    from mmf_amd.vault_builder import generate_embeddings_database
+    from oracle import models as M
+    n = 40
+    imgs = syn.images(n, 91)
+    lens = [(7 * i) % 76 + 2 for i in range(n)]
+    ids, _ = syn.clip_ids(n, 77, 92, lens)
+    table, arts = {}, []
+    for i in range(n):
+        p = str(tmp_path / f"a{i}.png")
+        Image.fromarray(imgs[i]).save(p)
+        table[f"t{i}"] = ids[i, :lens[i]].tolist()
+        arts.append({"article_id": i, "text_content": f"t{i}", "image_local_path": p})
+    (tmp_path / "seed.json").write_text(json.dumps(arts))
+    ck = str(tmp_path / "clip_detective_best.pth")
+    torch.save({"model_state_dict": {"clip." + k: torch.as_tensor(v) for k, v in clip_sd.items()},
+                "epoch": 3, "val_accuracy": 0.9}, ck)
+    db = generate_embeddings_database(ck, str(tmp_path / "seed.json"), str(tmp_path / "vault.pkl"),
+                                      processor=TableClipProcessor(table), batch=16)
+    assert db["article_ids"] == list(range(n)) and db["metadata"]["val_accuracy"] == 0.9
+    sd = M.to_torch(clip_sd)
+    with torch.no_grad():
+        px = np.stack([io_utils.clip_pixels(Image.fromarray(imgs[i])) for i in range(n)])
+        ie = M.l2n(M.clip_image_features(sd, M.clip_preprocess(torch.as_tensor(px)))).numpy()
+        msk = (np.arange(77)[None] < np.asarray(lens)[:, None]).astype(np.int32)
+        te = M.l2n(M.clip_text_features(sd, torch.as_tensor(ids), torch.as_tensor(msk))).numpy()
+    assert (db["image_embeddings"] * ie).sum(1).min() > 1 - 1e-4
+    assert (db["text_embeddings"] * te).sum(1).min() > 1 - 1e-4
+    emb, meta = io_utils.load_vault(str(tmp_path / "vault.pkl"))
+    assert emb.shape == (n, 512) and meta[3]["title"] == "t3"

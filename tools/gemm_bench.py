@@ -15,14 +15,15 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import mmf_amd.hip as hip  # noqa: E402
 
-# (name, M, N, K, act, out) at B=256: RoBERTa L=128, ViT L=50, CLIP text L=77
+# (name, M, N, K, act, out) at B=256: RoBERTa L=128, ViT L=50, CLIP text L=77 (out-proj / FFN-2
+# write their bf16 branch output; the fp32 residual add happens in add+LN)
 SHAPES = [
-    ("rob_qkv", 32768, 2304, 768, 0, "16"), ("rob_o", 32768, 768, 768, 0, "32r"),
-    ("rob_fc1", 32768, 3072, 768, 1, "16"), ("rob_fc2", 32768, 768, 3072, 0, "32r"),
-    ("vit_qkv", 12800, 2304, 768, 0, "16"), ("vit_o", 12800, 768, 768, 0, "32r"),
-    ("vit_fc1", 12800, 3072, 768, 2, "16"), ("vit_fc2", 12800, 768, 3072, 0, "32r"),
-    ("txt_qkv", 19712, 1536, 512, 0, "16"), ("txt_o", 19712, 512, 512, 0, "32r"),
-    ("txt_fc1", 19712, 2048, 512, 2, "16"), ("txt_fc2", 19712, 512, 2048, 0, "32r"),
+    ("rob_qkv", 32768, 2304, 768, 0, "16"), ("rob_o", 32768, 768, 768, 0, "16"),
+    ("rob_fc1", 32768, 3072, 768, 1, "16"), ("rob_fc2", 32768, 768, 3072, 0, "16"),
+    ("vit_qkv", 12800, 2304, 768, 0, "16"), ("vit_o", 12800, 768, 768, 0, "16"),
+    ("vit_fc1", 12800, 3072, 768, 2, "16"), ("vit_fc2", 12800, 768, 3072, 0, "16"),
+    ("txt_qkv", 19712, 1536, 512, 0, "16"), ("txt_o", 19712, 512, 512, 0, "16"),
+    ("txt_fc1", 19712, 2048, 512, 2, "16"), ("txt_fc2", 19712, 512, 2048, 0, "16"),
     ("patch", 12544, 768, 3072, 0, "32"), ("sq4096", 4096, 4096, 4096, 0, "16"),
 ]
 # one persistent round of 256x256 tiles (256 tiles) at growing K: per-K-step slope vs fixed cost
@@ -80,6 +81,7 @@ def main():
     ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
     ap.add_argument("--round", action="store_true", help="one 256-tile round at K = 256 .. 6144")
     ap.add_argument("--nodefer", action="store_true", help="also time each config with MMF_GEMM_DEFER=0")
+    ap.add_argument("--env", default="", help="extra timed pass per config with these VAR=VAL[;VAR=VAL] set")
     ap.add_argument("--probe", default="", help="MMF_GEMM_PROBE bits for an extra timed pass (1: drop bf16 stores)")
     a = ap.parse_args()
     if a.effnet:
@@ -118,6 +120,22 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
             row[cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+        for spec in [e for e in a.env.split("/") if e]:
+            kv = dict(x.split("=") for x in spec.split(";"))
+            os.environ.update(kv)
+            for cfg in a.configs.split(","):
+                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
+                call()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    call()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                row[spec + ":" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
+            for k in kv:
+                os.environ[k] = ""
         if a.probe:
             os.environ["MMF_GEMM_PROBE"] = a.probe
             for cfg in a.configs.split(","):
