@@ -4,9 +4,14 @@
 //   CLIP txt L=77,   8 heads, causal + key-padding mask  (TF clip:494-590)
 // One workgroup (4 waves) per (sequence, head).  K (row-major, XOR-swizzled) and V (transposed
 // [d][key]) of the whole head live in LDS; each wave takes 16-query tiles:
-//   S = Q K^T   (v_mfma_f32_16x16x32_bf16, Q fragments straight from global/L2)
-//   fp32 masked softmax in registers (rows spread over 16 lanes -> 4 xor-shuffles)
-//   O^T = V^T P^T so each lane ends with 4 consecutive head dims of one query (8-B stores).
+//   S^T = K Q^T (v_mfma_f32_16x16x32_bf16 with K as the A operand, Q fragments straight from
+//         global/L2): each lane ends with 4 consecutive KEYS of one query
+//   fp32 masked softmax in registers (a query's keys sit in 4 lanes -> 2 xor-shuffles)
+//   O^T = V^T P^T with P^T taken straight from the softmax registers as the MFMA B operand: the
+//         lane's 4 + 4 keys of a 32-key block are its two key tiles' values, so the contraction
+//         runs over keys in that permuted order and V^T is read with the same permutation (two
+//         8-B reads) -- P never round-trips through LDS.  Each lane ends with 4 consecutive head
+//         dims of one query (8-B stores).
 #include "common.h"
 #include "kernels.h"
 
@@ -20,8 +25,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
                                                         int ldo, int L, int H, int causal) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[LMAX * 64];
   __shared__ __attribute__((aligned(16))) bf16_t Vt[64 * VT_LD];
-  __shared__ __attribute__((aligned(16))) bf16_t Ps[4][16 * VT_LD];
-  __shared__ float kbias[LMAX];
+  __shared__ __attribute__((aligned(16))) float kbias[LMAX];
 
   const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
   const int D = H * 64;
@@ -51,7 +55,6 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
 
   const int fr = lane & 15, fg = lane >> 4;
   const int nqt = (L + 15) >> 4, nkt = Lk >> 4;
-  bf16_t* P = Ps[wave];
 
   for (int qt = wave; qt < nqt; qt += 4) {
     // Q fragments: row q = qt*16 + fr, dims 32*ks + 8*fg .. +7
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
         qf[ks] = as_bf16x8(v);
       }
     }
-    // S[q][key]: lane holds rows q = qt*16 + fg*4 + r, key = j*16 + fr
+    // S^T[key][q]: lane holds keys j*16 + fg*4 + r (r = 0..3) of query q = qt*16 + fr
     f32x4 s[LMAX / 16];
 #pragma unroll
     for (int j = 0; j < LMAX / 16; ++j) {
@@ -75,82 +78,73 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
         for (int ks = 0; ks < 2; ++ks) {
           const int key = j * 16 + fr, kc = ks * 4 + fg;
           const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + key * 64 + ((kc ^ (key & 7)) << 3)));
-          s[j] = mfma16x16x32(qf[ks], kf, s[j]);
+          s[j] = mfma16x16x32(kf, qf[ks], s[j]);
         }
       }
     }
-    // masked softmax (fp32), scale 1/sqrt(64)
-    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    // masked softmax over keys (fp32), scale 1/sqrt(64)
+    const int qq = qt * 16 + fr;
+    float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < LMAX / 16; ++j) {
       if (j < nkt) {
-        const int key = j * 16 + fr;
-        const float kb = kbias[key];
+        const float4 kb = *reinterpret_cast<const float4*>(kbias + j * 16 + fg * 4);
+        const float kbr[4] = {kb.x, kb.y, kb.z, kb.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int q = qt * 16 + fg * 4 + r;
-          float v = s[j][r] * 0.125f + kb;
-          if (causal && key > q) v = -INFINITY;
+          float v = s[j][r] * 0.125f + kbr[r];
+          if (causal && j * 16 + fg * 4 + r > qq) v = -INFINITY;
           s[j][r] = v;
-          mx[r] = fmaxf(mx[r], v);
+          mx = fmaxf(mx, v);
         }
       }
     }
-    float sum[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
-      sum[r] = 0.f;
-    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < LMAX / 16; ++j) {
       if (j < nkt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = (mx[r] == -INFINITY) ? 0.f : __expf(s[j][r] - mx[r]);
+          const float e = (mx == -INFINITY) ? 0.f : __expf(s[j][r] - mx);
           s[j][r] = e;
-          sum[r] += e;
+          sum += e;
         }
       }
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
-      sum[r] = sum[r] > 0.f ? 1.0f / sum[r] : 0.f;
-    }
-    // P (bf16, normalised) -> this wave's LDS tile [q][key]
-#pragma unroll
-    for (int j = 0; j < LMAX / 16; ++j) {
-      if (j < nkt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) P[(fg * 4 + r) * VT_LD + j * 16 + fr] = f2bf(s[j][r] * sum[r]);
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed
-    __builtin_amdgcn_wave_barrier();
-    // O^T[d][q] = sum_key V^T[d][key] P^T[key][q]; lane: d = dt*16 + fg*4 + r, q = qt*16 + fr
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+    // O^T[d][q] = sum_key V^T[d][key] P^T[key][q] over 32-key blocks; B operand of lane (fr, fg):
+    // k-index 8fg + i <-> key 32kb + 4fg + i (i < 4, tile 2kb) / 32kb + 16 + 4fg + (i - 4) (tile 2kb+1)
     f32x4 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kk = 0; kk < Lk; kk += 32) {
-      const bf16x8 pf = as_bf16x8(*reinterpret_cast<const uint4*>(P + fr * VT_LD + kk + fg * 8));
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8 vf = as_bf16x8(*reinterpret_cast<const uint4*>(Vt + (dt * 16 + fr) * VT_LD + kk + fg * 8));
-        o[dt] = mfma16x16x32(vf, pf, o[dt]);
+    for (int kb = 0; kb < LMAX / 32; ++kb) {
+      if (kb * 32 < Lk) {
+        const uint4 pk = make_uint4(pack2bf(s[2 * kb][0] * inv, s[2 * kb][1] * inv),
+                                    pack2bf(s[2 * kb][2] * inv, s[2 * kb][3] * inv),
+                                    pack2bf(s[2 * kb + 1][0] * inv, s[2 * kb + 1][1] * inv),
+                                    pack2bf(s[2 * kb + 1][2] * inv, s[2 * kb + 1][3] * inv));
+        const bf16x8 pf = as_bf16x8(pk);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16_t* vr = Vt + (dt * 16 + fr) * VT_LD + kb * 32 + fg * 4;
+          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+          o[dt] = mfma16x16x32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pf, o[dt]);
+        }
       }
     }
-    const int q = qt * 16 + fr;
-    if (q < L) {
-      bf16_t* dst = out + ((size_t)bi * L + q) * ldo + h * 64 + fg * 4;
+    if (qq < L) {
+      bf16_t* dst = out + ((size_t)bi * L + qq) * ldo + h * 64 + fg * 4;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         *reinterpret_cast<uint2*>(dst + dt * 16) =
             make_uint2(pack2bf(o[dt][0], o[dt][1]), pack2bf(o[dt][2], o[dt][3]));
     }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 

@@ -667,16 +667,23 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
   int H = 112, W = 112;
   for (const EffBlock& b : h->e_blocks) {
     const bf16_t* src = cur;
-    if (b.expand != 1) {
+    int nch = 0;
+    const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
+    const char* fe = getenv("MMF_FUSE_EXPAND");  // MMF_FUSE_EXPAND=0: separate expand launch (A/B)
+    const bool fuse = b.expand != 1 && expand_dw_applicable(b.cin, b.cexp) && !(fe && *fe == '0');
+    if (fuse) {
+      ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k + 2.0 * B * H * W * b.cin * b.cexp,
+                   (double)B * 2 * ((double)H * W * b.cin * (b.cexp / 48) + (double)Ho * Wo * b.cexp));
+      HIPCHK(launch_expand_dw(cur, b.cin, b.e.w, b.e.b, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride,
+                              &nch, s));
+    } else if (b.expand != 1) {
       GemmArgs g = gemm_args(cur, b.cin, b.e, B * H * W);
       g.act = 3;  // SiLU
       g.c16 = w.e_exp;
       CHK(gemm(h, g, s));
       src = w.e_exp;
     }
-    int nch = 0;
-    const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
-    {
+    if (!fuse) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k,
                    (double)B * b.cexp * 2 * ((double)H * W + (double)Ho * Wo));
       HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s));

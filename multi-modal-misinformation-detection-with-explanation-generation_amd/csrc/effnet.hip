@@ -69,6 +69,60 @@ __global__ __launch_bounds__(256) void stem_kernel(const void* src, const float*
   }
 }
 
+// Depthwise kxk + BN + SiLU + SE pool partial from an LDS input tile [IT][IT][CW] (zero padding
+// already materialised): thread (px, g) computes output pixels px, px + PX, ... of channel group g,
+// so the pool partial of a channel stays in one thread and is reduced across px in a fixed order
+// (deterministic, no atomics): one partial per (image, tile, channel).
+template <int K, int S>
+MMF_DEV void dw_compute(const bf16_t* tile, const float* sw, const float* sb, float* red, bf16_t* __restrict__ out,
+                        float* __restrict__ pool_part, int bi, int c0, int oy0, int ox0, int Ho, int Wo, int C,
+                        int CW, int T, int IT) {
+  const int tid = threadIdx.x, NG = CW / 8;
+  const int PX = 256 / NG;
+  const int g = tid % NG, px = tid / NG;
+  float psum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (px < PX) {
+    for (int p = px; p < T * T; p += PX) {
+      const int oy = p / T, ox = p - oy * T;
+      if (oy0 + oy >= Ho || ox0 + ox >= Wo) continue;
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = sb[g * 8 + j];
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const uint4 v = *reinterpret_cast<const uint4*>(tile + ((size_t)((oy * S + ky) * IT + ox * S + kx) * NG + g) * 8);
+          const float4 w0 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8);
+          const float4 w1 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8 + 4);
+          acc[0] = fmaf(lo_bf(v.x), w0.x, acc[0]); acc[1] = fmaf(hi_bf(v.x), w0.y, acc[1]);
+          acc[2] = fmaf(lo_bf(v.y), w0.z, acc[2]); acc[3] = fmaf(hi_bf(v.y), w0.w, acc[3]);
+          acc[4] = fmaf(lo_bf(v.z), w1.x, acc[4]); acc[5] = fmaf(hi_bf(v.z), w1.y, acc[5]);
+          acc[6] = fmaf(lo_bf(v.w), w1.z, acc[6]); acc[7] = fmaf(hi_bf(v.w), w1.w, acc[7]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[j] = act_apply(acc[j], ACT_SILU);
+        psum[j] += acc[j];
+      }
+      *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox) * C + c0 + g * 8) =
+          make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]), pack2bf(acc[4], acc[5]),
+                     pack2bf(acc[6], acc[7]));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[px * CW + g * 8 + j] = psum[j];
+  }
+  __syncthreads();
+  // fixed-order reduction over pixel lanes -> one partial per (image, tile, channel)
+  const int ntiles = gridDim.x;
+  for (int c = tid; c < CW; c += 256) {
+    float sum = 0.f;
+    for (int q = 0; q < PX; ++q) sum += red[q * CW + c];
+    pool_part[((size_t)bi * ntiles + blockIdx.x) * C + c0 + c] = sum;
+  }
+}
+
 // Depthwise kxk conv, LDS-tiled: a block owns a T x T output tile of one image and CW channels
 // (CW = 32 or 48, i.e. NG = 4 or 6 groups of 8).  The input tile with its halo
 // ((T-1)S + K)^2 x CW is read from HBM once, coalesced (zero padding written as zeros), and every
@@ -113,81 +167,155 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* __restrict__ 
   for (int i = tid; i < CW; i += 256) sb[i] = bias[c0 + i];
   __syncthreads();
 
-  const int PX = 256 / NG;
-  const int g = tid % NG, px = tid / NG;
-  float psum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (px < PX) {
-    for (int p = px; p < T * T; p += PX) {
-      const int oy = p / T, ox = p - oy * T;
-      if (oy0 + oy >= Ho || ox0 + ox >= Wo) continue;
-      float acc[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = sb[g * 8 + j];
-#pragma unroll
-      for (int ky = 0; ky < K; ++ky) {
-#pragma unroll
-        for (int kx = 0; kx < K; ++kx) {
-          const uint4 v = *reinterpret_cast<const uint4*>(tile + ((size_t)((oy * S + ky) * IT + ox * S + kx) * NG + g) * 8);
-          const float4 w0 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8);
-          const float4 w1 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8 + 4);
-          acc[0] = fmaf(lo_bf(v.x), w0.x, acc[0]); acc[1] = fmaf(hi_bf(v.x), w0.y, acc[1]);
-          acc[2] = fmaf(lo_bf(v.y), w0.z, acc[2]); acc[3] = fmaf(hi_bf(v.y), w0.w, acc[3]);
-          acc[4] = fmaf(lo_bf(v.z), w1.x, acc[4]); acc[5] = fmaf(hi_bf(v.z), w1.y, acc[5]);
-          acc[6] = fmaf(lo_bf(v.w), w1.z, acc[6]); acc[7] = fmaf(hi_bf(v.w), w1.w, acc[7]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        acc[j] = act_apply(acc[j], ACT_SILU);
-        psum[j] += acc[j];
-      }
-      *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox) * C + c0 + g * 8) =
-          make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]), pack2bf(acc[4], acc[5]),
-                     pack2bf(acc[6], acc[7]));
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[px * CW + g * 8 + j] = psum[j];
-  }
-  __syncthreads();
-  // fixed-order reduction over pixel lanes -> one partial per (image, tile, channel)
-  for (int c = tid; c < CW; c += 256) {
-    float sum = 0.f;
-    for (int q = 0; q < PX; ++q) sum += red[q * CW + c];
-    pool_part[((size_t)bi * gridDim.x + blockIdx.x) * C + c0 + c] = sum;
-  }
+  dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
 }
 
-// One block per image.  w2t is fc2's weight transposed to [Csq][C] (packed at load) so every
-// k-step of both matvecs is one coalesced row read; fc1 partial dots are spread over all waves.
-__global__ __launch_bounds__(256) void se_kernel(const float* pool_part, int nchunks, float inv_hw, const float* w1,
-                                                 const float* b1, const float* w2t, const float* b2, float* scale,
-                                                 int C, int Csq) {
+// MBConv front, fused: 1x1 expand (BN folded) + SiLU computed per input tile on the MFMA, straight
+// into the depthwise conv's LDS tile, then the depthwise conv of dwconv_kernel.  The expanded
+// activation (6x the block's input channels, the largest tensor of the block) never touches HBM:
+// the block reads its Cin-channel input (once per 48-channel group, plus the halo) instead of
+// writing and re-reading Cexp channels.  Used where Cin <= 64 (the high-resolution stages 2-4,
+// where that tensor dominates the image tower's traffic); elsewhere expand is its own launch.
+//  expand: E[pix][c] = SiLU(be[c] + sum_k X[pix][k] We[c][k]) as D = We . X^T on
+//          v_mfma_f32_16x16x32_bf16 (A = We rows of this channel group, B = 16 tile pixels), each
+//          lane ends with 4 consecutive channels of one pixel -> 8-B LDS writes; pixels outside the
+//          image are written as 0 (the depthwise conv zero-pads E, not X).
+// grid (tiles, Cexp / CW, B); block 256 threads; KS = ceil(Cin / 32) <= 2
+template <int K, int S, int KS>
+__global__ __launch_bounds__(256) void expand_dw_kernel(const bf16_t* __restrict__ x, int Cin,
+                                                        const bf16_t* __restrict__ we, const float* __restrict__ be,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        bf16_t* __restrict__ out, float* __restrict__ pool_part, int H,
+                                                        int W, int C, int CW, int T, int tiles_x) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
+  constexpr int PAD = (K - 1) / 2, KP = KS * 32;
+  const int NG = CW / 8, NF = CW / 16, IT = (T - 1) * S + K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int bi = blockIdx.z, c0 = blockIdx.y * CW;
+  const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
+  const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+  const int oy0 = ty0 * T, ox0 = tx0 * T;
+  bf16_t* tile = (bf16_t*)dw_smem;                          // [IT][IT][CW]
+  float* sw = (float*)(dw_smem + (size_t)IT * IT * CW * 2);  // [K*K][CW]
+  float* sb = sw + K * K * CW;                              // [CW]
+  float* red = sb + CW;                                     // [PX][CW]
+  float* sbe = red + (256 / NG) * CW;                       // [CW] expand bias
+  bf16_t* swe = (bf16_t*)(sbe + CW);                        // [CW][KP] expand weights (zero-padded K)
+
+  for (int i = tid; i < CW * (KP / 8); i += 256) {
+    const int r = i / (KP / 8), kc = i - r * (KP / 8);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (kc * 8 < Cin) v = *reinterpret_cast<const uint4*>(we + (size_t)(c0 + r) * Cin + kc * 8);
+    *reinterpret_cast<uint4*>(swe + r * KP + kc * 8) = v;
+  }
+  for (int i = tid; i < K * K * CW; i += 256) {
+    const int t = i / CW, c = i - t * CW;
+    sw[i] = w[(size_t)(c0 + c) * K * K + t];
+  }
+  for (int i = tid; i < CW; i += 256) {
+    sb[i] = bias[c0 + i];
+    sbe[i] = be[c0 + i];
+  }
+  __syncthreads();
+
+  // ---- expand the input tile (+halo) into LDS ----
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  const int npix = IT * IT, nrf = (npix + 15) / 16;
+  for (int rf = wave; rf < nrf; rf += 4) {
+    const int pix = rf * 16 + fr;
+    const int ty = pix / IT, tx = pix - ty * IT;
+    const int iy = iy0 + ty, ix = ix0 + tx;
+    const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    bf16x8 xf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 32 + fg * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (inimg && k < Cin) v = *reinterpret_cast<const uint4*>(x + (((size_t)bi * H + iy) * W + ix) * Cin + k);
+      xf[ks] = as_bf16x8(v);
+    }
+    for (int nf = 0; nf < NF; ++nf) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 wf = as_bf16x8(*reinterpret_cast<const uint4*>(swe + (nf * 16 + fr) * KP + ks * 32 + fg * 8));
+        acc = mfma16x16x32(wf, xf[ks], acc);
+      }
+      if (pix < npix) {
+        const int cl = nf * 16 + fg * 4;
+        const float4 b = *reinterpret_cast<const float4*>(sbe + cl);
+        float e[4] = {acc[0] + b.x, acc[1] + b.y, acc[2] + b.z, acc[3] + b.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) e[r] = inimg ? act_apply(e[r], ACT_SILU) : 0.f;
+        *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + cl) = make_uint2(pack2bf(e[0], e[1]), pack2bf(e[2], e[3]));
+      }
+    }
+  }
+  __syncthreads();
+  dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
+}
+
+// Squeeze-excitation, one 1024-thread block per image.  The three phases are each a few dependent
+// L2 round trips, so the kernel is latency-bound: every phase keeps many independent loads in
+// flight (unrolled partial sums) instead of walking dependent chains.
+//   pool : pooled[c] = sum over the dwconv's per-tile partials (fixed order) / HW
+//   fc1  : s1[o] = SiLU(b1[o] + w1[o,:] . pooled)  -- each of the 16 waves owns <= 4 outputs and
+//          accumulates them together (lanes stride over C), then one wave reduction per output
+//   fc2  : scale[c] = sigmoid(b2[c] + sum_j w2t[j][c] s1[j])  (w2t = fc2 weight transposed at load,
+//          so consecutive threads read consecutive addresses)
+constexpr int SE_THREADS = 1024;
+
+__global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, int nchunks, float inv_hw,
+                                                        const float* w1, const float* b1, const float* w2t,
+                                                        const float* b2, float* scale, int C, int Csq) {
   __shared__ float pooled[1280];
   __shared__ float s1[64];
   const int bi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* pp = pool_part + (size_t)bi * nchunks * C;
-  for (int c = tid; c < C; c += 256) {
-    float s = 0.f;
-    for (int k = 0; k < nchunks; ++k) s += pp[(size_t)k * C + c];
-    pooled[c] = s * inv_hw;
-  }
-  __syncthreads();
-  for (int o = wave; o < Csq; o += 4) {
-    const float* wr = w1 + (size_t)o * C;
-    float a0 = 0.f, a1 = 0.f;
-    int c = lane;
-    for (; c + 64 < C; c += 128) {
-      a0 = fmaf(wr[c], pooled[c], a0);
-      a1 = fmaf(wr[c + 64], pooled[c + 64], a1);
+  for (int c = tid; c < C; c += SE_THREADS) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int k = 0;
+    for (; k + 4 <= nchunks; k += 4) {
+      a0 += pp[(size_t)k * C + c];
+      a1 += pp[(size_t)(k + 1) * C + c];
+      a2 += pp[(size_t)(k + 2) * C + c];
+      a3 += pp[(size_t)(k + 3) * C + c];
     }
-    if (c < C) a0 = fmaf(wr[c], pooled[c], a0);
-    const float a = wave_sum(a0 + a1);
-    if (lane == 0) s1[o] = act_apply(a + b1[o], ACT_SILU);
+    for (; k < nchunks; ++k) a0 += pp[(size_t)k * C + c];
+    pooled[c] = ((a0 + a1) + (a2 + a3)) * inv_hw;
   }
   __syncthreads();
-  for (int c = tid; c < C; c += 256) {
-    float a = b2[c];
-    for (int j = 0; j < Csq; ++j) a = fmaf(w2t[(size_t)j * C + c], s1[j], a);
+  {
+    constexpr int OPW = 4;  // outputs per wave (Csq <= 64 = 16 waves x 4)
+    float acc[OPW] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < OPW; ++t) {
+      const int o = wave + 16 * t;
+      if (o < Csq) {
+        const float* wr = w1 + (size_t)o * C;
+        for (int c = lane; c < C; c += 64) acc[t] = fmaf(wr[c], pooled[c], acc[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < OPW; ++t) {
+      const int o = wave + 16 * t;
+      const float a = wave_sum(acc[t]);
+      if (o < Csq && lane == 0) s1[o] = act_apply(a + b1[o], ACT_SILU);
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += SE_THREADS) {
+    float a0 = b2[c], a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int j = 0;
+    for (; j + 4 <= Csq; j += 4) {
+      a0 = fmaf(w2t[(size_t)j * C + c], s1[j], a0);
+      a1 = fmaf(w2t[(size_t)(j + 1) * C + c], s1[j + 1], a1);
+      a2 = fmaf(w2t[(size_t)(j + 2) * C + c], s1[j + 2], a2);
+      a3 = fmaf(w2t[(size_t)(j + 3) * C + c], s1[j + 3], a3);
+    }
+    for (; j < Csq; ++j) a0 = fmaf(w2t[(size_t)j * C + c], s1[j], a0);
+    const float a = (a0 + a1) + (a2 + a3);
     scale[(size_t)bi * C + c] = 1.0f / (1.0f + expf(-a));
   }
 }
@@ -282,10 +410,34 @@ hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf
   return hipErrorInvalidValue;
 }
 
+bool expand_dw_applicable(int cin, int cexp) { return cin <= 64 && (cin % 8) == 0 && (cexp % 48) == 0; }
+
+hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const float* be, const float* w,
+                            const float* bias, bf16_t* out, float* pool_part, int B, int H, int W, int C, int k,
+                            int stride, int* nchunks_out, hipStream_t s) {
+  int T, CW, tiles_x, ntiles;
+  dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
+  if (!expand_dw_applicable(cin, C) || CW != 48) return hipErrorInvalidValue;
+  *nchunks_out = ntiles;
+  const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8), KS = (cin + 31) / 32;
+  const size_t smem = (size_t)IT * IT * CW * 2 + (size_t)(k * k * CW + CW + PX * CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
+  const dim3 grid(ntiles, C / CW, B), blk(256);
+#define MMF_EDW(KK, SS, QS)                                                                                      \
+  if (k == KK && stride == SS && KS == QS) {                                                                     \
+    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS>), grid, blk, smem, s, x, cin, we, be, w, bias, out, pool_part, \
+                       H, W, C, CW, T, tiles_x);                                                                 \
+    return hipGetLastError();                                                                                    \
+  }
+  MMF_EDW(3, 1, 1) MMF_EDW(3, 2, 1) MMF_EDW(5, 1, 1) MMF_EDW(5, 2, 1)
+  MMF_EDW(3, 1, 2) MMF_EDW(3, 2, 2) MMF_EDW(5, 1, 2) MMF_EDW(5, 2, 2)
+#undef MMF_EDW
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s) {
   if (C > 1280 || Csq > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(se_kernel, dim3(B), dim3(256), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2, b2, scale, C, Csq);
+  hipLaunchKernelGGL(se_kernel, dim3(B), dim3(SE_THREADS), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2, b2, scale, C, Csq);
   return hipGetLastError();
 }
 

@@ -98,5 +98,11 @@ hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const fl
 hipError_t launch_gap_classifier(const bf16_t* x, int HW, int C, const float* w, const float* b, float* logits,
                                  float* score, int score_stride, int B, hipStream_t s);
 hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);
+// fused MBConv front: expand 1x1 (we bf16 [C][cin], be fp32, BN folded) + SiLU computed per input
+// tile into LDS, then the depthwise conv of launch_dwconv (same outputs, same pool partials)
+bool expand_dw_applicable(int cin, int cexp);
+hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const float* be, const float* w,
+                            const float* bias, bf16_t* out, float* pool_part, int B, int H, int W, int C, int k,
+                            int stride, int* nchunks_out, hipStream_t s);
 // number of pool-partial chunks launch_dwconv uses for an output of Ho x Wo with C channels
 int dwconv_nchunks(int H, int W, int C, int stride);

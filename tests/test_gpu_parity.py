@@ -94,3 +94,17 @@ def test_batch_invariance_full_size(engine, det_sd):
         np.testing.assert_array_equal(a[40:48], b, err_msg=k)
     s = full["scores"].cpu().numpy()
     assert ((s[:, :3] >= 0) & (s[:, :3] <= 1)).all() and (np.abs(s[:, 3]) <= 1 + 1e-5).all()
+
+
+def test_fused_expand_dwconv_bit_identical(engine, monkeypatch):
+    """The fused MBConv front (1x1 expand computed per tile into the depthwise conv's LDS tile)
+    produces bit-identical EfficientNet outputs to the separate expand GEMM + depthwise launches
+    (same MFMA operand order over K, same bias / SiLU / bf16 rounding), on a full 256 batch."""
+    import mmf_amd.synthetic as syn
+    imgs = syn.images(256, 17)
+    monkeypatch.setenv("MMF_FUSE_EXPAND", "0")
+    lg0, _ = engine.effnet_forward(imgs)
+    monkeypatch.setenv("MMF_FUSE_EXPAND", "1")
+    lg1, _ = engine.effnet_forward(imgs)
+    torch.cuda.synchronize()
+    assert torch.equal(lg0, lg1)
