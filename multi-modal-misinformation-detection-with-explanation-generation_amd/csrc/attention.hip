@@ -2,15 +2,17 @@
 //   RoBERTa  L=128, 12 heads, key-padding mask          (TF roberta:158-251)
 //   CLIP ViT L=50,  12 heads, no mask                    (TF clip:280-333)
 //   CLIP txt L=77,   8 heads, causal + key-padding mask  (TF clip:494-590)
-// One workgroup (4 waves) per (sequence, head).  K (row-major, XOR-swizzled) and V (transposed
-// [d][key]) of the whole head live in LDS; each wave takes 16-query tiles:
+// One workgroup (4 waves) per (sequence, head).  K and V of the whole head live in LDS row-major
+// ([key][64], 16-B chunks XOR-swizzled by key & 7, both staged with 16-B stores); each wave takes
+// 16-query tiles:
 //   S^T = K Q^T (v_mfma_f32_16x16x32_bf16 with K as the A operand, Q fragments straight from
 //         global/L2): each lane ends with 4 consecutive KEYS of one query
 //   fp32 masked softmax in registers (a query's keys sit in 4 lanes -> 2 xor-shuffles)
 //   O^T = V^T P^T with P^T taken straight from the softmax registers as the MFMA B operand: the
 //         lane's 4 + 4 keys of a 32-key block are its two key tiles' values, so the contraction
-//         runs over keys in that permuted order and V^T is read with the same permutation (two
-//         8-B reads) -- P never round-trips through LDS.  Each lane ends with 4 consecutive head
+//         runs over keys in that permuted order and V^T is read with the same permutation by
+//         two ds_read_b64_tr_b16 (4 keys x 16 dims, transposed in the LDS read path) -- P never
+//         round-trips through LDS, V is never transposed by scalar stores.  Each lane ends with 4 consecutive head
 //         dims of one query (8-B stores).
 #include "common.h"
 #include "kernels.h"
@@ -18,13 +20,16 @@
 namespace {
 
 constexpr int LMAX = 128;
-constexpr int VT_LD = LMAX + 8;   // padded row of the transposed V / P tiles (272 B)
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+MMF_DEV int kv_swz(int key, int kc) { return key * 64 + ((kc ^ (key & 7)) << 3); }
 
 __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict__ qkv, int ld,
                                                         const int32_t* __restrict__ mask, bf16_t* __restrict__ out,
                                                         int ldo, int L, int H, int causal) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[LMAX * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[64 * VT_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[LMAX * 64];
   __shared__ __attribute__((aligned(16))) float kbias[LMAX];
 
   const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
@@ -33,7 +38,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
   const int Lk = (L + 31) & ~31;  // keys padded to the 32-deep PV k-step
   const bf16_t* base = qkv + (size_t)bi * L * ld;
 
-  // stage K (swizzled rows) and V^T; zero the padded keys so 0 * pad stays finite
+  // stage K and V (swizzled rows); zero the padded keys so 0 * pad stays finite
   for (int c = tid; c < Lk * 8; c += 256) {
     const int key = c >> 3, kc = c & 7;
     uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
@@ -41,13 +46,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
       kv = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + D + h * 64 + kc * 8);
       vv = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + 2 * D + h * 64 + kc * 8);
     }
-    *reinterpret_cast<uint4*>(Ks + key * 64 + ((kc ^ (key & 7)) << 3)) = kv;
-    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      Vt[(kc * 8 + 2 * j) * VT_LD + key] = (bf16_t)(w[j] & 0xffff);
-      Vt[(kc * 8 + 2 * j + 1) * VT_LD + key] = (bf16_t)(w[j] >> 16);
-    }
+    *reinterpret_cast<uint4*>(Ks + kv_swz(key, kc)) = kv;
+    *reinterpret_cast<uint4*>(Vs + kv_swz(key, kc)) = vv;
   }
   for (int k = tid; k < Lk; k += 256)
     kbias[k] = (k < L && (!mask || mask[(size_t)bi * L + k])) ? 0.f : -INFINITY;
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const int key = j * 16 + fr, kc = ks * 4 + fg;
-          const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + key * 64 + ((kc ^ (key & 7)) << 3)));
+          const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
           s[j] = mfma16x16x32(kf, qf[ks], s[j]);
         }
       }
@@ -129,12 +129,16 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
                                     pack2bf(s[2 * kb + 1][0] * inv, s[2 * kb + 1][1] * inv),
                                     pack2bf(s[2 * kb + 1][2] * inv, s[2 * kb + 1][3] * inv));
         const bf16x8 pf = as_bf16x8(pk);
+        // A operand V^T[d = dt*16 + fr][keys 32kb + 4fg + 0..3 | 32kb + 16 + 4fg + 0..3]: lane
+        // 4q + p of each 16-lane group addresses key row (.. + q), dims dt*16 + 4p .. +3
+        const int key0 = kb * 32 + fg * 4 + (fr >> 2), p = fr & 3;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
-          const bf16_t* vr = Vt + (dt * 16 + fr) * VT_LD + kb * 32 + fg * 4;
-          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-          o[dt] = mfma16x16x32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pf, o[dt]);
+          const int c = dt * 2 + (p >> 1), e = (p & 1) * 4;
+          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + kv_swz(key0, c) + e));
+          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + kv_swz(key0 + 16, c) + e));
+          const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+          o[dt] = mfma16x16x32(as_bf16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
         }
       }
     }

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(const bf16_t* __restrict
   const int NG = CW / 8, NF = CW / 16, IT = (T - 1) * S + K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int bi = blockIdx.z, c0 = blockIdx.y * CW;
+  const int bi = blockIdx.z;
   const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   const int oy0 = ty0 * T, ox0 = tx0 * T;
@@ -203,57 +203,72 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(const bf16_t* __restrict
   float* sbe = red + (256 / NG) * CW;                       // [CW] expand bias
   bf16_t* swe = (bf16_t*)(sbe + CW);                        // [CW][KP] expand weights (zero-padded K)
 
-  for (int i = tid; i < CW * (KP / 8); i += 256) {
-    const int r = i / (KP / 8), kc = i - r * (KP / 8);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (kc * 8 < Cin) v = *reinterpret_cast<const uint4*>(we + (size_t)(c0 + r) * Cin + kc * 8);
-    *reinterpret_cast<uint4*>(swe + r * KP + kc * 8) = v;
-  }
-  for (int i = tid; i < K * K * CW; i += 256) {
-    const int t = i / CW, c = i - t * CW;
-    sw[i] = w[(size_t)(c0 + c) * K * K + t];
-  }
-  for (int i = tid; i < CW; i += 256) {
-    sb[i] = bias[c0 + i];
-    sbe[i] = be[c0 + i];
-  }
-  __syncthreads();
-
-  // ---- expand the input tile (+halo) into LDS ----
+  // this wave's input-pixel fragments first: their HBM latency overlaps the weight staging
+  constexpr int MAXRF = 6;  // ceil(ceil(IT^2 / 16) / 4) for IT <= 19 (host-checked)
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
   const int npix = IT * IT, nrf = (npix + 15) / 16;
-  for (int rf = wave; rf < nrf; rf += 4) {
-    const int pix = rf * 16 + fr;
+  uint4 xr[MAXRF][KS];
+#pragma unroll
+  for (int it = 0; it < MAXRF; ++it) {
+    const int pix = (wave + 4 * it) * 16 + fr;
     const int ty = pix / IT, tx = pix - ty * IT;
     const int iy = iy0 + ty, ix = ix0 + tx;
     const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    bf16x8 xf[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = ks * 32 + fg * 8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (inimg && k < Cin) v = *reinterpret_cast<const uint4*>(x + (((size_t)bi * H + iy) * W + ix) * Cin + k);
-      xf[ks] = as_bf16x8(v);
-    }
-    for (int nf = 0; nf < NF; ++nf) {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 wf = as_bf16x8(*reinterpret_cast<const uint4*>(swe + (nf * 16 + fr) * KP + ks * 32 + fg * 8));
-        acc = mfma16x16x32(wf, xf[ks], acc);
-      }
-      if (pix < npix) {
-        const int cl = nf * 16 + fg * 4;
-        const float4 b = *reinterpret_cast<const float4*>(sbe + cl);
-        float e[4] = {acc[0] + b.x, acc[1] + b.y, acc[2] + b.z, acc[3] + b.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) e[r] = inimg ? act_apply(e[r], ACT_SILU) : 0.f;
-        *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + cl) = make_uint2(pack2bf(e[0], e[1]), pack2bf(e[2], e[3]));
-      }
+      xr[it][ks] = (inimg && k < Cin) ? *reinterpret_cast<const uint4*>(x + (((size_t)bi * H + iy) * W + ix) * Cin + k)
+                                      : make_uint4(0, 0, 0, 0);
     }
   }
-  __syncthreads();
-  dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
+  // every 48-channel group of the block's Cexp channels, reusing the input fragments above
+  for (int c0 = 0; c0 < C; c0 += CW) {
+    for (int i = tid; i < CW * (KP / 8); i += 256) {
+      const int r = i / (KP / 8), kc = i - r * (KP / 8);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kc * 8 < Cin) v = *reinterpret_cast<const uint4*>(we + (size_t)(c0 + r) * Cin + kc * 8);
+      *reinterpret_cast<uint4*>(swe + r * KP + kc * 8) = v;
+    }
+    for (int i = tid; i < K * K * CW; i += 256) {
+      const int t = i / CW, c = i - t * CW;
+      sw[i] = w[(size_t)(c0 + c) * K * K + t];
+    }
+    for (int i = tid; i < CW; i += 256) {
+      sb[i] = bias[c0 + i];
+      sbe[i] = be[c0 + i];
+    }
+    __syncthreads();
+
+    // ---- expand the input tile (+halo) into LDS ----
+#pragma unroll
+    for (int it = 0; it < MAXRF; ++it) {
+      const int rf = wave + 4 * it;
+      if (rf >= nrf) break;
+      const int pix = rf * 16 + fr;
+      const int ty = pix / IT, tx = pix - ty * IT;
+      const int iy = iy0 + ty, ix = ix0 + tx;
+      const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      for (int nf = 0; nf < NF; ++nf) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 wf = as_bf16x8(*reinterpret_cast<const uint4*>(swe + (nf * 16 + fr) * KP + ks * 32 + fg * 8));
+          acc = mfma16x16x32(wf, as_bf16x8(xr[it][ks]), acc);
+        }
+        if (pix < npix) {
+          const int cl = nf * 16 + fg * 4;
+          const float4 b = *reinterpret_cast<const float4*>(sbe + cl);
+          float e[4] = {acc[0] + b.x, acc[1] + b.y, acc[2] + b.z, acc[3] + b.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) e[r] = inimg ? act_apply(e[r], ACT_SILU) : 0.f;
+          *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + cl) = make_uint2(pack2bf(e[0], e[1]), pack2bf(e[2], e[3]));
+        }
+      }
+    }
+    __syncthreads();
+    dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
+    __syncthreads();  // the next group restages sw / sb / swe / tile and rewrites red
+  }
 }
 
 // Squeeze-excitation, one 1024-thread block per image.  The three phases are each a few dependent
@@ -420,8 +435,9 @@ hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const fl
   if (!expand_dw_applicable(cin, C) || CW != 48) return hipErrorInvalidValue;
   *nchunks_out = ntiles;
   const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8), KS = (cin + 31) / 32;
+  if (IT > 19) return hipErrorInvalidValue;  // the kernel's MAXRF prefetch depth
   const size_t smem = (size_t)IT * IT * CW * 2 + (size_t)(k * k * CW + CW + PX * CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
-  const dim3 grid(ntiles, C / CW, B), blk(256);
+  const dim3 grid(ntiles, 1, B), blk(256);
 #define MMF_EDW(KK, SS, QS)                                                                                      \
   if (k == KK && stride == SS && KS == QS) {                                                                     \
     hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS>), grid, blk, smem, s, x, cin, we, be, w, bias, out, pool_part, \

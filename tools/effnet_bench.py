@@ -1,0 +1,37 @@
+"""EfficientNet-B0 tower alone (B images, synthetic weights/inputs) for per-kernel profiling:
+
+    python tools/effnet_bench.py [--batch 256 --iters 10]
+    rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES ... -- python tools/effnet_bench.py --iters 2
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    import mmf_amd.synthetic as syn
+    import mmf_amd.weights as W
+    from mmf_amd.engine import Engine
+    eng = Engine(0, W.synthetic_detector_state(0), None, max_batch=a.batch)
+    img = torch.from_numpy(syn.images(a.batch, 3)).cuda()
+    eng.effnet_forward(img)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        eng.effnet_forward(img)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.iters
+    print(f"effnet B={a.batch}: {dt * 1e3:.3f} ms / forward, {a.batch / dt:.0f} img/s")
+
+
+if __name__ == "__main__":
+    main()
