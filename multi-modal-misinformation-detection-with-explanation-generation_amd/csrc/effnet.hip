@@ -123,6 +123,85 @@ MMF_DEV void dw_compute(const bf16_t* tile, const float* sw, const float* sb, fl
   }
 }
 
+// Compile-time-geometry variant of dw_compute: T x T output tile, CW channels, and each work item
+// (channel group g, output row oy, run of R consecutive outputs) walks the input row segment of a
+// kernel row once -- ((R-1)S + K) LDS reads / bf16 unpacks per kernel row instead of R*K -- and
+// reuses the kernel row's weights for all R outputs (K reads instead of R*K).  Per output the
+// VALU work drops by ~30 % at K = 5, R = 7, and every tile offset is an immediate.
+// Items = NG * T * (T / R) over the first (256 / NG) * NG threads (each keeps its channel group).
+template <int K, int S, int T, int CW, int R>
+MMF_DEV void dw_compute_ct(const bf16_t* tile, const float* sw, const float* sb, float* red, bf16_t* __restrict__ out,
+                           float* __restrict__ pool_part, int bi, int c0, int oy0, int ox0, int Ho, int Wo, int C) {
+  constexpr int NG = CW / 8, IT = (T - 1) * S + K, NR = T / R, ITEMS = NG * T * NR, IC = (R - 1) * S + K;
+  constexpr int STRIDE = (256 / NG) * NG;  // active threads: a thread's channel group g never changes
+  constexpr int NRED = STRIDE / NG;         // partial-sum slots per channel (<= the caller's red rows)
+  static_assert(T % R == 0, "runs tile the row");
+  const int tid = threadIdx.x;
+  const int g = tid % NG;
+  float psum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (tid < STRIDE) {
+    for (int item = tid; item < ITEMS; item += STRIDE) {
+      const int rest = item / NG;
+      const int run = rest % NR, oy = rest / NR, ox = run * R;
+      if (oy0 + oy >= Ho) continue;
+      float acc[R][8];
+#pragma unroll
+      for (int o = 0; o < R; ++o)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[o][j] = sb[g * 8 + j];
+#pragma unroll 1
+      for (int ky = 0; ky < K; ++ky) {
+        float wk[K][8];
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const float4 w0 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8);
+          const float4 w1 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8 + 4);
+          wk[kx][0] = w0.x; wk[kx][1] = w0.y; wk[kx][2] = w0.z; wk[kx][3] = w0.w;
+          wk[kx][4] = w1.x; wk[kx][5] = w1.y; wk[kx][6] = w1.z; wk[kx][7] = w1.w;
+        }
+        const bf16_t* row = tile + ((size_t)((oy * S + ky) * IT + ox * S) * NG + g) * 8;
+#pragma unroll
+        for (int col = 0; col < IC; ++col) {
+          const uint4 v = *reinterpret_cast<const uint4*>(row + col * NG * 8);
+          const float f[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
+                              lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+#pragma unroll
+          for (int o = 0; o < R; ++o) {
+            const int kx = col - o * S;
+            if (kx >= 0 && kx < K) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[o][j] = fmaf(f[j], wk[kx][j], acc[o][j]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < R; ++o) {
+        if (ox0 + ox + o < Wo) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            acc[o][j] = act_apply(acc[o][j], ACT_SILU);
+            psum[j] += acc[o][j];
+          }
+          *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox + o) * C + c0 + g * 8) =
+              make_uint4(pack2bf(acc[o][0], acc[o][1]), pack2bf(acc[o][2], acc[o][3]), pack2bf(acc[o][4], acc[o][5]),
+                         pack2bf(acc[o][6], acc[o][7]));
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[(tid / NG) * CW + g * 8 + j] = psum[j];
+  }
+  __syncthreads();
+  // fixed-order reduction over the thread slots of each channel -> one partial per (image, tile, channel)
+  const int ntiles = gridDim.x;
+  for (int c = tid; c < CW; c += 256) {
+    float sum = 0.f;
+    for (int q = 0; q < NRED; ++q) sum += red[q * CW + c];
+    pool_part[((size_t)bi * ntiles + blockIdx.x) * C + c0 + c] = sum;
+  }
+}
+
 // Depthwise kxk conv, LDS-tiled: a block owns a T x T output tile of one image and CW channels
 // (CW = 32 or 48, i.e. NG = 4 or 6 groups of 8).  The input tile with its halo
 // ((T-1)S + K)^2 x CW is read from HBM once, coalesced (zero padding written as zeros), and every
@@ -131,13 +210,15 @@ MMF_DEV void dw_compute(const bf16_t* tile, const float* sw, const float* sb, fl
 // one thread and is reduced across px in a fixed order (deterministic, no atomics): one partial
 // per (image, tile, channel).
 // grid (tiles_y * tiles_x, C / CW, B); block 256 threads (PX * NG of them active in phase 2)
-template <int K, int S>
-__global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* __restrict__ in, const float* __restrict__ w,
+// TT / CWT / R > 0: compile-time tile edge, channel width and output run (dw_compute_ct); 0: runtime
+template <int K, int S, int TT, int CWT, int R>
+__global__ __launch_bounds__(256, 3) void dwconv_kernel(const bf16_t* __restrict__ in, const float* __restrict__ w,
                                                      const float* __restrict__ bias, bf16_t* __restrict__ out,
-                                                     float* __restrict__ pool_part, int H, int W, int C, int CW,
-                                                     int T, int tiles_x) {
+                                                     float* __restrict__ pool_part, int H, int W, int C, int CW_,
+                                                     int T_, int tiles_x) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
   constexpr int PAD = (K - 1) / 2;
+  const int T = TT ? TT : T_, CW = CWT ? CWT : CW_;
   const int NG = CW / 8, IT = (T - 1) * S + K;  // input tile edge
   const int tid = threadIdx.x;
   const int bi = blockIdx.z, c0 = blockIdx.y * CW;
@@ -167,7 +248,8 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* __restrict__ 
   for (int i = tid; i < CW; i += 256) sb[i] = bias[c0 + i];
   __syncthreads();
 
-  dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
+  if constexpr (TT > 0) dw_compute_ct<K, S, TT, CWT, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C);
+  else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
 }
 
 // MBConv front, fused: 1x1 expand (BN folded) + SiLU computed per input tile on the MFMA, straight
@@ -181,14 +263,15 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16_t* __restrict__ 
 //          lane ends with 4 consecutive channels of one pixel -> 8-B LDS writes; pixels outside the
 //          image are written as 0 (the depthwise conv zero-pads E, not X).
 // grid (tiles, Cexp / CW, B); block 256 threads; KS = ceil(Cin / 32) <= 2
-template <int K, int S, int KS>
-__global__ __launch_bounds__(256) void expand_dw_kernel(const bf16_t* __restrict__ x, int Cin,
+template <int K, int S, int KS, int TT, int R>
+__global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restrict__ x, int Cin,
                                                         const bf16_t* __restrict__ we, const float* __restrict__ be,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         bf16_t* __restrict__ out, float* __restrict__ pool_part, int H,
-                                                        int W, int C, int CW, int T, int tiles_x) {
+                                                        int W, int C, int CW_, int T_, int tiles_x) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
   constexpr int PAD = (K - 1) / 2, KP = KS * 32;
+  const int T = TT ? TT : T_, CW = TT ? 48 : CW_;  // compile-time only on the dw_compute_ct path
   const int NG = CW / 8, NF = CW / 16, IT = (T - 1) * S + K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -248,6 +331,7 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(const bf16_t* __restrict
       const int ty = pix / IT, tx = pix - ty * IT;
       const int iy = iy0 + ty, ix = ix0 + tx;
       const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
+#pragma unroll 1
       for (int nf = 0; nf < NF; ++nf) {
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -266,7 +350,8 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(const bf16_t* __restrict
       }
     }
     __syncthreads();
-    dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
+    if constexpr (TT > 0) dw_compute_ct<K, S, TT, CW, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C);
+    else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
     __syncthreads();  // the next group restages sw / sb / swe / tile and rewrites red
   }
 }
@@ -411,10 +496,25 @@ hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf
   const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8);
   const size_t smem = (size_t)IT * IT * CW * 2 + (size_t)(k * k * CW + CW + PX * CW) * 4;
   const dim3 grid(ntiles, C / CW, B), blk(256);
+  // compile-time geometries of EfficientNet-B0 at 224^2 (output runs R chosen so that items <= 256)
+#define MMF_DWCT(KK, SS, TT, CC, RR)                                                                          \
+  if (k == KK && stride == SS && T == TT && CW == CC) {                                                        \
+    hipLaunchKernelGGL((dwconv_kernel<KK, SS, TT, CC, RR>), grid, blk, smem, s, in, w, bias, out, pool_part, H, W, \
+                       C, CW, T, tiles_x);                                                                    \
+    return hipGetLastError();                                                                                 \
+  }
+  const char* ct = getenv("MMF_DW_CT");  // MMF_DW_CT=0: runtime-geometry kernels only (A/B)
+  if (!(ct && *ct == '0')) {
+    MMF_DWCT(3, 1, 16, 32, 4)
+    MMF_DWCT(3, 1, 14, 48, 2)
+    MMF_DWCT(5, 1, 14, 48, 2)
+    MMF_DWCT(3, 2, 8, 48, 2)
+  }
+#undef MMF_DWCT
 #define MMF_DW(KK, SS)                                                                                        \
   if (k == KK && stride == SS) {                                                                              \
-    hipLaunchKernelGGL((dwconv_kernel<KK, SS>), grid, blk, smem, s, in, w, bias, out, pool_part, H, W, C, CW, \
-                       T, tiles_x);                                                                           \
+    hipLaunchKernelGGL((dwconv_kernel<KK, SS, 0, 0, 1>), grid, blk, smem, s, in, w, bias, out, pool_part, H, W, C, \
+                       CW, T, tiles_x);                                                                       \
     return hipGetLastError();                                                                                 \
   }
   MMF_DW(3, 1)
@@ -438,14 +538,28 @@ hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const fl
   if (IT > 19) return hipErrorInvalidValue;  // the kernel's MAXRF prefetch depth
   const size_t smem = (size_t)IT * IT * CW * 2 + (size_t)(k * k * CW + CW + PX * CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
   const dim3 grid(ntiles, 1, B), blk(256);
+#define MMF_EDWCT(KK, SS, QS, TT, RR)                                                                       \
+  if (k == KK && stride == SS && KS == QS && T == TT) {                                                       \
+    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, TT, RR>), grid, blk, smem, s, x, cin, we, be, w, bias, out, \
+                       pool_part, H, W, C, CW, T, tiles_x);                                                   \
+    return hipGetLastError();                                                                                 \
+  }
+  const char* ct = getenv("MMF_DW_CT");
+  if (!(ct && *ct == '0')) {
+    MMF_EDWCT(3, 2, 1, 8, 2)
+    MMF_EDWCT(3, 1, 1, 14, 2)
+    MMF_EDWCT(5, 1, 2, 14, 2)
+  }
+#undef MMF_EDWCT
 #define MMF_EDW(KK, SS, QS)                                                                                      \
   if (k == KK && stride == SS && KS == QS) {                                                                     \
-    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS>), grid, blk, smem, s, x, cin, we, be, w, bias, out, pool_part, \
-                       H, W, C, CW, T, tiles_x);                                                                 \
+    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, 0, 1>), grid, blk, smem, s, x, cin, we, be, w, bias, out,    \
+                       pool_part, H, W, C, CW, T, tiles_x);                                                      \
     return hipGetLastError();                                                                                    \
   }
-  MMF_EDW(3, 1, 1) MMF_EDW(3, 2, 1) MMF_EDW(5, 1, 1) MMF_EDW(5, 2, 1)
-  MMF_EDW(3, 1, 2) MMF_EDW(3, 2, 2) MMF_EDW(5, 1, 2) MMF_EDW(5, 2, 2)
+  // runtime-geometry fallbacks: the remaining EfficientNet-B0 fused blocks (T = 7) and, under
+  // MMF_DW_CT=0, the three above
+  MMF_EDW(3, 2, 1) MMF_EDW(3, 1, 1) MMF_EDW(5, 2, 1) MMF_EDW(5, 1, 2) MMF_EDW(3, 2, 2)
 #undef MMF_EDW
   return hipErrorInvalidValue;
 }

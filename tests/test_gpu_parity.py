@@ -108,3 +108,19 @@ def test_fused_expand_dwconv_bit_identical(engine, monkeypatch):
     lg1, _ = engine.effnet_forward(imgs)
     torch.cuda.synchronize()
     assert torch.equal(lg0, lg1)
+
+
+def test_compile_time_dwconv_matches_runtime_geometry(engine, monkeypatch):
+    """Depthwise kernels with compile-time tile geometry and output runs (dw_compute_ct, the
+    default) vs the runtime-geometry kernels (MMF_DW_CT=0).  Conv outputs are computed in the same
+    order; the SE pool partial sums are grouped differently, and those 1-ulp differences flip bf16
+    roundings downstream, so the comparison is at the north-star tolerance on deepfake_score (both
+    paths are also checked against the fp32 oracle by test_effnet_signal for the default)."""
+    import mmf_amd.synthetic as syn
+    imgs = syn.images(64, 19)
+    monkeypatch.setenv("MMF_DW_CT", "0")
+    _, s0 = engine.effnet_forward(imgs)
+    monkeypatch.setenv("MMF_DW_CT", "1")
+    _, s1 = engine.effnet_forward(imgs)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
