@@ -509,6 +509,10 @@ hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf
     MMF_DWCT(3, 1, 14, 48, 2)
     MMF_DWCT(5, 1, 14, 48, 2)
     MMF_DWCT(3, 2, 8, 48, 2)
+    MMF_DWCT(5, 1, 7, 48, 1)
+    MMF_DWCT(3, 1, 7, 48, 1)
+    MMF_DWCT(5, 2, 7, 48, 1)
+    MMF_DWCT(3, 2, 7, 48, 1)
   }
 #undef MMF_DWCT
 #define MMF_DW(KK, SS)                                                                                        \
@@ -549,6 +553,8 @@ hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const fl
     MMF_EDWCT(3, 2, 1, 8, 2)
     MMF_EDWCT(3, 1, 1, 14, 2)
     MMF_EDWCT(5, 1, 2, 14, 2)
+    MMF_EDWCT(5, 2, 1, 7, 1)
+    MMF_EDWCT(3, 2, 2, 7, 1)
   }
 #undef MMF_EDWCT
 #define MMF_EDW(KK, SS, QS)                                                                                      \
@@ -557,8 +563,7 @@ hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const fl
                        pool_part, H, W, C, CW, T, tiles_x);                                                      \
     return hipGetLastError();                                                                                    \
   }
-  // runtime-geometry fallbacks: the remaining EfficientNet-B0 fused blocks (T = 7) and, under
-  // MMF_DW_CT=0, the three above
+  // runtime-geometry fallbacks (MMF_DW_CT=0)
   MMF_EDW(3, 2, 1) MMF_EDW(3, 1, 1) MMF_EDW(5, 2, 1) MMF_EDW(5, 1, 2) MMF_EDW(3, 2, 2)
 #undef MMF_EDW
   return hipErrorInvalidValue;

@@ -690,7 +690,10 @@ int gemm_config(const GemmArgs& a) {
     }
     return best;
   }
-  return 3;
+  // register-staged tiles (e.g. the SE-scaled EfficientNet projects): 64x128 tiles when 128x128
+  // ones would leave the chip short of workgroups (late stages, M = B * 7^2, K = 1152)
+  const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
+  return t128 < 384 ? 2 : 3;
 }
 
 const char* gemm_config_name(int c) {
