@@ -38,36 +38,53 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
   const int Lk = (L + 31) & ~31;  // keys padded to the 32-deep PV k-step
   const bf16_t* base = qkv + (size_t)bi * L * ld;
 
-  // stage K and V (swizzled rows); zero the padded keys so 0 * pad stays finite
-  for (int c = tid; c < Lk * 8; c += 256) {
-    const int key = c >> 3, kc = c & 7;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nqt = (L + 15) >> 4, nkt = Lk >> 4;
+  // stage K and V (swizzled rows); zero the padded keys so 0 * pad stays finite.  All global loads
+  // (K, V and this wave's Q fragments for both of its query tiles) are issued before the first
+  // LDS store so the whole workgroup has its 48 KB in flight at once.
+  constexpr int NIT = LMAX * 8 / 256, NQT = LMAX / 64;
+  uint4 kr[NIT], vr[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int c = tid + i * 256, key = c >> 3, kc = c & 7;
+    kr[i] = make_uint4(0, 0, 0, 0);
+    vr[i] = make_uint4(0, 0, 0, 0);
     if (key < L) {
-      kv = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + D + h * 64 + kc * 8);
-      vv = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + 2 * D + h * 64 + kc * 8);
+      kr[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + D + h * 64 + kc * 8);
+      vr[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + 2 * D + h * 64 + kc * 8);
     }
-    *reinterpret_cast<uint4*>(Ks + kv_swz(key, kc)) = kv;
-    *reinterpret_cast<uint4*>(Vs + kv_swz(key, kc)) = vv;
+  }
+  // Q fragments: row q = qt*16 + fr, dims 32*ks + 8*fg .. +7, for qt = wave + 4*it
+  bf16x8 qfa[NQT][2];
+#pragma unroll
+  for (int it = 0; it < NQT; ++it) {
+    const int q = (wave + 4 * it) * 16 + fr;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q < L) v = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + h * 64 + ks * 32 + fg * 8);
+      qfa[it][ks] = as_bf16x8(v);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int c = tid + i * 256, key = c >> 3, kc = c & 7;
+    if (key < Lk) {
+      *reinterpret_cast<uint4*>(Ks + kv_swz(key, kc)) = kr[i];
+      *reinterpret_cast<uint4*>(Vs + kv_swz(key, kc)) = vr[i];
+    }
   }
   for (int k = tid; k < Lk; k += 256)
     kbias[k] = (k < L && (!mask || mask[(size_t)bi * L + k])) ? 0.f : -INFINITY;
   __syncthreads();
 
-  const int fr = lane & 15, fg = lane >> 4;
-  const int nqt = (L + 15) >> 4, nkt = Lk >> 4;
-
-  for (int qt = wave; qt < nqt; qt += 4) {
-    // Q fragments: row q = qt*16 + fr, dims 32*ks + 8*fg .. +7
-    bf16x8 qf[2];
-    {
-      const int q = qt * 16 + fr;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (q < L) v = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + h * 64 + ks * 32 + fg * 8);
-        qf[ks] = as_bf16x8(v);
-      }
-    }
+  static_assert(NQT == 2, "two query tiles per wave");
+  bf16x8 qf[2] = {qfa[0][0], qfa[0][1]};
+#pragma unroll 1
+  for (int it = 0; it < NQT; ++it) {
+    const int qt = wave + 4 * it;
+    if (qt >= nqt) break;
     // S^T[key][q]: lane holds keys j*16 + fg*4 + r (r = 0..3) of query q = qt*16 + fr
     f32x4 s[LMAX / 16];
 #pragma unroll
@@ -149,6 +166,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
         *reinterpret_cast<uint2*>(dst + dt * 16) =
             make_uint2(pack2bf(o[dt][0], o[dt][1]), pack2bf(o[dt][2], o[dt][3]));
     }
+    qf[0] = qfa[1][0];
+    qf[1] = qfa[1][1];
   }
 }
 

@@ -14,7 +14,12 @@ MMF_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 on gfx950 (RNE, NaN-preserving)
   return __builtin_bit_cast(bf16_t, b);
 }
-MMF_DEV uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 (RNE) for both halves; the scalar-cast form costs 2 cvt + shift + or
+MMF_DEV uint32_t pack2bf(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
 
 MMF_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 MMF_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -46,7 +51,7 @@ MMF_DEV float gelu_erf(float x) {
   p = fmaf(p, t, 0.127414796f);                       // a1/2
   p *= t;
   const float e = __builtin_amdgcn_exp2f(az * (az * -1.4426950408889634f));
-  return fmaxf(x, 0.0f) - fabsf(x) * (p * e);
+  return fmaf(-fabsf(x), p * e, fmaxf(x, 0.0f));
 }
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QUICK_GELU = 2, ACT_SILU = 3, ACT_RELU = 4 };
 MMF_DEV float act_apply(float x, int act) {
@@ -56,6 +61,44 @@ MMF_DEV float act_apply(float x, int act) {
     case ACT_SILU: return x * fast_rcp(1.0f + __expf(-x));
     case ACT_RELU: return fmaxf(x, 0.0f);
     default: return x;
+  }
+}
+
+// Two elements at once: the FMA-class steps become packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 /
+// v_pk_add_f32, 2 results per lane per issue), only the transcendentals stay per element.  Same
+// operations in the same order as the scalar forms above, so results are bit-identical.
+MMF_DEV f32x2_t gelu_erf2(f32x2_t x) {
+  const f32x2_t ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2_t az = ax * 0.70710678118654752f;
+  const f32x2_t d = __builtin_elementwise_fma(az, (f32x2_t)0.3275911f, (f32x2_t)1.0f);
+  const f32x2_t t = {fast_rcp(d.x), fast_rcp(d.y)};
+  f32x2_t p = __builtin_elementwise_fma((f32x2_t)0.5307027145f, t, (f32x2_t)-0.7265760135f);
+  p = __builtin_elementwise_fma(p, t, (f32x2_t)0.7107068705f);
+  p = __builtin_elementwise_fma(p, t, (f32x2_t)-0.142248368f);
+  p = __builtin_elementwise_fma(p, t, (f32x2_t)0.127414796f);
+  p = p * t;
+  const f32x2_t a = az * (az * -1.4426950408889634f);
+  const f32x2_t pe = p * (f32x2_t){__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  return (f32x2_t){fmaf(-ax.x, pe.x, fmaxf(x.x, 0.0f)), fmaf(-ax.y, pe.y, fmaxf(x.y, 0.0f))};
+}
+// x * sigmoid(k x) for a pair (SiLU k = 1, quick-GELU k = 1.702)
+MMF_DEV f32x2_t xsigmoid2(f32x2_t x, float k) {
+  const f32x2_t a = x * -k;
+  const f32x2_t d = (f32x2_t){__expf(a.x), __expf(a.y)} + 1.0f;
+  return x * (f32x2_t){fast_rcp(d.x), fast_rcp(d.y)};
+}
+// activation of 4 consecutive accumulator values (compile-time ACT), packed where it pays
+template <int ACT>
+MMF_DEV void act4(float* v) {
+#pragma unroll
+  for (int h = 0; h < 4; h += 2) {
+    f32x2_t x = {v[h], v[h + 1]};
+    if constexpr (ACT == ACT_GELU) x = gelu_erf2(x);
+    else if constexpr (ACT == ACT_QUICK_GELU) x = xsigmoid2(x, 1.702f);
+    else if constexpr (ACT == ACT_SILU) x = xsigmoid2(x, 1.0f);
+    else if constexpr (ACT == ACT_RELU) x = (f32x2_t){fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f)};
+    v[h] = x.x;
+    v[h + 1] = x.y;
   }
 }
 

@@ -178,11 +178,10 @@ MMF_DEV void dw_compute_ct(const bf16_t* tile, const float* sw, const float* sb,
 #pragma unroll
       for (int o = 0; o < R; ++o) {
         if (ox0 + ox + o < Wo) {
+          act4<ACT_SILU>(acc[o]);
+          act4<ACT_SILU>(acc[o] + 4);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            acc[o][j] = act_apply(acc[o][j], ACT_SILU);
-            psum[j] += acc[o][j];
-          }
+          for (int j = 0; j < 8; ++j) psum[j] += acc[o][j];
           *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox + o) * C + c0 + g * 8) =
               make_uint4(pack2bf(acc[o][0], acc[o][1]), pack2bf(acc[o][2], acc[o][3]), pack2bf(acc[o][4], acc[o][5]),
                          pack2bf(acc[o][6], acc[o][7]));
@@ -343,8 +342,9 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restr
           const int cl = nf * 16 + fg * 4;
           const float4 b = *reinterpret_cast<const float4*>(sbe + cl);
           float e[4] = {acc[0] + b.x, acc[1] + b.y, acc[2] + b.z, acc[3] + b.w};
+          act4<ACT_SILU>(e);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) e[r] = inimg ? act_apply(e[r], ACT_SILU) : 0.f;
+          for (int r = 0; r < 4; ++r) e[r] = inimg ? e[r] : 0.f;
           *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + cl) = make_uint2(pack2bf(e[0], e[1]), pack2bf(e[2], e[3]));
         }
       }

@@ -315,8 +315,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
             float v[4] = {acc[i + h2][j][0] + bias_r[i + h2].x, acc[i + h2][j][1] + bias_r[i + h2].y,
                           acc[i + h2][j][2] + bias_r[i + h2].z, acc[i + h2][j][3] + bias_r[i + h2].w};
             if (ACT != ACT_NONE && !(g.probe & 2)) {  // probe 2: skip the activation
-#pragma unroll
-              for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
+              act4<ACT>(v);
             }
             pk[h2] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
           }
@@ -371,8 +370,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
           float v[4] = {acc[i][j][0] + bias_r[i].x, acc[i][j][1] + bias_r[i].y, acc[i][j][2] + bias_r[i].z,
                         acc[i][j][3] + bias_r[i].w};
           if (ACT != ACT_NONE) {
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
+            act4<ACT>(v);
           }
           v[0] += rcur[i].x; v[1] += rcur[i].y; v[2] += rcur[i].z; v[3] += rcur[i].w;
           const uint32_t e = n < N ? m * (uint32_t)g.ldc + n : (kOOB >> 2);
@@ -549,8 +547,7 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
           float v[4] = {acc[i + h2][j][0] + b.x, acc[i + h2][j][1] + b.y, acc[i + h2][j][2] + b.z,
                         acc[i + h2][j][3] + b.w};
           if (ACT != ACT_NONE) {
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) v[tt] = act_apply(v[tt], ACT);
+            act4<ACT>(v);
           }
           pk[h2] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
         }

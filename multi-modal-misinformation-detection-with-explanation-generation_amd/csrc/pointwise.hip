@@ -118,8 +118,7 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
         const float4 b = *reinterpret_cast<const float4*>(sBias + nl);
         float v[4] = {acc[c][0] + b.x, acc[c][1] + b.y, acc[c][2] + b.z, acc[c][3] + b.w};
         if (ACT != ACT_NONE) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) v[t] = act_apply(v[t], ACT);
+          act4<ACT>(v);
         }
         *reinterpret_cast<float4*>(stage + fr * SLD + nl) = make_float4(v[0], v[1], v[2], v[3]);
       }
