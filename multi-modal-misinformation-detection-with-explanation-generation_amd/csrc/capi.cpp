@@ -659,7 +659,11 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
   Workspace& w = h->ws;
   bf16_t* cur = w.e_a;
   bf16_t* nxt = w.e_b;
-  {
+  // MMF_FUSE_STEM=0: separate stem launch + stage-1 depthwise (A/B and parity tests)
+  const EffBlock& b0 = h->e_blocks.front();
+  const char* fs = getenv("MMF_FUSE_STEM");
+  const bool fuse_stem = !(fs && *fs == '0') && b0.expand == 1 && b0.cexp == 32 && b0.k == 3 && b0.stride == 1;
+  if (!fuse_stem) {
     ProfScope ps(h, s, PK_STEM, 2.0 * B * 112 * 112 * 32 * 27, (double)B * (224 * 224 * 3 + 112 * 112 * 32 * 2));
     if (xf32) HIPCHK(launch_effnet_stem_f32(xf32, h->e_stem_w, h->e_stem_b, cur, B, s));
     else HIPCHK(launch_effnet_stem(img, h->e_stem_w, h->e_stem_b, cur, B, s));
@@ -671,7 +675,12 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
     const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
     const char* fe = getenv("MMF_FUSE_EXPAND");  // MMF_FUSE_EXPAND=0: separate expand launch (A/B)
     const bool fuse = b.expand != 1 && expand_dw_applicable(b.cin, b.cexp) && !(fe && *fe == '0');
-    if (fuse) {
+    if (&b == &b0 && fuse_stem) {
+      // stem output recomputed per 18x18 halo tile: 1.27x the stem MACs, image patch read once
+      ProfScope ps(h, s, PK_DW, 2.0 * B * 112 * 112 * 32 * (9 + 27 * 1.27),
+                   (double)B * (224 * 224 * 3 * 1.34 + 112 * 112 * 32 * 2));
+      HIPCHK(launch_effnet_stem_dw(img, xf32, h->e_stem_w, h->e_stem_b, b.wd, b.bd, w.e_dw, w.e_pool, B, &nch, s));
+    } else if (fuse) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k + 2.0 * B * H * W * b.cin * b.cexp,
                    (double)B * 2 * ((double)H * W * b.cin * (b.cexp / 48) + (double)Ho * Wo * b.cexp));
       HIPCHK(launch_expand_dw(cur, b.cin, b.e.w, b.e.b, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride,
@@ -683,7 +692,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
       CHK(gemm(h, g, s));
       src = w.e_exp;
     }
-    if (!fuse) {
+    if (!fuse && !(&b == &b0 && fuse_stem)) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k,
                    (double)B * b.cexp * 2 * ((double)H * W + (double)Ho * Wo));
       HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s));

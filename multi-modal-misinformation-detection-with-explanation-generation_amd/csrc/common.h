@@ -8,6 +8,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MMF_DEV __device__ __forceinline__
+#define MMF_DEV_HOST_INLINE __host__ __device__ inline
 
 MMF_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 MMF_DEV bf16_t f2bf(float f) {

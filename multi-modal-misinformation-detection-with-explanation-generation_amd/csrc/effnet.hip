@@ -188,6 +188,9 @@ MMF_DEV void dw_compute_ct(const bf16_t* tile, const float* sw, const float* sb,
         }
       }
     }
+  }
+  __syncthreads();  // `red` aliases the input tile: every tap read is done before it is overwritten
+  if (tid < STRIDE) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[(tid / NG) * CW + g * 8 + j] = psum[j];
   }
@@ -199,6 +202,13 @@ MMF_DEV void dw_compute_ct(const bf16_t* tile, const float* sw, const float* sb,
     for (int q = 0; q < NRED; ++q) sum += red[q * CW + c];
     pool_part[((size_t)bi * ntiles + blockIdx.x) * C + c0 + c] = sum;
   }
+}
+
+// LDS bytes of the input tile region.  Compile-time-geometry kernels (dw_compute_ct) reuse it for
+// the pool-partial slots `red` once the taps are done (fewer LDS bytes -> one more block per CU).
+MMF_DEV_HOST_INLINE int dw_tile_bytes(int IT, int CW, bool alias_red) {
+  const int t = IT * IT * CW * 2, r = (256 / (CW / 8)) * CW * 4;
+  return ((alias_red && r > t ? r : t) + 15) & ~15;
 }
 
 // Depthwise kxk conv, LDS-tiled: a block owns a T x T output tile of one image and CW channels
@@ -224,25 +234,54 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const bf16_t* __restrict
   const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   const int oy0 = ty0 * T, ox0 = tx0 * T;
-  bf16_t* tile = (bf16_t*)dw_smem;                       // [IT][IT][CW]
-  float* sw = (float*)(dw_smem + (size_t)IT * IT * CW * 2);  // [K*K][CW]
-  float* sb = sw + K * K * CW;                           // [CW]
-  float* red = sb + CW;                                  // [PX][CW]
+  bf16_t* tile = (bf16_t*)dw_smem;                                 // [IT][IT][CW]
+  float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, TT > 0));  // [K*K][CW]
+  float* sb = sw + K * K * CW;                                     // [CW]
+  float* red = TT > 0 ? (float*)dw_smem : sb + CW;                 // [PX][CW]
 
   // ---- input tile (+halo) -> LDS ----
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
-  for (int idx = tid; idx < IT * IT * NG; idx += 256) {
+  auto tile_src = [&](int idx, uint4& v) {
     const int g = idx % NG, pix = idx / NG;
     const int ty = pix / IT, tx = pix - ty * IT;
     const int iy = iy0 + ty, ix = ix0 + tx;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+    v = make_uint4(0, 0, 0, 0);
+    if (idx < IT * IT * NG && iy >= 0 && iy < H && ix >= 0 && ix < W)
       v = *reinterpret_cast<const uint4*>(in + (((size_t)bi * H + iy) * W + ix) * C + c0 + g * 8);
-    *reinterpret_cast<uint4*>(tile + (size_t)idx * 8) = v;
+  };
+  if constexpr (TT > 0) {
+    // compile-time tile: every thread's loads are issued before its first LDS store, so the
+    // block pays one HBM latency for the tile instead of one per loop trip
+    constexpr int NL = ((((TT - 1) * S + K) * ((TT - 1) * S + K) * (CWT / 8)) + 255) / 256;
+    uint4 v[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) tile_src(tid + i * 256, v[i]);
+#pragma unroll
+    for (int i = 0; i < NL; ++i)
+      if (tid + i * 256 < IT * IT * NG) *reinterpret_cast<uint4*>(tile + (size_t)(tid + i * 256) * 8) = v[i];
+  } else {
+    for (int idx = tid; idx < IT * IT * NG; idx += 256) {
+      uint4 v;
+      tile_src(idx, v);
+      *reinterpret_cast<uint4*>(tile + (size_t)idx * 8) = v;
+    }
   }
-  for (int i = tid; i < K * K * CW; i += 256) {
-    const int t = i / CW, c = i - t * CW;
-    sw[i] = w[(size_t)(c0 + c) * K * K + t];
+  if constexpr (TT > 0) {
+    constexpr int NW = (K * K * CWT + 255) / 256;
+    float wv[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int i = tid + j * 256, t = i / CWT, c = i - t * CWT;
+      wv[j] = i < K * K * CWT ? w[(size_t)(c0 + c) * K * K + t] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NW; ++j)
+      if (tid + j * 256 < K * K * CWT) sw[tid + j * 256] = wv[j];
+  } else {
+    for (int i = tid; i < K * K * CW; i += 256) {
+      const int t = i / CW, c = i - t * CW;
+      sw[i] = w[(size_t)(c0 + c) * K * K + t];
+    }
   }
   for (int i = tid; i < CW; i += 256) sb[i] = bias[c0 + i];
   __syncthreads();
@@ -278,11 +317,11 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restr
   const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   const int oy0 = ty0 * T, ox0 = tx0 * T;
-  bf16_t* tile = (bf16_t*)dw_smem;                          // [IT][IT][CW]
-  float* sw = (float*)(dw_smem + (size_t)IT * IT * CW * 2);  // [K*K][CW]
-  float* sb = sw + K * K * CW;                              // [CW]
-  float* red = sb + CW;                                     // [PX][CW]
-  float* sbe = red + (256 / NG) * CW;                       // [CW] expand bias
+  bf16_t* tile = (bf16_t*)dw_smem;                                 // [IT][IT][CW]
+  float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, TT > 0));  // [K*K][CW]
+  float* sb = sw + K * K * CW;                                     // [CW]
+  float* red = TT > 0 ? (float*)dw_smem : sb + CW;                 // [PX][CW]
+  float* sbe = TT > 0 ? sb + CW : red + (256 / NG) * CW;           // [CW] expand bias
   bf16_t* swe = (bf16_t*)(sbe + CW);                        // [CW][KP] expand weights (zero-padded K)
 
   // this wave's input-pixel fragments first: their HBM latency overlaps the weight staging
@@ -354,6 +393,139 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restr
     else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
     __syncthreads();  // the next group restages sw / sb / swe / tile and rewrites red
   }
+}
+
+// Stem + stage-1 depthwise, fused: the stem (ImageNet normalise -> conv3x3 s2 3->32 + BN + SiLU)
+// is computed per 16x16 depthwise tile straight into the depthwise conv's LDS tile (its 18x18
+// halo recomputed, 1.27x the stem work), so the 112x112x32 stem activation -- the largest tensor
+// of the image tower -- never touches HBM: the block reads a 37x37x3 uint8 image patch instead.
+//  stem on the MFMA as a K = 27 (padded to 32) GEMM: D[ch][pix] = W[ch][k] . P[k][pix] with
+//  k = (ky, kx, c) so that each ky contributes 9 CONTIGUOUS floats of one patch row (HWC);
+//  operands split as bf16 hi + lo (x = xh + xl, w = wh + wl; wl.xh + wh.xl + wh.xh, fp32
+//  accumulation) so the conv keeps ~16 mantissa bits, well under the bf16 rounding of its output.
+// grid (49, 1, B); block 256
+constexpr int SD_T = 16, SD_IT = 18, SD_PR = 2 * SD_IT + 1, SD_PW = SD_PR * 3;
+
+template <bool F32>
+__global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const float* __restrict__ ws,
+                                                      const float* __restrict__ bs, const float* __restrict__ wd,
+                                                      const float* __restrict__ bd, bf16_t* __restrict__ out,
+                                                      float* __restrict__ pool_part) {
+  constexpr int CW = 32, NPIX = SD_IT * SD_IT, NMT = (NPIX + 15) / 16;
+  __shared__ __attribute__((aligned(16))) float patch[(SD_PR * SD_PW + 255) / 256 * 256];  // image patch, HWC
+  __shared__ __attribute__((aligned(16))) bf16_t tile[NPIX * CW];      // stem output tile (+halo)
+  __shared__ __attribute__((aligned(16))) float sw[9 * CW];
+  __shared__ __attribute__((aligned(16))) float sb[CW];
+  float* red = patch;  // pool-partial slots [64][32]: the patch is dead once the stem tile is built
+  static_assert((SD_PR * SD_PW + 255) / 256 * 256 >= (256 / (CW / 8)) * CW, "red fits in the patch");
+  const uint8_t* img = (const uint8_t*)src;
+  const float* xf = (const float*)src;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int bi = blockIdx.z;
+  const int ty0 = blockIdx.x / 7, tx0 = blockIdx.x - ty0 * 7;
+  const int oy0 = ty0 * SD_T, ox0 = tx0 * SD_T;
+  const int py0 = 2 * oy0 - 3, px0 = 2 * ox0 - 3;  // image coords of patch (0, 0)
+
+  const float wd0 = wd[(tid % CW) * 9 + tid / CW];
+  const float wd1 = tid + 256 < 9 * CW ? wd[((tid + 256) % CW) * 9 + (tid + 256) / CW] : 0.f;
+  const float bd0 = tid < CW ? bd[tid] : 0.f;
+  // stem weight fragments (A operand: row = output channel nt*16 + fr, k = fg*8 + e), split hi/lo
+  int offk[8];
+  bf16x8 whi[2], wlo[2];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = fg * 8 + e, ky = k / 9, r9 = k - ky * 9;
+    offk[e] = k < 27 ? ky * SD_PW + r9 : -1;
+  }
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    float wv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = fg * 8 + e, ky = k / 9, r9 = k - ky * 9, kx = r9 / 3, c = r9 - kx * 3;
+      wv[e] = k < 27 ? ws[(nt * 16 + fr) * 27 + c * 9 + ky * 3 + kx] : 0.f;
+    }
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      h[q] = pack2bf(wv[2 * q], wv[2 * q + 1]);
+      l[q] = pack2bf(wv[2 * q] - lo_bf(h[q]), wv[2 * q + 1] - hi_bf(h[q]));
+    }
+    whi[nt] = as_bf16x8(make_uint4(h[0], h[1], h[2], h[3]));
+    wlo[nt] = as_bf16x8(make_uint4(l[0], l[1], l[2], l[3]));
+  }
+  float4 sbias[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) sbias[nt] = *reinterpret_cast<const float4*>(bs + nt * 16 + fg * 4);
+  // ---- normalised patch -> LDS (zero outside the image: the stem pads after Normalize) ----
+  constexpr int NP = SD_PR * SD_PW, NL = (NP + 255) / 256;
+  float raw[NL];  // all of this thread's loads in flight before the first LDS store
+  int chan[NL];   // channel of the element, -1 outside the image (zero padding)
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int idx = tid + i * 256;
+    const int pr = idx / SD_PW, rem = idx - pr * SD_PW;
+    const int pc = rem / 3, c = rem - pc * 3;
+    const int iy = py0 + pr, ix = px0 + pc;
+    // unconditional load from a clamped address (no divergent region around the load, so the
+    // compiler does not drain vmcnt per element); out-of-image elements are zeroed below
+    const bool ok = idx < NP && iy >= 0 && iy < 224 && ix >= 0 && ix < 224;
+    const int iyc = min(max(iy, 0), 223), ixc = min(max(ix, 0), 223);
+    chan[i] = ok ? c : -1;
+    if constexpr (F32) raw[i] = xf[(((size_t)bi * 3 + c) * 224 + iyc) * 224 + ixc];
+    else raw[i] = __builtin_bit_cast(float, (uint32_t)img[(((size_t)bi * 224 + iyc) * 224 + ixc) * 3 + c]);
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {  // (the array is padded to NL * 256: no branch around the stores)
+    const int c = chan[i];
+    float v = raw[i];
+    if constexpr (!F32) {  // ToTensor + Normalize: u / (255 std) - mean / std
+      const float sc = c == 0 ? 1.0f / (255.0f * 0.229f) : c == 1 ? 1.0f / (255.0f * 0.224f) : 1.0f / (255.0f * 0.225f);
+      const float of = c == 0 ? -0.485f / 0.229f : c == 1 ? -0.456f / 0.224f : -0.406f / 0.225f;
+      v = fmaf((float)__builtin_bit_cast(uint32_t, v), sc, of);
+    }
+    patch[tid + i * 256] = c < 0 ? 0.f : v;
+  }
+  sw[tid] = wd0;
+  if (tid + 256 < 9 * CW) sw[tid + 256] = wd1;
+  if (tid < CW) sb[tid] = bd0;
+  __syncthreads();
+
+  // ---- stem: 16 tile pixels per MFMA column block ----
+  for (int mt = wave; mt < NMT; mt += 4) {
+    const int p = mt * 16 + fr;
+    const int pc = p < NPIX ? p : NPIX - 1;
+    const int sy = pc / SD_IT, sx = pc - sy * SD_IT;
+    const int base = sy * 2 * SD_PW + sx * 6;
+    float xv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = offk[e] >= 0 ? patch[base + offk[e]] : 0.f;
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      h[q] = pack2bf(xv[2 * q], xv[2 * q + 1]);
+      l[q] = pack2bf(xv[2 * q] - lo_bf(h[q]), xv[2 * q + 1] - hi_bf(h[q]));
+    }
+    const bf16x8 xhi = as_bf16x8(make_uint4(h[0], h[1], h[2], h[3]));
+    const bf16x8 xlo = as_bf16x8(make_uint4(l[0], l[1], l[2], l[3]));
+    const int gy = oy0 - 1 + sy, gx = ox0 - 1 + sx;  // stem output coords of this pixel
+    const bool inimg = gy >= 0 && gy < 112 && gx >= 0 && gx < 112;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc = mfma16x16x32(wlo[nt], xhi, acc);
+      acc = mfma16x16x32(whi[nt], xlo, acc);
+      acc = mfma16x16x32(whi[nt], xhi, acc);
+      float e4[4] = {acc[0] + sbias[nt].x, acc[1] + sbias[nt].y, acc[2] + sbias[nt].z, acc[3] + sbias[nt].w};
+      act4<ACT_SILU>(e4);
+      if (p < NPIX)
+        *reinterpret_cast<uint2*>(tile + p * CW + nt * 16 + fg * 4) =
+            inimg ? make_uint2(pack2bf(e4[0], e4[1]), pack2bf(e4[2], e4[3])) : make_uint2(0, 0);
+    }
+  }
+  __syncthreads();
+  dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW);
 }
 
 // Squeeze-excitation, one 1024-thread block per image.  The three phases are each a few dependent
@@ -459,6 +631,16 @@ hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* b
   return hipGetLastError();
 }
 
+hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
+                                 const float* wd, const float* bd, bf16_t* out, float* pool_part, int B,
+                                 int* nchunks_out, hipStream_t s) {
+  *nchunks_out = 49;  // = dwconv_nchunks(112, 112, 32, 1): the SE reads the same partial layout
+  const dim3 grid(49, 1, B), blk(256);
+  if (xf32) hipLaunchKernelGGL(stem_dw_kernel<true>, grid, blk, 0, s, (const void*)xf32, ws, bs, wd, bd, out, pool_part);
+  else hipLaunchKernelGGL(stem_dw_kernel<false>, grid, blk, 0, s, (const void*)img, ws, bs, wd, bd, out, pool_part);
+  return hipGetLastError();
+}
+
 hipError_t launch_effnet_stem_f32(const float* x, const float* w, const float* bias, bf16_t* out, int B,
                                   hipStream_t s) {
   const size_t total = (size_t)B * 112 * 112;
@@ -494,12 +676,13 @@ hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf
   if (C % CW) return hipErrorInvalidValue;
   *nchunks_out = ntiles;
   const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8);
-  const size_t smem = (size_t)IT * IT * CW * 2 + (size_t)(k * k * CW + CW + PX * CW) * 4;
+  const size_t smem = (size_t)dw_tile_bytes(IT, CW, false) + (size_t)(k * k * CW + CW + PX * CW) * 4;
+  const size_t smem_ct = (size_t)dw_tile_bytes(IT, CW, true) + (size_t)(k * k * CW + CW) * 4;
   const dim3 grid(ntiles, C / CW, B), blk(256);
   // compile-time geometries of EfficientNet-B0 at 224^2 (output runs R chosen so that items <= 256)
 #define MMF_DWCT(KK, SS, TT, CC, RR)                                                                          \
   if (k == KK && stride == SS && T == TT && CW == CC) {                                                        \
-    hipLaunchKernelGGL((dwconv_kernel<KK, SS, TT, CC, RR>), grid, blk, smem, s, in, w, bias, out, pool_part, H, W, \
+    hipLaunchKernelGGL((dwconv_kernel<KK, SS, TT, CC, RR>), grid, blk, smem_ct, s, in, w, bias, out, pool_part, H, W, \
                        C, CW, T, tiles_x);                                                                    \
     return hipGetLastError();                                                                                 \
   }
@@ -540,11 +723,13 @@ hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const fl
   *nchunks_out = ntiles;
   const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8), KS = (cin + 31) / 32;
   if (IT > 19) return hipErrorInvalidValue;  // the kernel's MAXRF prefetch depth
-  const size_t smem = (size_t)IT * IT * CW * 2 + (size_t)(k * k * CW + CW + PX * CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
+  const size_t smem =
+      (size_t)dw_tile_bytes(IT, CW, false) + (size_t)(k * k * CW + CW + PX * CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
+  const size_t smem_ct = (size_t)dw_tile_bytes(IT, CW, true) + (size_t)(k * k * CW + CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
   const dim3 grid(ntiles, 1, B), blk(256);
 #define MMF_EDWCT(KK, SS, QS, TT, RR)                                                                       \
   if (k == KK && stride == SS && KS == QS && T == TT) {                                                       \
-    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, TT, RR>), grid, blk, smem, s, x, cin, we, be, w, bias, out, \
+    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, TT, RR>), grid, blk, smem_ct, s, x, cin, we, be, w, bias, out, \
                        pool_part, H, W, C, CW, T, tiles_x);                                                   \
     return hipGetLastError();                                                                                 \
   }

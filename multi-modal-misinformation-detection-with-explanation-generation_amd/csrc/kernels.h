@@ -91,6 +91,11 @@ hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* b
                               hipStream_t s);
 hipError_t launch_effnet_stem_f32(const float* x_nchw, const float* w, const float* bias, bf16_t* out, int B,
                                   hipStream_t s);
+// stem fused into the stage-1 depthwise conv (3x3 s1, 32 channels at 112^2) + its SE pool partials;
+// exactly one of img (uint8 HWC) / xf32 (normalised fp32 NCHW) is non-null
+hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
+                                 const float* wd, const float* bd, bf16_t* out, float* pool_part, int B,
+                                 int* nchunks_out, hipStream_t s);
 hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part,
                          int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s);
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
