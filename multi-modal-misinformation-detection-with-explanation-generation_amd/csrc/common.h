@@ -107,6 +107,15 @@ MMF_DEV f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Rows of 16 lanes pair up (lanes l, l ^ 16): a = this lane's 4-column group i, b = group i + 1
+// (packed bf16x4 each).  Even rows end with [own a | partner's a], odd rows with
+// [partner's b | own b]: 16 contiguous bytes per lane.  v_permlane16_swap (VALU, no LDS trip).
+MMF_DEV uint4 pair_rows16(uint2 a, uint2 b) {
+  const auto x = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto y = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  return make_uint4(x[0], y[0], x[1], y[1]);
+}
+
 MMF_DEV bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
 // Raw buffer access (CDNA SRSRC): 32-bit byte offsets with hardware bounds checking -- loads at
