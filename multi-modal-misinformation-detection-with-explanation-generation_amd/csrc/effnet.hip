@@ -599,12 +599,31 @@ __global__ __launch_bounds__(256) void gap_classifier_kernel(const bf16_t* x, in
   const int bi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float l0 = 0.f, l1 = 0.f;
   const float inv = 1.0f / (float)HW;
-  for (int c = tid; c < C; c += 256) {
-    float s = 0.f;
-    for (int p = 0; p < HW; ++p) s += bf2f(x[((size_t)bi * HW + p) * C + c]);
-    s *= inv;
-    l0 = fmaf(w[c], s, l0);
-    l1 = fmaf(w[C + c], s, l1);
+  // 8 channels per thread (16-B loads), pixels summed in order; 7 rows of loads in flight
+  for (int c8 = tid * 8; c8 < C; c8 += 256 * 8) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bf16_t* xp = x + (size_t)bi * HW * C + c8;
+    int p = 0;
+    for (; p + 7 <= HW; p += 7) {
+      uint4 v[7];
+#pragma unroll
+      for (int u = 0; u < 7; ++u) v[u] = *reinterpret_cast<const uint4*>(xp + (size_t)(p + u) * C);
+#pragma unroll
+      for (int u = 0; u < 7; ++u) {
+        s[0] += lo_bf(v[u].x); s[1] += hi_bf(v[u].x); s[2] += lo_bf(v[u].y); s[3] += hi_bf(v[u].y);
+        s[4] += lo_bf(v[u].z); s[5] += hi_bf(v[u].z); s[6] += lo_bf(v[u].w); s[7] += hi_bf(v[u].w);
+      }
+    }
+    for (; p < HW; ++p) {
+      const uint4 v = *reinterpret_cast<const uint4*>(xp + (size_t)p * C);
+      s[0] += lo_bf(v.x); s[1] += hi_bf(v.x); s[2] += lo_bf(v.y); s[3] += hi_bf(v.y);
+      s[4] += lo_bf(v.z); s[5] += hi_bf(v.z); s[6] += lo_bf(v.w); s[7] += hi_bf(v.w);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      l0 = fmaf(w[c8 + j], s[j] * inv, l0);
+      l1 = fmaf(w[C + c8 + j], s[j] * inv, l1);
+    }
   }
   l0 = wave_sum(l0);
   l1 = wave_sum(l1);
@@ -763,6 +782,7 @@ hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const fl
 
 hipError_t launch_gap_classifier(const bf16_t* x, int HW, int C, const float* w, const float* b, float* logits,
                                  float* score, int score_stride, int B, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;  // 16-B channel groups
   hipLaunchKernelGGL(gap_classifier_kernel, dim3(B), dim3(256), 0, s, x, HW, C, w, b, logits, score, score_stride);
   return hipGetLastError();
 }

@@ -7,49 +7,65 @@
 namespace {
 
 // misinfo_forensics.py:57-69, 97-98, 342-347: two Linear(768,256)-ReLU-Linear(256,2) heads on the
-// CLS row, softmax[:, 1].  Block = 4 rows; thread j = hidden unit j; W1 stored transposed [768][256]
-// so a k-step reads one coalesced 1-KB row.
-__global__ __launch_bounds__(256) void text_heads_kernel(const float* x, int row_stride, const float* w1a,
+// CLS row, softmax[:, 1].  Block = 4 rows; W1 stored transposed [768][256] so a k-step of the 256
+// hidden units reads one coalesced 1-KB row.
+__global__ __launch_bounds__(1024) void text_heads_kernel(const float* x, int row_stride, const float* w1a,
                                                          const float* b1a, const float* w2a, const float* b2a,
                                                          const float* w1m, const float* b1m, const float* w2m,
                                                          const float* b2m, float* ai_logits, float* mi_logits,
                                                          float* scores, int score_stride, int B) {
+  // 1024 threads: hidden unit h = tid % 256 of K-slice ks = tid / 256 (192 inputs each), so each
+  // thread's dependent load/FMA chain is a quarter of the 768; slices combined in fixed order.
+  constexpr int KS = 4, KL = 768 / KS;
   __shared__ float xs[4][768];
-  __shared__ float red[4][4][4];  // [wave][row][head*2+o]
-  const int tid = threadIdx.x, r0 = blockIdx.x * 4;
-  for (int i = tid; i < 4 * 768; i += 256) {
+  __shared__ float hp[KS][2][4][256];  // [slice][head][row][hidden] partial sums
+  __shared__ float red[4][4][4];       // [wave][row][head*2+o]
+  const int tid = threadIdx.x, r0 = blockIdx.x * 4, h = tid & 255, ks = tid >> 8;
+  for (int i = tid; i < 4 * 768; i += 1024) {
     const int r = i / 768, c = i % 768;
     xs[r][c] = (r0 + r < B) ? x[(size_t)(r0 + r) * row_stride + c] : 0.f;
   }
   __syncthreads();
-  float part[4][4];
 #pragma unroll
   for (int head = 0; head < 2; ++head) {
-    const float* w1 = head ? w1m : w1a;
-    const float* b1 = head ? b1m : b1a;
-    const float* w2 = head ? w2m : w2a;
+    const float* w1 = (head ? w1m : w1a) + (size_t)ks * KL * 256 + h;
     float hsum[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < 768; ++k) {
-      const float w = w1[(size_t)k * 256 + tid];
+#pragma unroll 8
+    for (int k = 0; k < KL; ++k) {
+      const float w = w1[(size_t)k * 256];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) hsum[r] = fmaf(w, xs[r][k], hsum[r]);
+      for (int r = 0; r < 4; ++r) hsum[r] = fmaf(w, xs[r][ks * KL + k], hsum[r]);
     }
-    const float w20 = w2[tid], w21 = w2[256 + tid], bb = b1[tid];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float hv = fmaxf(hsum[r] + bb, 0.f);
-      part[r][head * 2 + 0] = hv * w20;
-      part[r][head * 2 + 1] = hv * w21;
-    }
+    for (int r = 0; r < 4; ++r) hp[ks][head][r][h] = hsum[r];
   }
-  const int lane = tid & 63, wave = tid >> 6;
+  __syncthreads();
+  if (tid < 256) {  // waves 0-3: hidden units -> ReLU -> the 2 x 2 output logits per row
+    float part[4][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+    for (int head = 0; head < 2; ++head) {
+      const float* b1 = head ? b1m : b1a;
+      const float* w2 = head ? w2m : w2a;
+      const float w20 = w2[h], w21 = w2[256 + h], bb = b1[h];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      const float v = wave_sum(part[r][o]);
-      if (lane == 0) red[wave][r][o] = v;
+      for (int r = 0; r < 4; ++r) {
+        float hs = hp[0][head][r][h];
+#pragma unroll
+        for (int q = 1; q < KS; ++q) hs += hp[q][head][r][h];
+        const float hv = fmaxf(hs + bb, 0.f);
+        part[r][head * 2 + 0] = hv * w20;
+        part[r][head * 2 + 1] = hv * w21;
+      }
     }
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        const float v = wave_sum(part[r][o]);
+        if (lane == 0) red[wave][r][o] = v;
+      }
+  }
   __syncthreads();
   if (tid < 4 && r0 + tid < B) {
     const int r = tid, row = r0 + r;
@@ -134,29 +150,42 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* a, const float
   if (lane == 0) out[(size_t)row * ostride] = s;
 }
 
-// S[B][N] = Q[B][D] . V[N][D]^T, fp32 (misinfo_forensics.py:446).  Tile 16 queries x 64 rows.
+// S[B][N] = Q[B][D] . V[N][D]^T, fp32 (misinfo_forensics.py:446).  Tile 16 queries x 64 rows,
+// 64-deep K chunks staged through LDS with 16-B loads; the next chunk's loads (clamped rows,
+// no divergent region) are in flight while the current one is consumed.  Every output is one
+// fp32 FMA chain over k = 0 .. D-1 in order.  D % 64 == 0 (host-checked).
 __global__ __launch_bounds__(256) void vault_sims_kernel(const float* q, const float* v, float* S, int B, int N,
                                                          int D) {
-  __shared__ float qs[16][33];
-  __shared__ float vs[64][33];
+  constexpr int KC = 64, LD = KC + 4;  // row stride 68 floats: 16-B aligned, rows 4 banks apart
+  __shared__ __attribute__((aligned(16))) float qs[16 * LD];
+  __shared__ __attribute__((aligned(16))) float vs[64 * LD];
   const int tid = threadIdx.x, tq = tid >> 4, tv = tid & 15;
   const int q0 = blockIdx.y * 16, v0 = blockIdx.x * 64;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < D; k0 += 32) {
-    for (int i = tid; i < 16 * 32; i += 256) {
-      const int r = i >> 5, c = i & 31;
-      qs[r][c] = (q0 + r < B) ? q[(size_t)(q0 + r) * D + k0 + c] : 0.f;
-    }
-    for (int i = tid; i < 64 * 32; i += 256) {
-      const int r = i >> 5, c = i & 31;
-      vs[r][c] = (v0 + r < N) ? v[(size_t)(v0 + r) * D + k0 + c] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int k = 0; k < 32; ++k) {
-      const float a = qs[tq][k];
+  // this thread's chunk pieces: one float4 of Q (row tid / 16, col 4 (tid % 16)), four of V
+  const int qr = tid >> 4, qc = (tid & 15) * 4;
+  const float* qp = q + (size_t)min(q0 + qr, B - 1) * D + qc;
+  const float* vp[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = fmaf(a, vs[tv + 16 * j][k], acc[j]);
+  for (int i = 0; i < 4; ++i) vp[i] = v + (size_t)min(v0 + qr + 16 * i, N - 1) * D + qc;
+  float4 rq, rv[4];
+  auto load = [&](int k0) {
+    rq = *reinterpret_cast<const float4*>(qp + k0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rv[i] = *reinterpret_cast<const float4*>(vp[i] + k0);
+  };
+  load(0);
+  for (int k0 = 0; k0 < D; k0 += KC) {
+    *reinterpret_cast<float4*>(qs + qr * LD + qc) = rq;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(vs + (qr + 16 * i) * LD + qc) = rv[i];
+    __syncthreads();
+    if (k0 + KC < D) load(k0 + KC);
+#pragma unroll 16
+    for (int k = 0; k < KC; ++k) {
+      const float a = qs[tq * LD + k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(a, vs[(tv + 16 * j) * LD + k], acc[j]);
     }
     __syncthreads();
   }
@@ -240,7 +269,7 @@ hipError_t launch_text_heads(const float* x, int row_stride, const float* w1a, c
                              const float* b2a, const float* w1m, const float* b1m, const float* w2m,
                              const float* b2m, float* ai_logits, float* mi_logits, float* scores, int score_stride,
                              int B, hipStream_t s) {
-  hipLaunchKernelGGL(text_heads_kernel, dim3((B + 3) / 4), dim3(256), 0, s, x, row_stride, w1a, b1a, w2a, b2a, w1m,
+  hipLaunchKernelGGL(text_heads_kernel, dim3((B + 3) / 4), dim3(1024), 0, s, x, row_stride, w1a, b1a, w2a, b2a, w1m,
                      b1m, w2m, b2m, ai_logits, mi_logits, scores, score_stride, B);
   return hipGetLastError();
 }
@@ -259,7 +288,8 @@ hipError_t launch_rowdot(const float* a, const float* c, float* out, int ostride
 }
 
 hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s) {
-  if (D & 31) return hipErrorInvalidValue;
+  if (D & 63) return hipErrorInvalidValue;
+  if (B <= 0 || N <= 0) return hipSuccess;
   hipLaunchKernelGGL(vault_sims_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
   return hipGetLastError();
 }
