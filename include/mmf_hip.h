@@ -67,7 +67,8 @@ int mmf_ready(mmf_handle* h);
 int mmf_reserve(mmf_handle* h, int max_batch, int max_text_len, int max_clip_len);
 
 /* Signals 1-2 — analyze_text (misinfo_forensics.py:319-352): RoBERTa + dual heads.
- * ids/mask int32 [B, L] device.  Outputs fp32 [B, 2] logits each (may be NULL) and
+ * ids/mask int32 [B, L <= 512] device (the reference tokenizer truncates at 512, :327-333; L > 128
+ * takes the long-sequence attention kernel).  Outputs fp32 [B, 2] logits each (may be NULL) and
  * scores fp32 [B, 2] = softmax(.)[:,1] of (ai, misinfo) (may be NULL). */
 int mmf_text_forward(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L,
                      float* ai_logits, float* misinfo_logits, float* scores2, void* stream);
@@ -146,7 +147,7 @@ int mmf_gemm_bf16_ex(const void* A, int lda, const void* W, int ldw, const float
                      void* stream);
 
 /* Low-level attention op for tests: qkv bf16 [B*L, 3*H*64] (q|k|v), mask int32 [B,L] or NULL,
- * causal 0/1 -> out bf16 [B*L, H*64]. */
+ * causal 0/1 -> out bf16 [B*L, H*64].  L <= 512. */
 int mmf_attention_bf16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,
                        void* stream);
 

@@ -323,9 +323,17 @@ class MisinfoForensics:
         if self.roberta_tokenizer is None:
             raise RuntimeError("no RoBERTa tokenizer (pass roberta_tokenizer=)")
         ids = io_utils.tokenize_roberta(self.roberta_tokenizer, text)
-        if len(ids) > self.engine.max_text_len:
-            raise ValueError(f"text of {len(ids)} tokens exceeds the reserved length {self.engine.max_text_len}")
+        self._fit_text(len(ids))
         return np.asarray([ids], dtype=np.int32)
+
+    def _fit_text(self, n_tokens: int) -> None:
+        """The tokenizer truncates at 512 (misinfo_forensics.py:327-333); workspaces are reserved for
+        `max_text_len` (128 by default) and grown to the full 512 the first time a longer text
+        arrives, so every text the reference accepts runs on the device."""
+        if n_tokens > self.engine.max_text_len:
+            if n_tokens > 512:
+                raise ValueError(f"text of {n_tokens} tokens: RoBERTa positions end at 512")
+            self.engine.reserve(self.engine.max_batch, 512, self.engine.max_clip_len)
 
     def _clip_ids(self, texts: List[str], truncation: bool = False):
         if self.clip_processor is None:
@@ -498,6 +506,7 @@ class MisinfoForensics:
         reference's result dicts."""
         rob = [io_utils.tokenize_roberta(self.roberta_tokenizer, t) for t in texts]
         rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
+        self._fit_text(rid.shape[1])
         cid, cm = self._clip_ids(list(texts))
         pils = [io_utils.to_pil(i) for i in images]
         eff = np.stack([io_utils.effnet_pixels(p) for p in pils])

@@ -1,4 +1,5 @@
-// Fused multi-head attention for the three encoders (head_dim 64, sequence <= 128):
+// Fused multi-head attention for the three encoders (head_dim 64, sequence <= 128; RoBERTa up to 512
+// by attention_long_kernel below):
 //   RoBERTa  L=128, 12 heads, key-padding mask          (TF roberta:158-251)
 //   CLIP ViT L=50,  12 heads, no mask                    (TF clip:280-333)
 //   CLIP txt L=77,   8 heads, causal + key-padding mask  (TF clip:494-590)
@@ -171,11 +172,166 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
   }
 }
 
+// Sequences of 129..512 tokens (RoBERTa truncates at 512, misinfo_forensics.py:327-333): the whole
+// head's K and V (up to 2 x 64 KB) stay resident in LDS (one workgroup per CU) and each 16-query
+// tile walks the keys in 128-key chunks with an online softmax (running max / sum per query, O
+// rescaled when the max grows).  The S^T / P^T-in-registers / transposed-V formulation is the one
+// of attention_kernel above; P is rounded to bf16 unnormalised (<= 1) and O divided by the sum at
+// the end.
+constexpr int LLONG = 512, KCH = 128;
+
+__global__ __launch_bounds__(256) void attention_long_kernel(const bf16_t* __restrict__ qkv, int ld,
+                                                             const int32_t* __restrict__ mask,
+                                                             bf16_t* __restrict__ out, int ldo, int L, int H,
+                                                             int causal) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[LLONG * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[LLONG * 64];
+  __shared__ __attribute__((aligned(16))) float kbias[LLONG];
+
+  const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
+  const int D = H * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Lk = (L + 31) & ~31;
+  const bf16_t* base = qkv + (size_t)bi * L * ld;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nqt = (L + 15) >> 4;
+
+  // stage K and V in batches of 4 x 16 B per thread (loads of a batch issued before its stores)
+  for (int c0 = 0; c0 < Lk * 8; c0 += 4 * 256) {
+    uint4 kr[4], vr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + tid + i * 256, key = c >> 3, kc = c & 7;
+      kr[i] = make_uint4(0, 0, 0, 0);
+      vr[i] = make_uint4(0, 0, 0, 0);
+      if (key < L) {
+        kr[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + D + h * 64 + kc * 8);
+        vr[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + 2 * D + h * 64 + kc * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + tid + i * 256, key = c >> 3, kc = c & 7;
+      if (key < Lk) {
+        *reinterpret_cast<uint4*>(Ks + kv_swz(key, kc)) = kr[i];
+        *reinterpret_cast<uint4*>(Vs + kv_swz(key, kc)) = vr[i];
+      }
+    }
+  }
+  for (int k = tid; k < Lk; k += 256)
+    kbias[k] = (k < L && (!mask || mask[(size_t)bi * L + k])) ? 0.f : -INFINITY;
+  __syncthreads();
+
+#pragma unroll 1
+  for (int qt = wave; qt < nqt; qt += 4) {
+    const int qq = qt * 16 + fr;
+    bf16x8 qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (qq < L) v = *reinterpret_cast<const uint4*>(base + (size_t)qq * ld + h * 64 + ks * 32 + fg * 8);
+      qf[ks] = as_bf16x8(v);
+    }
+    float m = -INFINITY, sum = 0.f;
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int k0 = 0; k0 < Lk; k0 += KCH) {
+      const int nkt = min(KCH, Lk - k0) >> 4;  // 16-key tiles in this chunk (even: Lk % 32 == 0)
+      f32x4 s[KCH / 16];
+#pragma unroll
+      for (int j = 0; j < KCH / 16; ++j) {
+        s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (j < nkt) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            const int key = k0 + j * 16 + fr, kc = ks * 4 + fg;
+            const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
+            s[j] = mfma16x16x32(kf, qf[ks], s[j]);
+          }
+        }
+      }
+      float mc = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < KCH / 16; ++j) {
+        if (j < nkt) {
+          const float4 kb = *reinterpret_cast<const float4*>(kbias + k0 + j * 16 + fg * 4);
+          const float kbr[4] = {kb.x, kb.y, kb.z, kb.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = s[j][r] * 0.125f + kbr[r];
+            if (causal && k0 + j * 16 + fg * 4 + r > qq) v = -INFINITY;
+            s[j][r] = v;
+            mc = fmaxf(mc, v);
+          }
+        }
+      }
+      mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+      mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+      const float mn = fmaxf(m, mc);
+      const float alpha = (m == -INFINITY) ? 0.f : __expf(m - mn);  // m == -inf: nothing accumulated yet
+      m = mn;
+      float cs = 0.f;
+#pragma unroll
+      for (int j = 0; j < KCH / 16; ++j) {
+        if (j < nkt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = (mn == -INFINITY) ? 0.f : __expf(s[j][r] - mn);
+            s[j][r] = e;
+            cs += e;
+          }
+        }
+      }
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      sum = sum * alpha + cs;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < KCH / 32; ++kb) {
+        if (2 * kb < nkt) {
+          const uint4 pk = make_uint4(pack2bf(s[2 * kb][0], s[2 * kb][1]), pack2bf(s[2 * kb][2], s[2 * kb][3]),
+                                      pack2bf(s[2 * kb + 1][0], s[2 * kb + 1][1]),
+                                      pack2bf(s[2 * kb + 1][2], s[2 * kb + 1][3]));
+          const bf16x8 pf = as_bf16x8(pk);
+          const int key0 = k0 + kb * 32 + fg * 4 + (fr >> 2), p = fr & 3;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const int c = dt * 2 + (p >> 1), e = (p & 1) * 4;
+            const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + kv_swz(key0, c) + e));
+            const i16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + kv_swz(key0 + 16, c) + e));
+            const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+            o[dt] = mfma16x16x32(as_bf16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
+          }
+        }
+      }
+    }
+    if (qq < L) {
+      const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+      bf16_t* dst = out + ((size_t)bi * L + qq) * ldo + h * 64 + fg * 4;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *reinterpret_cast<uint2*>(dst + dt * 16) =
+            make_uint2(pack2bf(o[dt][0] * inv, o[dt][1] * inv), pack2bf(o[dt][2] * inv, o[dt][3] * inv));
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, bf16_t* out, int ldo, int B, int L,
                             int H, int causal, hipStream_t s) {
-  if (L <= 0 || L > LMAX || (ldqkv & 7) || (ldo & 3)) return hipErrorInvalidValue;
+  if (L <= 0 || L > LLONG || (ldqkv & 7) || (ldo & 3)) return hipErrorInvalidValue;
+  if (L > LMAX) {
+    hipLaunchKernelGGL(attention_long_kernel, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H,
+                       causal);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(attention_kernel, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal);
   return hipGetLastError();
 }

@@ -807,7 +807,6 @@ int mmf_ready(mmf_handle* h) { return h ? h->ready : 0; }
 int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   if (!h || B <= 0 || Lr <= 0 || Lr > 512 || Lc <= 0 || Lc > 77)
     return fail(MMF_EINVAL, "mmf_reserve: bad shape B=%d Lr=%d Lc=%d", B, Lr, Lc);
-  if (Lr > 128) return fail(MMF_EINVAL, "mmf_reserve: RoBERTa length %d > 128 not supported yet", Lr);
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipDeviceSynchronize());
   for (void* p : h->ws_allocs) (void)hipFree(p);
@@ -878,7 +877,7 @@ int mmf_text_forward(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
                      float* scores2, void* stream) {
   if (!h || !ids || !mask) return fail(MMF_EINVAL, "null argument");
   if (!(h->ready & 1)) return fail(MMF_EINVAL, "text model (RoBERTa + heads) not loaded");
-  if (L > 128) return fail(MMF_EINVAL, "RoBERTa length %d > 128 not supported yet", L);
+  if (L > 512) return fail(MMF_EINVAL, "RoBERTa length %d > 512 (position table ends at 514)", L);
   CHK(check_cap(h, B, L, 1));
   HIPCHK(hipSetDevice(h->device));
   return run_text(h, ids, mask, B, L, ai, mi, scores2, 2, (hipStream_t)stream);
@@ -984,7 +983,7 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   if (!h || !rob_ids || !rob_mask || !clip_ids || !clip_mask || !img_eff || !scores5 || !probs2)
     return fail(MMF_EINVAL, "null argument");
   if ((h->ready & 31) != 31) return fail(MMF_EINVAL, "not all models loaded (ready mask %d)", h->ready);
-  if (Lr > 128 || Lc > 77) return fail(MMF_EINVAL, "lengths Lr=%d (<=128) Lc=%d (<=77)", Lr, Lc);
+  if (Lr > 512 || Lc > 77) return fail(MMF_EINVAL, "lengths Lr=%d (<=512) Lc=%d (<=77)", Lr, Lc);
   CHK(check_cap(h, B, Lr, Lc));
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;

@@ -60,6 +60,20 @@ def test_analyze_pairs_match_reference(forensics, golden_json, golden_inputs):
         _check(forensics.analyze(text=f"sample text {i}", image_path=_pil(golden_inputs, i), verbose=False), ref)
 
 
+def test_long_text_analyze_text(forensics, det_sd, clip_sd):
+    """A 400-token article (past the 128 reserved by default; the reference truncates at 512):
+    the workspaces grow and analyze_text matches the oracle's single-text forward."""
+    import mmf_amd.synthetic as syn
+    from oracle.pipeline import OracleForensics
+    ids, _ = syn.roberta_ids(1, 400, 91)
+    forensics.roberta_tokenizer.table["long article"] = ids[0].tolist()
+    got = forensics.analyze_text("long article")
+    assert forensics.engine.max_text_len == 512
+    ref = OracleForensics(det_sd, clip_sd).analyze_text(ids[0])
+    for k in ("ai_score", "misinfo_score"):
+        assert abs(got[k] - ref[k]) < TOL, (k, got[k], ref[k])
+
+
 def test_analyze_single_modalities(forensics, golden_json, golden_inputs):
     for n, i in enumerate((0, 1)):
         _check(forensics.analyze(text=f"sample text {i}", verbose=False), golden_json["analyze_text_only"][n])

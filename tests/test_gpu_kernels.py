@@ -158,6 +158,9 @@ def _attn_ref(qkv, mask, B, L, H, causal):
 
 @pytest.mark.parametrize("B,L,H,causal,masked", [
     (3, 128, 12, 0, True), (4, 50, 12, 0, False), (5, 77, 8, 1, True), (2, 5, 12, 0, True), (2, 33, 8, 1, False),
+    # L > 128: attention_long_kernel (K/V resident in LDS, online softmax over 128-key chunks)
+    (3, 512, 12, 0, True), (2, 512, 12, 0, False), (3, 200, 12, 0, True), (2, 129, 8, 1, True),
+    (2, 300, 12, 1, False),
 ])
 def test_attention_vs_torch_fp32(lib, B, L, H, causal, masked):
     import mmf_amd.hip as hip

@@ -151,3 +151,24 @@ def test_compile_time_dwconv_matches_runtime_geometry(engine, monkeypatch):
     _, s1 = engine.effnet_forward(imgs)
     torch.cuda.synchronize()
     np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
+
+
+def test_long_text_up_to_512(det_sd, clip_sd):
+    """RoBERTa inputs past 128 tokens (the reference truncates at 512, misinfo_forensics.py:327-333):
+    each padded row must score like the oracle's unpadded single-text analyze_text."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    from oracle.pipeline import OracleForensics
+    lens = [512, 300, 129, 17]
+    ids, mask = syn.roberta_ids(len(lens), 512, 77, lens)
+    eng = Engine(0, det_sd, clip_sd, max_batch=len(lens), max_text_len=512)
+    _, _, sc = eng.text_forward(ids, mask)
+    torch.cuda.synchronize()
+    sc = sc.cpu().numpy()
+    orc = OracleForensics(det_sd, clip_sd)
+    for i, n in enumerate(lens):
+        r = orc.analyze_text(ids[i, :n])
+        assert abs(sc[i, 0] - r["ai_score"]) < TOL and abs(sc[i, 1] - r["misinfo_score"]) < TOL, (i, n, sc[i], r)
+    eng.close()
