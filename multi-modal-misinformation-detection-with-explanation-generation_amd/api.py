@@ -502,8 +502,16 @@ class MisinfoForensics:
                 "explanation": exp}
 
     def analyze_pairs(self, texts: List[str], images: List) -> List[Dict]:
-        """Batched analyze() for text+image pairs: one analyze_batch launch sequence, then the
-        reference's result dicts."""
+        """Batched analyze() for text+image pairs: one analyze_batch launch sequence per
+        `max_batch` pairs, then the reference's result dicts (one per pair, in order)."""
+        if len(texts) != len(images):
+            raise ValueError(f"{len(texts)} texts vs {len(images)} images")
+        cap = self.engine.max_batch
+        if len(texts) > cap:
+            res = []
+            for i in range(0, len(texts), cap):
+                res.extend(self.analyze_pairs(texts[i:i + cap], images[i:i + cap]))
+            return res
         rob = [io_utils.tokenize_roberta(self.roberta_tokenizer, t) for t in texts]
         rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
         self._fit_text(rid.shape[1])

@@ -93,6 +93,24 @@ def test_batched_dicts_equal_single(forensics, golden_inputs):
         assert one["verdict"] == batch[i]["verdict"] and one["explanation"] == batch[i]["explanation"]
 
 
+def test_analyze_pairs_chunks_past_capacity(forensics, golden_inputs):
+    """More pairs than the reserved batch: analyze_pairs runs max_batch-sized chunks and returns
+    one dict per pair, in order, equal to the single-launch result."""
+    texts = [f"sample text {i % 8}" for i in range(10)]
+    imgs = [_pil(golden_inputs, i % 8) for i in range(10)]
+    full = forensics.analyze_pairs(texts, imgs)
+    e = forensics.engine
+    keep = (e.max_batch, e.max_text_len, e.max_clip_len)
+    e.reserve(4, keep[1], keep[2])
+    try:
+        chunked = forensics.analyze_pairs(texts, imgs)
+    finally:
+        e.reserve(*keep)
+    assert len(chunked) == 10
+    for a, b in zip(chunked, full):
+        _check(a, b)
+
+
 def test_detector_forward_methods(forensics, golden, golden_inputs):
     from oracle import models as M
     x = M.effnet_preprocess(torch.as_tensor(golden_inputs["imgs"]))
