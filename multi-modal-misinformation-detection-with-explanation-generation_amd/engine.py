@@ -174,6 +174,9 @@ class Engine:
                 "rule": torch.empty(B, dtype=torch.int32, device=d), "top_sims": self._f32(B, 5),
                 "top_idx": torch.empty((B, 5), dtype=torch.int32, device=d)}
 
+    def host_pipeline(self, B: int, Lr: int, Lc: int = 77) -> "HostPipeline":
+        return HostPipeline(self, B, Lr, Lc)
+
     def close(self) -> None:
         if getattr(self, "h", None):
             self.lib.mmf_destroy(self.h)
@@ -184,3 +187,56 @@ class Engine:
             self.close()
         except Exception:  # noqa: BLE001
             pass
+
+
+class HostPipeline:
+    """analyze_batch over batches that start in HOST memory (the boundary of analyze_pairs and of a
+    serving loop): two device input slots, H2D copies of batch i+1 on a copy stream while batch i
+    computes on the current stream (ids int32 + uint8 images, ~38.6 MB per 256 pairs), results
+    copied back into pinned host tensors.  Host inputs should be pinned (`torch.Tensor.pin_memory`)
+    for the copies to run asynchronously."""
+
+    _IN = ("rid", "rm", "cid", "cm", "img")
+
+    def __init__(self, eng: Engine, B: int, Lr: int, Lc: int = 77):
+        self.eng, self.B = eng, B
+        d = eng.device
+        shapes = {"rid": ((B, Lr), torch.int32), "rm": ((B, Lr), torch.int32), "cid": ((B, Lc), torch.int32),
+                  "cm": ((B, Lc), torch.int32), "img": ((B, 224, 224, 3), torch.uint8)}
+        self.slots = [{k: torch.empty(sh, dtype=dt, device=d) for k, (sh, dt) in shapes.items()} for _ in range(2)]
+        self.outs = [eng.alloc_outputs(B) for _ in range(2)]
+        self.host_out = [{k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in o.items()}
+                         for o in self.outs]
+        self.copy_stream = torch.cuda.Stream(device=d)
+        self.ready = [torch.cuda.Event() for _ in range(2)]
+        self.free = [torch.cuda.Event() for _ in range(2)]
+        self.done = [torch.cuda.Event() for _ in range(2)]
+        self.i = 0
+
+    def submit(self, batch: Dict[str, torch.Tensor]) -> int:
+        """Queue one host batch {rid, rm, cid, cm, img}; returns the slot whose results
+        `result(slot)` returns once the batch has finished.  Never blocks on the device except
+        when the slot is still in use by the batch submitted two calls earlier."""
+        k = self.i & 1
+        main = torch.cuda.current_stream(self.eng.device)
+        if self.i >= 2:
+            self.done[k].synchronize()  # the host copy of that slot's previous results is complete
+        with torch.cuda.stream(self.copy_stream):
+            if self.i >= 2:
+                self.copy_stream.wait_event(self.free[k])  # compute of batch i-2 has read the slot
+            for n in self._IN:
+                self.slots[k][n].copy_(batch[n], non_blocking=True)
+            self.ready[k].record(self.copy_stream)
+        main.wait_event(self.ready[k])
+        sl = self.slots[k]
+        self.eng.analyze_batch(sl["rid"], sl["rm"], sl["cid"], sl["cm"], sl["img"], out=self.outs[k])
+        self.free[k].record(main)
+        for n, v in self.outs[k].items():
+            self.host_out[k][n].copy_(v, non_blocking=True)
+        self.done[k].record(main)
+        self.i += 1
+        return k
+
+    def result(self, slot: int) -> Dict[str, torch.Tensor]:
+        self.done[slot].synchronize()
+        return self.host_out[slot]

@@ -172,3 +172,30 @@ def test_long_text_up_to_512(det_sd, clip_sd):
         r = orc.analyze_text(ids[i, :n])
         assert abs(sc[i, 0] - r["ai_score"]) < TOL and abs(sc[i, 1] - r["misinfo_score"]) < TOL, (i, n, sc[i], r)
     eng.close()
+
+
+def test_host_pipeline_matches_device_batches(engine, golden_inputs):
+    """engine.HostPipeline (host inputs, double-buffered H2D on a copy stream) returns, per
+    submitted batch, exactly what analyze_batch returns for the same device-resident batch."""
+    import mmf_amd.synthetic as syn
+    B = 16
+    batches = []
+    for seed in (5, 6, 7):
+        rid, rm = syn.roberta_ids(B, 128, seed, [128, 70, 9])
+        cid, cm = syn.clip_ids(B, 77, seed, [77, 30, 4])
+        batches.append({"rid": torch.from_numpy(rid).pin_memory(), "rm": torch.from_numpy(rm).pin_memory(),
+                        "cid": torch.from_numpy(cid).pin_memory(), "cm": torch.from_numpy(cm).pin_memory(),
+                        "img": torch.from_numpy(syn.images(B, seed)).pin_memory()})
+    pipe = engine.host_pipeline(B, 128, 77)
+    got = []
+    for i, b in enumerate(batches):
+        slot = pipe.submit(b)
+        if i >= 1:
+            got.append({k: v.clone() for k, v in pipe.result(prev).items()})
+        prev = slot
+    got.append({k: v.clone() for k, v in pipe.result(prev).items()})
+    for b, g in zip(batches, got):
+        ref = engine.analyze_batch(b["rid"], b["rm"], b["cid"], b["cm"], b["img"])
+        torch.cuda.synchronize()
+        for k, v in ref.items():
+            assert torch.equal(v.cpu(), g[k]), k
