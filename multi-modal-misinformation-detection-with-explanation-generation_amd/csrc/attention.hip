@@ -26,7 +26,7 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 MMF_DEV int kv_swz(int key, int kc) { return key * 64 + ((kc ^ (key & 7)) << 3); }
 
-__global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict__ qkv, int ld,
+__global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restrict__ qkv, int ld,
                                                         const int32_t* __restrict__ mask, bf16_t* __restrict__ out,
                                                         int ldo, int L, int H, int causal) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[LMAX * 64];

@@ -84,6 +84,9 @@ struct Workspace {
   // EfficientNet
   bf16_t *e_a = nullptr, *e_b = nullptr, *e_exp = nullptr, *e_dw = nullptr;
   float *e_pool = nullptr, *e_scale = nullptr;
+  // split-K partials of the skinny-M GEMMs, one per tower (the towers run on concurrent streams)
+  float *sk_text = nullptr, *sk_vit = nullptr, *sk_ctext = nullptr;
+  size_t sk_elems = 0;
   // vault
   float* s_sims = nullptr;
   int s_cap_n = 0;
@@ -451,6 +454,12 @@ GemmArgs gemm_args(const bf16_t* A, int lda, const Lin16& l, int M) {
   return g;
 }
 
+GemmArgs with_ws(GemmArgs g, float* ws, size_t elems) {
+  g.ws = ws;
+  g.ws_elems = elems;
+  return g;
+}
+
 int gemm(mmf_handle* h, const GemmArgs& g, hipStream_t s) {
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
@@ -527,17 +536,17 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
     }
     const int Mr = last ? B : M;            // rows after the attention
     const int rs = last ? L * 768 : 768;    // row stride of ctx / residual stream at this point
-    g = gemm_args(w.r_ctx, rs, Ly.o, Mr);
+    g = with_ws(gemm_args(w.r_ctx, rs, Ly.o, Mr), w.sk_text, w.sk_elems);
     g.res32 = w.r_x;
     g.ldr = rs;
     g.c32 = w.r_y;
     CHK(gemm(h, g, s));
     CHK(lnorm(h, w.r_y, 768, Ly.ln1, last ? w.r_y : w.r_x, 768, w.r_xb, 768, Mr, 768, s));
-    g = gemm_args(w.r_xb, 768, Ly.fc1, Mr);
+    g = with_ws(gemm_args(w.r_xb, 768, Ly.fc1, Mr), w.sk_text, w.sk_elems);
     g.act = 1;  // GELU-erf
     g.c16 = w.r_h;
     CHK(gemm(h, g, s));
-    g = gemm_args(w.r_h, 3072, Ly.fc2, Mr);
+    g = with_ws(gemm_args(w.r_h, 3072, Ly.fc2, Mr), w.sk_text, w.sk_elems);
     g.res32 = last ? w.r_y : w.r_x;
     g.c32 = last ? w.r_x : w.r_y;
     CHK(gemm(h, g, s));
@@ -556,7 +565,8 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
 // into compact buffers (xc fp32, ctxc bf16); on return xc holds them (before the final LN).
 int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, bf16_t* xb, bf16_t* qkv,
                      bf16_t* ctx, bf16_t* hid, const int32_t* mask, int causal, int B, int L,
-                     const int32_t* last_rows, float* xc, bf16_t* ctxc, hipStream_t s) {
+                     const int32_t* last_rows, float* xc, bf16_t* ctxc, float* skws, size_t sk_elems,
+                     hipStream_t s) {
   const int M = B * L;
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = layers[i];
@@ -566,16 +576,16 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
     CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
     if (i == 11) {
       HIPCHK(launch_gather_rows2(ctx, x, last_rows, L, H, ctxc, xc, B, s));
-      g = gemm_args(ctxc, H, Ly.o, B);
+      g = with_ws(gemm_args(ctxc, H, Ly.o, B), skws, sk_elems);
       g.res32 = xc;
       g.c32 = xc;
       CHK(gemm(h, g, s));
       CHK(lnorm(h, xc, H, Ly.ln2, nullptr, 0, xb, H, B, H, s));
-      g = gemm_args(xb, H, Ly.fc1, B);
+      g = with_ws(gemm_args(xb, H, Ly.fc1, B), skws, sk_elems);
       g.act = 2;  // quick_gelu
       g.c16 = hid;
       CHK(gemm(h, g, s));
-      g = gemm_args(hid, I, Ly.fc2, B);
+      g = with_ws(gemm_args(hid, I, Ly.fc2, B), skws, sk_elems);
       g.res32 = xc;
       g.c32 = xc;
       CHK(gemm(h, g, s));
@@ -619,13 +629,13 @@ int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStre
                                        h->v_layers[0].ln1.b, 1e-5f, w.v_x, w.v_xb, B, s));
   }
   CHK(run_clip_encoder(h, h->v_layers, 768, 3072, 12, w.v_x, w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50,
-                       nullptr, w.v_xc, w.v_ctxc, s));
+                       nullptr, w.v_xc, w.v_ctxc, w.sk_vit, w.sk_elems, s));
   HIPCHK(launch_gather_ln(w.v_xc, nullptr, 1, h->v_post.g, h->v_post.b, 1e-5f, w.v_cls, nullptr, B, 768, s));
   Lin16 pj;
   pj.w = h->v_proj;
   pj.out = 512;
   pj.in = 768;
-  g = gemm_args(w.v_cls, 768, pj, B);
+  g = with_ws(gemm_args(w.v_cls, 768, pj, B), w.sk_vit, w.sk_elems);
   g.c32 = emb;
   CHK(gemm(h, g, s));
   HIPCHK(launch_l2norm(emb, B, 512, s));
@@ -641,13 +651,13 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
   }
   HIPCHK(launch_eos_index(ids, w.t_eos, B, L, h->eos_id, s));
   CHK(run_clip_encoder(h, h->t_layers, 512, 2048, 8, w.t_x, w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, w.t_eos,
-                       w.t_xc, w.t_ctxc, s));
+                       w.t_xc, w.t_ctxc, w.sk_ctext, w.sk_elems, s));
   HIPCHK(launch_gather_ln(w.t_xc, nullptr, 1, h->t_final.g, h->t_final.b, 1e-5f, w.t_pool, nullptr, B, 512, s));
   Lin16 pj;
   pj.w = h->t_proj;
   pj.out = 512;
   pj.in = 512;
-  GemmArgs g = gemm_args(w.t_pool, 512, pj, B);
+  GemmArgs g = with_ws(gemm_args(w.t_pool, 512, pj, B), w.sk_ctext, w.sk_elems);
   g.c32 = emb;
   CHK(gemm(h, g, s));
   HIPCHK(launch_l2norm(emb, B, 512, s));
@@ -843,6 +853,10 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   CHK(A((void**)&w.v_ctxc, (size_t)B * 768 * 2));
   CHK(A((void**)&w.t_xc, (size_t)B * 512 * 4));
   CHK(A((void**)&w.t_ctxc, (size_t)B * 512 * 2));
+  w.sk_elems = (size_t)B * 9216;  // max over the compact layers of (K / 256) * N
+  CHK(A((void**)&w.sk_text, w.sk_elems * 4));
+  CHK(A((void**)&w.sk_vit, w.sk_elems * 4));
+  CHK(A((void**)&w.sk_ctext, w.sk_elems * 4));
   // EfficientNet activation sizes per image
   size_t max_io = 112 * 112 * 32, max_exp = 0, max_dw = 0, max_pool = 0, max_c = 1280;
   {

@@ -52,6 +52,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
+  if (gridDim.y > 1) {  // split-K slice z: K-range [z*K, (z+1)*K) (g.K = slice depth), fp32 partials
+    const int z = blockIdx.y;
+    g.A += (size_t)z * g.K;
+    g.W += (size_t)z * g.K;
+    g.c32 += (size_t)z * g.M * g.ldc;
+  }
   const int M = g.M, N = g.N, K = g.K;
   const int nk = (K + BK - 1) / BK;
 
@@ -654,6 +660,65 @@ hipError_t run(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Split-K reduction: C = act(sum_z P[z] + bias) (+ residual), the epilogue of gemm_bf16_kernel
+// in the same order; one thread per 4 consecutive columns.  res32 may alias c32 (in place).
+template <int ACT>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int S, GemmArgs g) {
+  const int nq = g.N >> 2;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= g.M * nq) return;
+  const int m = idx / nq, n = (idx - m * nq) * 4;
+  const size_t plane = (size_t)g.M * g.N;
+  const float* p = P + (size_t)m * g.N + n;
+  float4 acc = *reinterpret_cast<const float4*>(p);
+  for (int z = 1; z < S; ++z) {
+    const float4 v = *reinterpret_cast<const float4*>(p + z * plane);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  float v[4] = {acc.x, acc.y, acc.z, acc.w};
+  if (g.bias) {
+    const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
+    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+  }
+  if (ACT != ACT_NONE) act4<ACT>(v);
+  if (g.res32) {
+    const float4 r = *reinterpret_cast<const float4*>(g.res32 + (size_t)m * g.ldr + n);
+    v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+  } else if (g.res16) {
+    const uint2 r = *reinterpret_cast<const uint2*>(g.res16 + (size_t)m * g.ldr + n);
+    v[0] += lo_bf(r.x); v[1] += hi_bf(r.x); v[2] += lo_bf(r.y); v[3] += hi_bf(r.y);
+  }
+  if (g.c32) *reinterpret_cast<float4*>(g.c32 + (size_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+  if (g.c16)
+    *reinterpret_cast<uint2*>(g.c16 + (size_t)m * g.ldc + n) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+}
+
+// Skinny-M GEMMs with a deep K (the compact last encoder layers and projections, M = batch): the
+// 64x128 tiles alone give 16-96 workgroups, each walking K = 768..3072 serially (latency-bound).
+// Split K into S slices of 256 (grid.y = S, fp32 partials in a caller workspace) and reduce.
+template <int BM, int BN, int WGM, int WGN>
+hipError_t run_splitk(const GemmArgs& a, int S, hipStream_t s) {
+  const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
+  GemmArgs p{};
+  p.A = a.A; p.lda = a.lda; p.W = a.W; p.ldw = a.ldw;
+  p.c32 = a.ws; p.ldc = a.N;
+  p.M = a.M; p.N = a.N; p.K = a.K / S;
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p, tilesN);
+  const int threads = a.M * (a.N >> 2);
+  const dim3 grid((threads + 255) / 256);
+  switch (a.act) {
+    case ACT_NONE: hipLaunchKernelGGL(splitk_reduce_kernel<ACT_NONE>, grid, dim3(256), 0, s, a.ws, S, a); break;
+    case ACT_GELU: hipLaunchKernelGGL(splitk_reduce_kernel<ACT_GELU>, grid, dim3(256), 0, s, a.ws, S, a); break;
+    case ACT_QUICK_GELU:
+      hipLaunchKernelGGL(splitk_reduce_kernel<ACT_QUICK_GELU>, grid, dim3(256), 0, s, a.ws, S, a);
+      break;
+    case ACT_SILU: hipLaunchKernelGGL(splitk_reduce_kernel<ACT_SILU>, grid, dim3(256), 0, s, a.ws, S, a); break;
+    case ACT_RELU: hipLaunchKernelGGL(splitk_reduce_kernel<ACT_RELU>, grid, dim3(256), 0, s, a.ws, S, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 // The LDS-DMA kernel addresses its epilogue operands with 32-bit raw-buffer byte offsets.
@@ -726,6 +791,15 @@ int gemm_config(const GemmArgs& a) {
   return t128 < 384 ? 2 : 3;
 }
 
+int gemm_splitk_factor(const GemmArgs& a) {
+  // slices of 256 (4 K-steps) when that gives >= 2 of them; the partial planes need N % 4 == 0
+  // and 16-B aligned rows for the reduction's float4 accesses
+  if (a.ascale || (a.K % 256) || a.K < 512 || (a.N & 3) || (a.ldc & 3) || (a.ldr & 3)) return 1;
+  const char* e = getenv("MMF_GEMM_SPLITK");  // benchmarking override: 0 disables
+  if (e && *e == '0') return 1;
+  return a.K / 256;
+}
+
 const char* gemm_config_name(int c) {
   static const char* names[] = {"gemm_bf16<256,32,4,1>",  "gemm_bf16<256,64,4,1>",  "gemm_bf16<64,128,1,4>",
                                 "gemm_bf16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
@@ -746,7 +820,11 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
   switch (gemm_config(a)) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);
-    case 2: return run<64, 128, 1, 4>(a, s);
+    case 2: {
+      const int S = gemm_splitk_factor(a);
+      if (S > 1 && a.ws && (size_t)S * a.M * a.N <= a.ws_elems) return run_splitk<64, 128, 1, 4>(a, S, s);
+      return run<64, 128, 1, 4>(a, s);
+    }
     case 4: return run_glds<256, 256, 2, 4>(a, s);
     case 5: return run_glds<256, 128, 4, 2>(a, s);
     case 6: return run_glds<256, 192, 4, 2>(a, s);

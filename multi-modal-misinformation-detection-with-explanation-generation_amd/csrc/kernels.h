@@ -20,7 +20,12 @@ struct GemmArgs {
   int rows_per_batch;            // rows of A per batch item when ascale != null
   int M, N, K, act;
   int probe;                     // benchmarking probes (0 in production; see gemm.hip)
+  float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
+  size_t ws_elems;               // its capacity in floats
 };
+// split-K factor the skinny-M (M <= 512) GEMM path uses for this (K) -- independent of M, so
+// results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
+int gemm_splitk_factor(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
 const char* gemm_config_name(int c);

@@ -194,20 +194,24 @@ __global__ __launch_bounds__(256) void clip_vision_assemble_kernel(const float* 
   store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
 }
 
-__global__ void eos_index_kernel(const int32_t* ids, int32_t* out, int B, int L, int eos) {
-  const int bi = blockIdx.x * blockDim.x + threadIdx.x;
+// EOS pooling index per sequence (TF clip:561-582): one wave per row, lanes stride the positions,
+// one wave reduction (the sequential per-thread scan took ~21 us at B = 256 on one workgroup).
+__global__ __launch_bounds__(256) void eos_index_kernel(const int32_t* ids, int32_t* out, int B, int L, int eos) {
+  const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (bi >= B) return;
   const int32_t* r = ids + (size_t)bi * L;
-  int best = 0;
-  if (eos == 2) {  // legacy configs: argmax(ids) (first maximal position)
-    int mv = r[0];
-    for (int t = 1; t < L; ++t)
-      if (r[t] > mv) { mv = r[t]; best = t; }
-  } else {
-    for (int t = 0; t < L; ++t)
-      if (r[t] == eos) { best = t; break; }
+  int key = eos == 2 ? -1 : 0x7fffffff;
+  for (int t = lane; t < L; t += 64) {
+    const int v = r[t];
+    if (eos == 2) key = max(key, v * 1024 + (1023 - t));  // argmax(ids), first maximal position (L <= 1024)
+    else if (v == eos) key = min(key, t);                  // first EOS position
   }
-  out[bi] = best;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int k2 = __shfl_xor(key, o, 64);
+    key = eos == 2 ? max(key, k2) : min(key, k2);
+  }
+  if (lane == 0) out[bi] = eos == 2 ? 1023 - (key & 1023) : (key == 0x7fffffff ? 0 : key);
 }
 
 template <int NV>
@@ -312,7 +316,8 @@ hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, c
 }
 
 hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int eos_id, hipStream_t s) {
-  hipLaunchKernelGGL(eos_index_kernel, dim3((B + 255) / 256), dim3(256), 0, s, ids, out, B, L, eos_id);
+  if (L > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(eos_index_kernel, dim3((B + 3) / 4), dim3(256), 0, s, ids, out, B, L, eos_id);
   return hipGetLastError();
 }
 

@@ -199,3 +199,28 @@ def test_host_pipeline_matches_device_batches(engine, golden_inputs):
         torch.cuda.synchronize()
         for k, v in ref.items():
             assert torch.equal(v.cpu(), g[k]), k
+
+
+def test_splitk_compact_layers_match_unsplit(engine, golden):
+    """The compact last encoder layers and projections (M = batch, K = 512..3072) run split-K
+    (fp32 partials over 256-deep K slices + a reduction with the same bias/act/residual order);
+    against the unsplit kernel only the fp32 summation order differs."""
+    import os
+    import mmf_amd.synthetic as syn
+    B = 64
+    rid, rm = syn.roberta_ids(B, 128, 21, [128, 77, 12])
+    cid, cm = syn.clip_ids(B, 77, 21, [77, 33, 6])
+    imgs = syn.images(B, 21)
+    outs = []
+    for v in ("0", "1"):
+        os.environ["MMF_GEMM_SPLITK"] = v
+        try:
+            o = engine.analyze_batch(rid, rm, cid, cm, imgs)
+            torch.cuda.synchronize()
+            outs.append({k: t.cpu().numpy() for k, t in o.items()})
+        finally:
+            os.environ.pop("MMF_GEMM_SPLITK", None)
+    a, b = outs
+    np.testing.assert_allclose(a["scores"], b["scores"], atol=2e-4)
+    np.testing.assert_allclose(a["probs"], b["probs"], atol=2e-4)
+    np.testing.assert_array_equal(a["top_idx"], b["top_idx"])
