@@ -126,7 +126,8 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
   constexpr int C = NV * 256;
-  for (int t = wave; t < L; t += 4) {
+  // blockIdx.y splits the sequence's rows over gridDim.y workgroups (each redoes the cheap scan)
+  for (int t = blockIdx.y * 4 + wave; t < L; t += 4 * gridDim.y) {
     float4 v[NV];
     load_row<NV>(v, word + (size_t)s_ids[t] * C, lane);
     add_row<NV>(v, type0, lane);
@@ -284,7 +285,8 @@ hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const flo
                                 const float* g, const float* b, float eps, float* x, bf16_t* xb, int B, int L,
                                 int H, int pad_id, hipStream_t s) {
   if (H != 768 || L > 512) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, x, xb, L,
+  // 4 workgroups per sequence: one per sequence left the chip at 256 workgroups (~77 us at B = 256)
+  hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B, 4), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, x, xb, L,
                      pad_id);
   return hipGetLastError();
 }
