@@ -224,3 +224,29 @@ def test_splitk_compact_layers_match_unsplit(engine, golden):
     np.testing.assert_allclose(a["scores"], b["scores"], atol=2e-4)
     np.testing.assert_allclose(a["probs"], b["probs"], atol=2e-4)
     np.testing.assert_array_equal(a["top_idx"], b["top_idx"])
+
+
+def test_effnet_config3_batch512(det_sd, clip_sd):
+    """BASELINE configs[2]: EfficientNet-B0 at B = 512 (the bench runs 256).  Sampled rows against
+    the fp32 oracle at the north-star tolerance, and every row of a slice bit-identical to the
+    same images run as a batch of 8 (size-independent property)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    from oracle import models as M
+    eng = Engine(0, det_sd, clip_sd, max_batch=512)
+    imgs = syn.images(512, 31)
+    lg, sc = eng.effnet_forward(imgs)
+    lg8, sc8 = eng.effnet_forward(imgs[200:208])
+    torch.cuda.synchronize()
+    sc, sc8 = sc.cpu().numpy(), sc8.cpu().numpy()
+    assert np.isfinite(sc).all() and ((sc >= 0) & (sc <= 1)).all()
+    np.testing.assert_array_equal(sc[200:208], sc8)
+    np.testing.assert_array_equal(lg.cpu().numpy()[200:208], lg8.cpu().numpy())
+    rows = [0, 137, 311, 511]
+    sd = M.to_torch(det_sd)
+    with torch.no_grad():
+        ref = torch.softmax(M.effnet_forward(sd, M.effnet_preprocess(torch.as_tensor(imgs[rows]))), 1)[:, 1].numpy()
+    np.testing.assert_allclose(sc[rows], ref, atol=TOL)
+    eng.close()
