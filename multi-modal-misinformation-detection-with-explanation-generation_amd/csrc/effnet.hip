@@ -566,7 +566,15 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
       const int o = wave + 16 * t;
       if (o < Csq) {
         const float* wr = w1 + (size_t)o * C;
-        for (int c = lane; c < C; c += 64) acc[t] = fmaf(wr[c], pooled[c], acc[t]);
+        int c = lane;
+        for (; c + 192 < C; c += 256) {  // 4 loads in flight per output (same ascending-c order)
+          const float w0 = wr[c], w1v = wr[c + 64], w2v = wr[c + 128], w3 = wr[c + 192];
+          acc[t] = fmaf(w0, pooled[c], acc[t]);
+          acc[t] = fmaf(w1v, pooled[c + 64], acc[t]);
+          acc[t] = fmaf(w2v, pooled[c + 128], acc[t]);
+          acc[t] = fmaf(w3, pooled[c + 192], acc[t]);
+        }
+        for (; c < C; c += 64) acc[t] = fmaf(wr[c], pooled[c], acc[t]);
       }
     }
 #pragma unroll
@@ -580,6 +588,20 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
   for (int c = tid; c < C; c += SE_THREADS) {
     float a0 = b2[c], a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int j = 0;
+    // 16 weight loads in flight per step (one L2 round trip per 16 inputs instead of per 4); the
+    // accumulation order is unchanged (input j -> accumulator j % 4, ascending j)
+    for (; j + 16 <= Csq; j += 16) {
+      float wv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) wv[u] = w2t[(size_t)(j + u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        a0 = fmaf(wv[u], s1[j + u], a0);
+        a1 = fmaf(wv[u + 1], s1[j + u + 1], a1);
+        a2 = fmaf(wv[u + 2], s1[j + u + 2], a2);
+        a3 = fmaf(wv[u + 3], s1[j + u + 3], a3);
+      }
+    }
     for (; j + 4 <= Csq; j += 4) {
       a0 = fmaf(w2t[(size_t)j * C + c], s1[j], a0);
       a1 = fmaf(w2t[(size_t)(j + 1) * C + c], s1[j + 1], a1);
