@@ -60,6 +60,33 @@ def test_analyze_pairs_match_reference(forensics, golden_json, golden_inputs):
         _check(forensics.analyze(text=f"sample text {i}", image_path=_pil(golden_inputs, i), verbose=False), ref)
 
 
+def test_no_vault_loaded(golden, golden_json, golden_inputs, det_sd, clip_sd):
+    """Truth-Vault not loaded (misinfo_forensics.py:422-428): search_vault returns the reference's
+    unloaded dict, analyze() and analyze_pairs() run the other four signals with
+    vault_discrepancy = 0 and no matches, and agree with the oracle's analyze without a vault."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from tables import TableClipProcessor, TableRobertaTokenizer
+    from misinfo_forensics import MisinfoForensics
+    from oracle.pipeline import OracleForensics
+    rob, clp = _tables(golden, golden_inputs)
+    mf = MisinfoForensics(fusion_weights="/nonexistent", faiss_index_path="/nonexistent",
+                          roberta_tokenizer=TableRobertaTokenizer(rob), clip_processor=TableClipProcessor(clp),
+                          detector_state=det_sd, clip_state=clip_sd, max_batch=8, verbose=False)
+    assert not mf.vault_loaded
+    assert mf.search_vault(_pil(golden_inputs, 0), "sample text 0") == golden_json["search_vault_unloaded"]
+    orc = OracleForensics(det_sd, clip_sd, eos_token_id=golden_inputs["eos"])
+    texts = [f"sample text {i}" for i in range(4)]
+    batch = mf.analyze_pairs(texts, [_pil(golden_inputs, i) for i in range(4)])
+    for i in range(4):
+        t = (golden["rob_ids"][i, :golden_inputs["rob_lens"][i]], golden["clip_ids"][i, :golden_inputs["clip_lens"][i]])
+        ref = orc.analyze(text=t, image=golden_inputs["imgs"][i])
+        assert ref["scores"]["vault_discrepancy"] == 0.0 and ref["vault_matches"] == []
+        for got in (mf.analyze(text=texts[i], image_path=_pil(golden_inputs, i), verbose=False), batch[i]):
+            _check(got, ref)
+    mf.engine.close()
+
+
 def test_long_text_analyze_text(forensics, det_sd, clip_sd):
     """A 400-token article (past the 128 reserved by default; the reference truncates at 512):
     the workspaces grow and analyze_text matches the oracle's single-text forward."""
