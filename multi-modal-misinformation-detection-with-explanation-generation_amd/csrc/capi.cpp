@@ -72,6 +72,7 @@ const int kStages[7][6] = {{1, 3, 1, 32, 16, 1},  {6, 3, 2, 16, 24, 2},   {6, 5,
 struct Workspace {
   // RoBERTa
   float *r_x = nullptr, *r_y = nullptr;
+  uint16_t* r_lo = nullptr;  // fp16 low part of the split post-LN residual stream (hi = r_xb)
   bf16_t *r_xb = nullptr, *r_qkv = nullptr, *r_ctx = nullptr, *r_h = nullptr;
   // CLIP vision
   bf16_t *v_col = nullptr, *v_xb = nullptr, *v_qkv = nullptr, *v_ctx = nullptr, *v_h = nullptr, *v_cls = nullptr;
@@ -489,6 +490,13 @@ int add_ln(mmf_handle* h, float* x, int ldx, const bf16_t* y, int ldy, const LNp
   return 0;
 }
 
+int add_ln_hilo(mmf_handle* h, bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy, const LNp& p, int rows,
+                hipStream_t s) {
+  ProfScope ps(h, s, PK_LN, 9.0 * rows * 768, (double)rows * 768 * (2 + 2 + 2 + 2 + 2));
+  HIPCHK(launch_add_ln_hilo(hi, lo, ld, y, ldy, p.g, p.b, 1e-5f, rows, 768, s));
+  return 0;
+}
+
 int check_cap(mmf_handle* h, int B, int Lr, int Lc) {
   if (B <= 0) return fail(MMF_EINVAL, "batch must be > 0 (got %d)", B);
   if (B > h->cap_b || Lr > h->cap_lr || Lc > h->cap_lc)
@@ -502,8 +510,8 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   Workspace& w = h->ws;
   const int M = B * L;
   {
-    ProfScope ps(h, s, PK_EMBED, 10.0 * M * 768, (double)M * 768 * (4 + 4 + 4 + 2));
-    HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, w.r_x,
+    ProfScope ps(h, s, PK_EMBED, 10.0 * M * 768, (double)M * 768 * (4 + 4 + 2 + 2));
+    HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, w.r_lo,
                                 w.r_xb, B, L, 768, 1, s));
   }
   for (int i = 0; i < 12; ++i) {
@@ -522,7 +530,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       g = gemm_args(w.r_ctx, 768, Ly.o, M);
       g.c16 = y;
       CHK(gemm(h, g, s));
-      CHK(add_ln(h, w.r_x, 768, y, 768, Ly.ln1, nullptr, w.r_x, w.r_xb, 768, M, 768, s));
+      CHK(add_ln_hilo(h, w.r_xb, w.r_lo, 768, y, 768, Ly.ln1, M, s));
       g = gemm_args(w.r_xb, 768, Ly.fc1, M);
       g.act = 1;  // GELU-erf
       g.c16 = w.r_h;
@@ -531,14 +539,16 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       g = gemm_args(w.r_h, 3072, Ly.fc2, M);
       g.c16 = y;
       CHK(gemm(h, g, s));
-      CHK(add_ln(h, w.r_x, 768, y, 768, Ly.ln2, nullptr, w.r_x, w.r_xb, 768, M, 768, s));
+      CHK(add_ln_hilo(h, w.r_xb, w.r_lo, 768, y, 768, Ly.ln2, M, s));
       continue;
     }
     const int Mr = last ? B : M;            // rows after the attention
-    const int rs = last ? L * 768 : 768;    // row stride of ctx / residual stream at this point
+    const int rs = last ? L * 768 : 768;    // row stride of ctx at this point
+    // the B CLS rows of the split residual stream, as fp32 (r_y, compact)
+    HIPCHK(launch_hilo_rows(w.r_xb, w.r_lo, rs, w.r_y, B, 768, s));
     g = with_ws(gemm_args(w.r_ctx, rs, Ly.o, Mr), w.sk_text, w.sk_elems);
-    g.res32 = w.r_x;
-    g.ldr = rs;
+    g.res32 = w.r_y;
+    g.ldr = 768;
     g.c32 = w.r_y;
     CHK(gemm(h, g, s));
     CHK(lnorm(h, w.r_y, 768, Ly.ln1, last ? w.r_y : w.r_x, 768, w.r_xb, 768, Mr, 768, s));
@@ -829,6 +839,7 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   CHK(A((void**)&w.r_x, Mr * 768 * 4));
   CHK(A((void**)&w.r_y, Mr * 768 * 4));
   CHK(A((void**)&w.r_xb, Mr * 768 * 2));
+  CHK(A((void**)&w.r_lo, Mr * 768 * 2));
   CHK(A((void**)&w.r_qkv, Mr * 2304 * 2));
   CHK(A((void**)&w.r_ctx, Mr * 768 * 2));
   CHK(A((void**)&w.r_h, Mr * 3072 * 2));

@@ -51,8 +51,13 @@ hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, b
 
 // RoBERTa embeddings + LayerNorm -> x fp32 [B*L][H], xb bf16 [B*L][H]
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
-                                const float* g, const float* b, float eps, float* x, bf16_t* xb, int B, int L,
+                                const float* g, const float* b, float eps, uint16_t* xlo, bf16_t* xb, int B, int L,
                                 int H, int pad_id, hipStream_t s);
+// RoBERTa post-LN residual stream split as hi = bf16(x) (also the GEMM operand), lo = fp16(x - hi)
+hipError_t launch_add_ln_hilo(bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy, const float* g,
+                              const float* b, float eps, int rows, int C, hipStream_t s);
+hipError_t launch_hilo_rows(const bf16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
+                            hipStream_t s);
 // CLIP text embeddings (tok + pos) -> x fp32, then LN1 of layer 0 -> xb bf16
 hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
                                   const float* b, float eps, float* x, bf16_t* xb, int B, int L, int H,

@@ -97,12 +97,79 @@ __global__ __launch_bounds__(256) void add_ln_kernel(const float* x, int ldx, co
   store_row<NV>(v, o32 ? o32 + (size_t)row * ldx : nullptr, o16 + (size_t)row * ldo, lane);
 }
 
+// RoBERTa's post-LN residual stream in split precision: x = hi + lo with hi = bf16(x) (the very
+// tensor the next GEMM reads) and lo = fp16(x - hi) (|lo| <= 2^-8 |x|; ~19 significant bits in
+// all, vs 24 for fp32).  4 bytes per element like fp32, but hi doubles as the bf16 GEMM operand,
+// so add+LN writes 4 instead of 6 bytes per element (12 -> 10 B/elem of HBM traffic).
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+MMF_DEV uint32_t pack2h(float a, float b) {
+  const f16x2_t h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, h);
+}
+MMF_DEV float lo_h(uint32_t w) { return (float)__builtin_bit_cast(f16x2_t, w).x; }
+MMF_DEV float hi_h(uint32_t w) { return (float)__builtin_bit_cast(f16x2_t, w).y; }
+
+template <int NV>
+MMF_DEV void store_row_hilo(const float4 (&v)[NV], bf16_t* hi, uint16_t* lo, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    const uint2 h = make_uint2(pack2bf(v[i].x, v[i].y), pack2bf(v[i].z, v[i].w));
+    *reinterpret_cast<uint2*>(hi + c) = h;
+    *reinterpret_cast<uint2*>(lo + c) = make_uint2(pack2h(v[i].x - lo_bf(h.x), v[i].y - hi_bf(h.x)),
+                                                   pack2h(v[i].z - lo_bf(h.y), v[i].w - hi_bf(h.y)));
+  }
+}
+
+// post-LN add+LayerNorm on the split stream: s = (hi + lo) + y; (hi, lo) = split(LN(s)), in place
+template <int NV>
+__global__ __launch_bounds__(256) void add_ln_hilo_kernel(bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy,
+                                                          const float* g, const float* b, float eps, int rows) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float4 v[NV];
+  uint2 xh[NV], xl[NV], a[NV];
+  bf16_t* hr = hi + (size_t)row * ld;
+  uint16_t* lr = lo + (size_t)row * ld;
+  const bf16_t* yr = y + (size_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    xh[i] = *reinterpret_cast<const uint2*>(hr + c);
+    xl[i] = *reinterpret_cast<const uint2*>(lr + c);
+    a[i] = *reinterpret_cast<const uint2*>(yr + c);
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i].x = (lo_bf(xh[i].x) + lo_h(xl[i].x)) + lo_bf(a[i].x);
+    v[i].y = (hi_bf(xh[i].x) + hi_h(xl[i].x)) + hi_bf(a[i].x);
+    v[i].z = (lo_bf(xh[i].y) + lo_h(xl[i].y)) + lo_bf(a[i].y);
+    v[i].w = (hi_bf(xh[i].y) + hi_h(xl[i].y)) + hi_bf(a[i].y);
+  }
+  ln_row<NV>(v, g, b, eps, NV * 256, lane);
+  store_row_hilo<NV>(v, hr, lr, lane);
+}
+
+// fp32 rows (hi + lo) of the split stream, gathered with a row stride (the last layer's CLS rows)
+__global__ __launch_bounds__(256) void hilo_rows_kernel(const bf16_t* hi, const uint16_t* lo, int row_stride,
+                                                        float* out, int B, int C) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  const bf16_t* hr = hi + (size_t)row * row_stride;
+  const uint16_t* lr = lo + (size_t)row * row_stride;
+  for (int c = lane * 4; c < C; c += 256) {
+    const uint2 h = *reinterpret_cast<const uint2*>(hr + c), l = *reinterpret_cast<const uint2*>(lr + c);
+    *reinterpret_cast<float4*>(out + (size_t)row * C + c) =
+        make_float4(lo_bf(h.x) + lo_h(l.x), hi_bf(h.x) + hi_h(l.x), lo_bf(h.y) + lo_h(l.y), hi_bf(h.y) + hi_h(l.y));
+  }
+}
+
 // RoBERTa: position ids = cumsum(ids != pad) * (ids != pad) + pad (TF roberta:142-155);
 // x = LN(word[id] + type[0] + pos[pid]).  One block per sequence.
 template <int NV>
 __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, const float* word, const float* pos,
                                                             const float* type0, const float* g, const float* b,
-                                                            float eps, float* x, bf16_t* xb, int L, int pad) {
+                                                            float eps, uint16_t* xlo, bf16_t* xb, int L, int pad) {
   __shared__ int s_ids[512];
   __shared__ int s_pos[512];
   const int bi = blockIdx.x, tid = threadIdx.x;
@@ -134,7 +201,7 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
     add_row<NV>(v, pos + (size_t)s_pos[t] * C, lane);
     ln_row<NV>(v, g, b, eps, C, lane);
     const size_t r = (size_t)bi * L + t;
-    store_row<NV>(v, x + r * C, xb + r * C, lane);
+    store_row_hilo<NV>(v, xb + r * C, xlo + r * C, lane);
   }
 }
 
@@ -282,11 +349,11 @@ hipError_t launch_add_ln(const float* x, int ldx, const bf16_t* y, int ldy, cons
 }
 
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
-                                const float* g, const float* b, float eps, float* x, bf16_t* xb, int B, int L,
+                                const float* g, const float* b, float eps, uint16_t* xlo, bf16_t* xb, int B, int L,
                                 int H, int pad_id, hipStream_t s) {
   if (H != 768 || L > 512) return hipErrorInvalidValue;
   // 4 workgroups per sequence: one per sequence left the chip at 256 workgroups (~77 us at B = 256)
-  hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B, 4), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, x, xb, L,
+  hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B, 4), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, xlo, xb, L,
                      pad_id);
   return hipGetLastError();
 }
@@ -344,5 +411,19 @@ hipError_t launch_gather_rows2(const bf16_t* a16, const float* a32, const int32_
 
 hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s) {
   hipLaunchKernelGGL(l2norm_kernel, dim3((B + 3) / 4), dim3(256), 0, s, x, B, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_ln_hilo(bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy, const float* g,
+                              const float* b, float eps, int rows, int C, hipStream_t s) {
+  if (C != 768 || (ld & 3) || (ldy & 3)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_ln_hilo_kernel<3>, dim3((rows + 3) / 4), dim3(256), 0, s, hi, lo, ld, y, ldy, g, b, eps, rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_hilo_rows(const bf16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
+                            hipStream_t s) {
+  if ((C & 3) || (row_stride & 3)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(hilo_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, s, hi, lo, row_stride, out, B, C);
   return hipGetLastError();
 }
