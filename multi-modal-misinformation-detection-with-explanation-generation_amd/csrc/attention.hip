@@ -26,25 +26,29 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 MMF_DEV int kv_swz(int key, int kc) { return key * 64 + ((kc ^ (key & 7)) << 3); }
 
+// LK = keys padded to the 32-deep PV k-step, a compile-time constant (32 / 64 / 96 / 128) so the
+// key-tile loops carry no runtime bounds: the K-fragment reads of a query tile batch up ahead of
+// its MFMAs instead of sitting in one basic block per key tile.
+template <int LK>
 __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restrict__ qkv, int ld,
                                                         const int32_t* __restrict__ mask, bf16_t* __restrict__ out,
                                                         int ldo, int L, int H, int causal) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[LMAX * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[LMAX * 64];
-  __shared__ __attribute__((aligned(16))) float kbias[LMAX];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[LK * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[LK * 64];
+  __shared__ __attribute__((aligned(16))) float kbias[LK];
 
   const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
   const int D = H * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int Lk = (L + 31) & ~31;  // keys padded to the 32-deep PV k-step
   const bf16_t* base = qkv + (size_t)bi * L * ld;
 
   const int fr = lane & 15, fg = lane >> 4;
-  const int nqt = (L + 15) >> 4, nkt = Lk >> 4;
+  const int nqt = (L + 15) >> 4;
+  constexpr int NKT = LK / 16;
   // stage K and V (swizzled rows); zero the padded keys so 0 * pad stays finite.  All global loads
   // (K, V and this wave's Q fragments for both of its query tiles) are issued before the first
   // LDS store so the whole workgroup has its 48 KB in flight at once.
-  constexpr int NIT = LMAX * 8 / 256, NQT = LMAX / 64;
+  constexpr int NIT = LK * 8 / 256, NQT = LMAX / 64;
   uint4 kr[NIT], vr[NIT];
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
@@ -70,13 +74,11 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
   }
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
-    const int c = tid + i * 256, key = c >> 3, kc = c & 7;
-    if (key < Lk) {
-      *reinterpret_cast<uint4*>(Ks + kv_swz(key, kc)) = kr[i];
-      *reinterpret_cast<uint4*>(Vs + kv_swz(key, kc)) = vr[i];
-    }
+    const int c = tid + i * 256, key = c >> 3, kc = c & 7;  // key < LK always
+    *reinterpret_cast<uint4*>(Ks + kv_swz(key, kc)) = kr[i];
+    *reinterpret_cast<uint4*>(Vs + kv_swz(key, kc)) = vr[i];
   }
-  for (int k = tid; k < Lk; k += 256)
+  for (int k = tid; k < LK; k += 256)
     kbias[k] = (k < L && (!mask || mask[(size_t)bi * L + k])) ? 0.f : -INFINITY;
   __syncthreads();
 
@@ -87,48 +89,42 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
     const int qt = wave + 4 * it;
     if (qt >= nqt) break;
     // S^T[key][q]: lane holds keys j*16 + fg*4 + r (r = 0..3) of query q = qt*16 + fr
-    f32x4 s[LMAX / 16];
+    f32x4 s[NKT];
 #pragma unroll
-    for (int j = 0; j < LMAX / 16; ++j) {
+    for (int j = 0; j < NKT; ++j) {
       s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (j < nkt) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int key = j * 16 + fr, kc = ks * 4 + fg;
-          const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
-          s[j] = mfma16x16x32(kf, qf[ks], s[j]);
-        }
+      for (int ks = 0; ks < 2; ++ks) {
+        const int key = j * 16 + fr, kc = ks * 4 + fg;
+        const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
+        s[j] = mfma16x16x32(kf, qf[ks], s[j]);
       }
     }
     // masked softmax over keys (fp32), scale 1/sqrt(64)
     const int qq = qt * 16 + fr;
     float mx = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < LMAX / 16; ++j) {
-      if (j < nkt) {
-        const float4 kb = *reinterpret_cast<const float4*>(kbias + j * 16 + fg * 4);
-        const float kbr[4] = {kb.x, kb.y, kb.z, kb.w};
+    for (int j = 0; j < NKT; ++j) {
+      const float4 kb = *reinterpret_cast<const float4*>(kbias + j * 16 + fg * 4);
+      const float kbr[4] = {kb.x, kb.y, kb.z, kb.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = s[j][r] * 0.125f + kbr[r];
-          if (causal && j * 16 + fg * 4 + r > qq) v = -INFINITY;
-          s[j][r] = v;
-          mx = fmaxf(mx, v);
-        }
+      for (int r = 0; r < 4; ++r) {
+        float v = s[j][r] * 0.125f + kbr[r];
+        if (causal && j * 16 + fg * 4 + r > qq) v = -INFINITY;
+        s[j][r] = v;
+        mx = fmaxf(mx, v);
       }
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < LMAX / 16; ++j) {
-      if (j < nkt) {
+    for (int j = 0; j < NKT; ++j) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = (mx == -INFINITY) ? 0.f : __expf(s[j][r] - mx);
-          s[j][r] = e;
-          sum += e;
-        }
+      for (int r = 0; r < 4; ++r) {
+        const float e = (mx == -INFINITY) ? 0.f : __expf(s[j][r] - mx);
+        s[j][r] = e;
+        sum += e;
       }
     }
     sum += __shfl_xor(sum, 16, 64);
@@ -140,8 +136,8 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kb = 0; kb < LMAX / 32; ++kb) {
-      if (kb * 32 < Lk) {
+    for (int kb = 0; kb < LK / 32; ++kb) {
+      {
         const uint4 pk = make_uint4(pack2bf(s[2 * kb][0] * inv, s[2 * kb][1] * inv),
                                     pack2bf(s[2 * kb][2] * inv, s[2 * kb][3] * inv),
                                     pack2bf(s[2 * kb + 1][0] * inv, s[2 * kb + 1][1] * inv),
@@ -332,6 +328,11 @@ hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, b
                        causal);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(attention_kernel, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal);
+  switch ((L + 31) >> 5) {
+    case 1: hipLaunchKernelGGL(attention_kernel<32>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal); break;
+    case 2: hipLaunchKernelGGL(attention_kernel<64>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal); break;
+    case 3: hipLaunchKernelGGL(attention_kernel<96>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal); break;
+    default: hipLaunchKernelGGL(attention_kernel<128>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal);
+  }
   return hipGetLastError();
 }
