@@ -222,24 +222,35 @@ __global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids
   store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
 }
 
-// CLIP patch embedding operand: A[b*49 + p][c*1024 + ky*32 + kx] = (img/255 - mean_c)/std_c
+// CLIP patch embedding operand: A[b*49 + p][c*1024 + ky*32 + kx] = (img/255 - mean_c)/std_c.
+// One thread per (patch row, ky, 8-pixel group): the 24 interleaved RGB bytes arrive as three
+// 8-B loads (was 8 single-byte loads per channel) and leave as one 16-B store per channel.
 __global__ __launch_bounds__(256) void clip_im2col_kernel(const uint8_t* img, bf16_t* A, int B) {
   const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const size_t total = (size_t)B * 49 * 384;
+  const size_t total = (size_t)B * 49 * 128;
   if (gid >= total) return;
-  const int g = gid % 384;
-  const size_t rowp = gid / 384;
+  const int g = gid % 128;
+  const size_t rowp = gid / 128;
   const int p = rowp % 49, bi = rowp / 49;
-  const int c = g >> 7, ky = (g & 127) >> 2, kx0 = (g & 3) * 8;
+  const int ky = g >> 2, kx0 = (g & 3) * 8;
   const int y = (p / 7) * 32 + ky, x0 = (p % 7) * 32 + kx0;
-  const float mean = c == 0 ? 0.48145466f : (c == 1 ? 0.4578275f : 0.40821073f);
-  const float istd = 1.0f / (c == 0 ? 0.26862954f : (c == 1 ? 0.26130258f : 0.27577711f));
-  const uint8_t* src = img + (((size_t)bi * 224 + y) * 224 + x0) * 3 + c;
-  float v[8];
+  const uint2* src = reinterpret_cast<const uint2*>(img + (((size_t)bi * 224 + y) * 224 + x0) * 3);  // 8-B aligned
+  const uint2 w0 = src[0], w1 = src[1], w2 = src[2];
+  const uint32_t wd[6] = {w0.x, w0.y, w1.x, w1.y, w2.x, w2.y};
+  constexpr float kMean[3] = {0.48145466f, 0.4578275f, 0.40821073f};
+  constexpr float kStd[3] = {0.26862954f, 0.26130258f, 0.27577711f};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = ((float)src[j * 3] * (1.0f / 255.0f) - mean) * istd;
-  *reinterpret_cast<uint4*>(A + rowp * 3072 + g * 8) =
-      make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  for (int c = 0; c < 3; ++c) {
+    const float mean = kMean[c], istd = 1.0f / kStd[c];
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int byte = j * 3 + c;
+      v[j] = ((float)((wd[byte >> 2] >> ((byte & 3) * 8)) & 0xffu) * (1.0f / 255.0f) - mean) * istd;
+    }
+    *reinterpret_cast<uint4*>(A + rowp * 3072 + c * 1024 + ky * 32 + kx0) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  }
 }
 
 // CLIP vision: e = (t==0 ? class_emb : patch[b*49+t-1]) + pos[t]; x = pre_LN(e); xb = LN1(x)
@@ -369,7 +380,8 @@ hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const fl
 }
 
 hipError_t launch_clip_im2col(const uint8_t* img, bf16_t* A, int B, hipStream_t s) {
-  const size_t total = (size_t)B * 49 * 384;
+  if (reinterpret_cast<uintptr_t>(img) & 7) return hipErrorInvalidValue;  // 8-B pixel-row loads
+  const size_t total = (size_t)B * 49 * 128;
   hipLaunchKernelGGL(clip_im2col_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, img, A, B);
   return hipGetLastError();
 }
