@@ -328,11 +328,14 @@ hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, b
                        causal);
     return hipGetLastError();
   }
-  switch ((L + 31) >> 5) {
-    case 1: hipLaunchKernelGGL(attention_kernel<32>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal); break;
-    case 2: hipLaunchKernelGGL(attention_kernel<64>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal); break;
-    case 3: hipLaunchKernelGGL(attention_kernel<96>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal); break;
-    default: hipLaunchKernelGGL(attention_kernel<128>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal);
+#define MMF_ATTN(LK) \
+  hipLaunchKernelGGL(attention_kernel<LK>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal)
+  switch ((L + 31) >> 5) {  // keys padded to 32
+    case 1: MMF_ATTN(32); break;
+    case 2: MMF_ATTN(64); break;
+    case 3: MMF_ATTN(96); break;
+    default: MMF_ATTN(128);
   }
+#undef MMF_ATTN
   return hipGetLastError();
 }
