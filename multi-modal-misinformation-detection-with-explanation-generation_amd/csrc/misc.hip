@@ -7,8 +7,10 @@
 namespace {
 
 // misinfo_forensics.py:57-69, 97-98, 342-347: two Linear(768,256)-ReLU-Linear(256,2) heads on the
-// CLS row, softmax[:, 1].  Block = 4 rows; W1 stored transposed [768][256] so a k-step of the 256
-// hidden units reads one coalesced 1-KB row.
+// CLS row, softmax[:, 1].  Block = 4 rows x ONE head (blockIdx.y: 0 = ai, 1 = misinfo), so a block
+// streams 0.75 MB of W1 instead of 1.5 MB (the per-block L2 stream is what bounds this kernel at
+// the end of the RoBERTa tower); W1 stored transposed [768][256] so a k-step of the 256 hidden
+// units reads one coalesced 1-KB row.  Per head the arithmetic order is unchanged.
 __global__ __launch_bounds__(1024) void text_heads_kernel(const float* x, int row_stride, const float* w1a,
                                                          const float* b1a, const float* w2a, const float* b2a,
                                                          const float* w1m, const float* b1m, const float* w2m,
@@ -18,17 +20,21 @@ __global__ __launch_bounds__(1024) void text_heads_kernel(const float* x, int ro
   // thread's dependent load/FMA chain is a quarter of the 768; slices combined in fixed order.
   constexpr int KS = 4, KL = 768 / KS;
   __shared__ float xs[4][768];
-  __shared__ float hp[KS][2][4][256];  // [slice][head][row][hidden] partial sums
-  __shared__ float red[4][4][4];       // [wave][row][head*2+o]
-  const int tid = threadIdx.x, r0 = blockIdx.x * 4, h = tid & 255, ks = tid >> 8;
+  __shared__ float hp[KS][4][256];  // [slice][row][hidden] partial sums
+  __shared__ float red[4][4][2];    // [wave][row][o]
+  const int tid = threadIdx.x, r0 = blockIdx.x * 4, h = tid & 255, ks = tid >> 8, head = blockIdx.y;
+  const float* w1h = head ? w1m : w1a;
+  const float* b1 = head ? b1m : b1a;
+  const float* w2 = head ? w2m : w2a;
+  const float* b2 = head ? b2m : b2a;
+  float* logits = head ? mi_logits : ai_logits;
   for (int i = tid; i < 4 * 768; i += 1024) {
     const int r = i / 768, c = i % 768;
     xs[r][c] = (r0 + r < B) ? x[(size_t)(r0 + r) * row_stride + c] : 0.f;
   }
   __syncthreads();
-#pragma unroll
-  for (int head = 0; head < 2; ++head) {
-    const float* w1 = (head ? w1m : w1a) + (size_t)ks * KL * 256 + h;
+  {
+    const float* w1 = w1h + (size_t)ks * KL * 256 + h;
     float hsum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
     for (int k = 0; k < KL; ++k) {
@@ -37,31 +43,26 @@ __global__ __launch_bounds__(1024) void text_heads_kernel(const float* x, int ro
       for (int r = 0; r < 4; ++r) hsum[r] = fmaf(w, xs[r][ks * KL + k], hsum[r]);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) hp[ks][head][r][h] = hsum[r];
+    for (int r = 0; r < 4; ++r) hp[ks][r][h] = hsum[r];
   }
   __syncthreads();
-  if (tid < 256) {  // waves 0-3: hidden units -> ReLU -> the 2 x 2 output logits per row
-    float part[4][4];
+  if (tid < 256) {  // waves 0-3: hidden units -> ReLU -> the 2 output logits per row
+    float part[4][2];
+    const float w20 = w2[h], w21 = w2[256 + h], bb = b1[h];
 #pragma unroll
-    for (int head = 0; head < 2; ++head) {
-      const float* b1 = head ? b1m : b1a;
-      const float* w2 = head ? w2m : w2a;
-      const float w20 = w2[h], w21 = w2[256 + h], bb = b1[h];
+    for (int r = 0; r < 4; ++r) {
+      float hs = hp[0][r][h];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float hs = hp[0][head][r][h];
-#pragma unroll
-        for (int q = 1; q < KS; ++q) hs += hp[q][head][r][h];
-        const float hv = fmaxf(hs + bb, 0.f);
-        part[r][head * 2 + 0] = hv * w20;
-        part[r][head * 2 + 1] = hv * w21;
-      }
+      for (int q = 1; q < KS; ++q) hs += hp[q][r][h];
+      const float hv = fmaxf(hs + bb, 0.f);
+      part[r][0] = hv * w20;
+      part[r][1] = hv * w21;
     }
     const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int o = 0; o < 4; ++o) {
+      for (int o = 0; o < 2; ++o) {
         const float v = wave_sum(part[r][o]);
         if (lane == 0) red[wave][r][o] = v;
       }
@@ -69,18 +70,15 @@ __global__ __launch_bounds__(1024) void text_heads_kernel(const float* x, int ro
   __syncthreads();
   if (tid < 4 && r0 + tid < B) {
     const int r = tid, row = r0 + r;
-    float l[4];
+    float l[2];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) l[o] = red[0][r][o] + red[1][r][o] + red[2][r][o] + red[3][r][o];
-    l[0] += b2a[0]; l[1] += b2a[1]; l[2] += b2m[0]; l[3] += b2m[1];
-    if (ai_logits) { ai_logits[row * 2] = l[0]; ai_logits[row * 2 + 1] = l[1]; }
-    if (mi_logits) { mi_logits[row * 2] = l[2]; mi_logits[row * 2 + 1] = l[3]; }
-    if (scores) {
-      // softmax(l)[1] = exp(l1 - m) / (exp(l0 - m) + exp(l1 - m))
-      const float ma = fmaxf(l[0], l[1]), mm = fmaxf(l[2], l[3]);
-      const float ea0 = expf(l[0] - ma), ea1 = expf(l[1] - ma), em0 = expf(l[2] - mm), em1 = expf(l[3] - mm);
-      scores[(size_t)row * score_stride] = ea1 / (ea0 + ea1);
-      scores[(size_t)row * score_stride + 1] = em1 / (em0 + em1);
+    for (int o = 0; o < 2; ++o) l[o] = red[0][r][o] + red[1][r][o] + red[2][r][o] + red[3][r][o];
+    l[0] += b2[0]; l[1] += b2[1];
+    if (logits) { logits[row * 2] = l[0]; logits[row * 2 + 1] = l[1]; }
+    if (scores) {  // softmax(l)[1] = exp(l1 - m) / (exp(l0 - m) + exp(l1 - m))
+      const float m = fmaxf(l[0], l[1]);
+      const float e0 = expf(l[0] - m), e1 = expf(l[1] - m);
+      scores[(size_t)row * score_stride + head] = e1 / (e0 + e1);
     }
   }
 }
@@ -284,7 +282,7 @@ hipError_t launch_text_heads(const float* x, int row_stride, const float* w1a, c
                              const float* b2a, const float* w1m, const float* b1m, const float* w2m,
                              const float* b2m, float* ai_logits, float* mi_logits, float* scores, int score_stride,
                              int B, hipStream_t s) {
-  hipLaunchKernelGGL(text_heads_kernel, dim3((B + 3) / 4), dim3(1024), 0, s, x, row_stride, w1a, b1a, w2a, b2a, w1m,
+  hipLaunchKernelGGL(text_heads_kernel, dim3((B + 3) / 4, 2), dim3(1024), 0, s, x, row_stride, w1a, b1a, w2a, b2a, w1m,
                      b1m, w2m, b2m, ai_logits, mi_logits, scores, score_stride, B);
   return hipGetLastError();
 }
