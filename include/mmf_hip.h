@@ -93,15 +93,29 @@ int mmf_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb_unit, vo
 int mmf_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* emb_unit,
                   void* stream);
 
+/* analyze_consistency (misinfo_forensics.py:375-408) / CLIPSimilarityEngine.calculate_similarity
+ * (clip_similarity_engine.py:63-119): both CLIP towers (text tower on a concurrent stream) and the
+ * cosine of the unit embeddings.  img uint8 [B,224,224,3], ids/mask int32 [B, L<=77]; sim fp32 [B];
+ * img_emb / txt_emb fp32 [B, 512] unit (may be NULL: handle workspaces are used). */
+int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, const int32_t* mask, int B, int L,
+                         float* img_emb, float* txt_emb, float* sim, void* stream);
+
 /* Truth-Vault (misinfo_forensics.py:214-246, 443-445): host fp32 [N, D=512] raw embeddings; rows
  * are L2-normalised once here instead of on every search call. */
 int mmf_set_vault(mmf_handle* h, const float* host_vault, int N, int D);
+/* The same with rows already L2-normalised by the caller: the Python host side normalises exactly
+ * as the reference line does, in the vault's own dtype (numpy, misinfo_forensics.py:443-445 --
+ * float16 vaults renormalise in float16; a zero row becomes NaN), and uploads the float32 result.
+ * Replaces the previous vault and its title embeddings (their device memory is freed). */
+int mmf_set_vault_normalized(mmf_handle* h, const float* host_vault_unit, int N, int D);
 /* Pre-compute the CLIP text embeddings of the vault titles (used for text_similarity,
  * misinfo_forensics.py:467-484) from device ids/mask int32 [N, L<=77].  Synchronous. */
 int mmf_set_vault_titles(mmf_handle* h, const int32_t* ids, const int32_t* mask, int N, int L, void* stream);
 
 /* search_vault core (misinfo_forensics.py:443-464, 467-484): q fp32 [B, 512] unit image
- * embeddings; top-k (k <= 8) similarities fp32 [B, k] and indices int32 [B, k] (descending);
+ * embeddings; top-k (1 <= k <= N; k > 8 needs N <= 16384) similarities fp32 [B, k] and indices
+ * int32 [B, k] in np.argsort(sims)[-k:][::-1] order (descending; NaN rows first, exact ties by
+ * descending index);
  * discrepancy fp32 [B] = top1 > thresh ? top1 : 0; optional text_emb fp32 [B, 512] unit caption
  * embeddings -> text_sim fp32 [B] = cos(caption, title[top1]) where top1 > thresh, else 0. */
 int mmf_vault_topk(mmf_handle* h, const float* q_unit, int B, int k, float thresh, float* sims, int32_t* idx,
@@ -133,6 +147,15 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
 int mmf_profile_begin(mmf_handle* h);
 int mmf_profile_end(mmf_handle* h, int max_kinds, int* counts, double* ms, double* flops, double* bytes);
 const char* mmf_profile_kind_name(int kind);
+
+/* Run-time options (A/B switches; defaults read once per process from MMF_* environment variables):
+ * "concurrent" (tower streams), "fuse_stem", "fuse_expand", "dw_ct", "gemm_splitk", "gemm_config",
+ * "gemm_group_m".  h = NULL reads/changes the process defaults used by the handle-less ops below
+ * and by handles created afterwards. */
+int mmf_set_option(mmf_handle* h, const char* name, int value);
+int mmf_get_option(mmf_handle* h, const char* name, int* value);
+/* Device bytes currently owned by the handle (weights, workspaces, vault). */
+int64_t mmf_device_bytes(mmf_handle* h);
 
 /* Low-level op exported for unit tests of the GEMM kernel: C = act(A @ W^T + bias) + residual.
  * A bf16 [M,K] (lda), W bf16 [N,K] (ldw), bias fp32 [N] or NULL, residual fp32 [M,N] (ldc) or NULL,

@@ -1,0 +1,75 @@
+"""Rank plumbing of the benchmark (bench.py), factored out so that the multi-process path runs in
+the CPU test suite exactly as it runs on an 8-GPU node (tests/test_bench_multirank_cpu.py drives
+these functions over a gloo world of 2 with a CPU stand-in engine).
+
+One process per GPU (torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE and
+MASTER_*); the batch is sharded by rank with no collective on the data path:
+every rank times its own steps, the barrier brackets the timed region, and the whole-job time is
+the MAX over ranks (one all_reduce of one float) -- the only collective traffic.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Callable, Optional
+
+import torch
+
+INPUT_SEED = 1234  # inputs seeded 1234 + rank
+
+
+def rank_env() -> tuple:
+    """(world, rank, local_rank) from the launcher's environment (1, 0, 0 when run directly)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def input_seed(rank: int) -> int:
+    """Each rank draws its own shard of the synthetic workload."""
+    return INPUT_SEED + rank
+
+
+def init_dist(world: int, backend: str, device: Optional[torch.device] = None):
+    """torch.distributed with `backend` ("nccl" = RCCL over xGMI on the GPU node, "gloo" in the CPU
+    tests) when world > 1, else None."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    if backend == "nccl":
+        dist.init_process_group(backend, device_id=device)
+    else:
+        dist.init_process_group(backend)
+    return dist
+
+
+def timed_steps(step: Callable[[], None], steps: int, warmup: int, dist=None,
+                sync: Callable[[], None] = lambda: None, device: Optional[torch.device] = None) -> float:
+    """`warmup` untimed steps, then exactly `steps` timed steps bracketed by a barrier and a device
+    synchronisation on both sides; returns the MAX over ranks of the timed wall time (seconds)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    return max_over_ranks(dt, dist, device)
+
+
+def max_over_ranks(x: float, dist=None, device: Optional[torch.device] = None) -> float:
+    if not dist:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def whole_job_rate(world: int, units_per_rank_step: int, steps: int, seconds: float) -> float:
+    """Units all ranks processed / whole-job time (weak scaling: per-rank work fixed)."""
+    return world * units_per_rank_step * steps / seconds

@@ -93,13 +93,57 @@ struct Workspace {
   int s_cap_n = 0;
 };
 
+// Run-time options.  Defaults come from the environment ONCE per process (MMF_* variables, for the
+// A/B tools), are copied into every handle at mmf_create and changed with mmf_set_option; no kernel
+// launch reads the environment.
+struct Options {
+  int concurrent = 1;   // towers of mmf_analyze_batch on concurrent streams
+  int fuse_stem = 1;    // stem fused into the stage-1 depthwise conv
+  int fuse_expand = 1;  // 1x1 expand fused into the depthwise conv (stages 2-4)
+  int dw_ct = 1;        // compile-time depthwise tile geometries
+  int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
+  int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
+  int gemm_group_m = 0; // persistent GEMM tile order
+};
+struct OptName { const char* name; int Options::*field; const char* env; };
+const OptName kOptNames[] = {
+    {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
+    {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"}, {"dw_ct", &Options::dw_ct, "MMF_DW_CT"},
+    {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
+    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"},
+};
+Options& process_options() {
+  static Options o = [] {
+    Options d;
+    for (const OptName& n : kOptNames) {
+      const char* e = getenv(n.env);
+      if (e && *e) d.*(n.field) = atoi(e);
+    }
+    return d;
+  }();
+  return o;
+}
+
+void apply_options(const Options& o, GemmArgs* g) {
+  g->force_cfg = o.gemm_config >= 0 ? o.gemm_config + 1 : 0;
+  g->no_splitk = o.gemm_splitk ? 0 : 1;
+  g->group_m = o.gemm_group_m;
+}
+
+// Device allocations are owned per group so that re-loading one component (or the vault, or the
+// workspaces) frees exactly what it replaces.
+enum AllocGroup { AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_COUNT };
+
 }  // namespace
 
 struct mmf_handle {
   int device = 0;
   int eos_id = 49407;
   std::map<std::string, HostT> staged;
-  std::vector<void*> allocs;
+  std::vector<void*> groups[AG_COUNT];
+  size_t group_bytes[AG_COUNT] = {};
+  int cur_group = AG_TEXT;  // group of the weight uploads of the component being finalized
+  Options opt;
   int ready = 0;
   // RoBERTa + heads
   float *r_word = nullptr, *r_pos = nullptr, *r_type0 = nullptr;
@@ -132,7 +176,6 @@ struct mmf_handle {
   // workspace capacity
   Workspace ws;
   int cap_b = 0, cap_lr = 0, cap_lc = 0;
-  std::vector<void*> ws_allocs;
   // per-kernel event timing (mmf_profile_begin/end)
   struct ProfRec { int ev; int kind; double flops, bytes; };
   bool prof = false;
@@ -142,11 +185,10 @@ struct mmf_handle {
   // fork/join streams of mmf_analyze_batch (text, effnet, clip-text towers beside the caller's)
   hipStream_t tower[3] = {nullptr, nullptr, nullptr};
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
-  int concurrent = 1;
 
   ~mmf_handle() {
-    for (void* p : allocs) (void)hipFree(p);
-    for (void* p : ws_allocs) (void)hipFree(p);
+    for (auto& g : groups)
+      for (void* p : g) (void)hipFree(p);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < 3; ++i) {
       if (tower[i]) (void)hipStreamDestroy(tower[i]);
@@ -158,11 +200,22 @@ struct mmf_handle {
 
 namespace {
 
-int dev_alloc(mmf_handle* h, void** p, size_t bytes, bool workspace = false) {
+int dev_alloc(mmf_handle* h, void** p, size_t bytes, int group) {
   if (bytes == 0) bytes = 16;
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) return fail(MMF_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-  (workspace ? h->ws_allocs : h->allocs).push_back(*p);
+  h->groups[group].push_back(*p);
+  h->group_bytes[group] += bytes;
+  return 0;
+}
+
+// Free one group's buffers after the device has drained (any queued launch may still read them).
+int free_group(mmf_handle* h, int group) {
+  if (h->groups[group].empty()) return 0;
+  HIPCHK(hipDeviceSynchronize());
+  for (void* p : h->groups[group]) HIPCHK(hipFree(p));
+  h->groups[group].clear();
+  h->group_bytes[group] = 0;
   return 0;
 }
 
@@ -210,7 +263,7 @@ struct ProfScope {
 template <typename T>
 int upload(mmf_handle* h, T** dst, const std::vector<T>& v) {
   void* p;
-  CHK(dev_alloc(h, &p, v.size() * sizeof(T)));
+  CHK(dev_alloc(h, &p, v.size() * sizeof(T), h->cur_group));
   HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   *dst = (T*)p;
   return 0;
@@ -461,7 +514,8 @@ GemmArgs with_ws(GemmArgs g, float* ws, size_t elems) {
   return g;
 }
 
-int gemm(mmf_handle* h, const GemmArgs& g, hipStream_t s) {
+int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
+  apply_options(h->opt, &g);
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
   ProfScope ps(h, s, gemm_config(g) * kGemmActs + g.act, 2.0 * M * N * K, 2.0 * (M * K + N * K) + M * N * out_b);
@@ -679,10 +733,9 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
   Workspace& w = h->ws;
   bf16_t* cur = w.e_a;
   bf16_t* nxt = w.e_b;
-  // MMF_FUSE_STEM=0: separate stem launch + stage-1 depthwise (A/B and parity tests)
+  // option fuse_stem = 0: separate stem launch + stage-1 depthwise (A/B and parity tests)
   const EffBlock& b0 = h->e_blocks.front();
-  const char* fs = getenv("MMF_FUSE_STEM");
-  const bool fuse_stem = !(fs && *fs == '0') && b0.expand == 1 && b0.cexp == 32 && b0.k == 3 && b0.stride == 1;
+  const bool fuse_stem = h->opt.fuse_stem && b0.expand == 1 && b0.cexp == 32 && b0.k == 3 && b0.stride == 1;
   if (!fuse_stem) {
     ProfScope ps(h, s, PK_STEM, 2.0 * B * 112 * 112 * 32 * 27, (double)B * (224 * 224 * 3 + 112 * 112 * 32 * 2));
     if (xf32) HIPCHK(launch_effnet_stem_f32(xf32, h->e_stem_w, h->e_stem_b, cur, B, s));
@@ -693,8 +746,8 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
     const bf16_t* src = cur;
     int nch = 0;
     const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
-    const char* fe = getenv("MMF_FUSE_EXPAND");  // MMF_FUSE_EXPAND=0: separate expand launch (A/B)
-    const bool fuse = b.expand != 1 && expand_dw_applicable(b.cin, b.cexp) && !(fe && *fe == '0');
+    // option fuse_expand = 0: separate expand launch (A/B)
+    const bool fuse = b.expand != 1 && expand_dw_applicable(b.cin, b.cexp) && h->opt.fuse_expand;
     if (&b == &b0 && fuse_stem) {
       // stem output recomputed per 18x18 halo tile: 1.27x the stem MACs, image patch read once
       ProfScope ps(h, s, PK_DW, 2.0 * B * 112 * 112 * 32 * (9 + 27 * 1.27),
@@ -704,7 +757,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k + 2.0 * B * H * W * b.cin * b.cexp,
                    (double)B * 2 * ((double)H * W * b.cin * (b.cexp / 48) + (double)Ho * Wo * b.cexp));
       HIPCHK(launch_expand_dw(cur, b.cin, b.e.w, b.e.b, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride,
-                              &nch, s));
+                              &nch, s, h->opt.dw_ct));
     } else if (b.expand != 1) {
       GemmArgs g = gemm_args(cur, b.cin, b.e, B * H * W);
       g.act = 3;  // SiLU
@@ -715,7 +768,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
     if (!fuse && !(&b == &b0 && fuse_stem)) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k,
                    (double)B * b.cexp * 2 * ((double)H * W + (double)Ho * Wo));
-      HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s));
+      HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s, h->opt.dw_ct));
     }
     ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, (double)B * b.cexp * 4 * (nch + 1));
     HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s));
@@ -740,11 +793,23 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
   return 0;
 }
 
+// fork/join streams of the multi-tower entry points, created on first use
+int ensure_towers(mmf_handle* h) {
+  if (h->tower[0]) return 0;
+  for (int i = 0; i < 3; ++i) {
+    HIPCHK(hipStreamCreateWithFlags(&h->tower[i], hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
+  }
+  HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+  return 0;
+}
+
 int ensure_sims(mmf_handle* h) {
   if (!h->vault_n || !h->cap_b) return 0;
   if (h->ws.s_cap_n >= h->vault_n) return 0;
+  CHK(free_group(h, AG_SIMS));
   void* p;
-  CHK(dev_alloc(h, &p, (size_t)h->cap_b * h->vault_n * sizeof(float), true));
+  CHK(dev_alloc(h, &p, (size_t)h->cap_b * h->vault_n * sizeof(float), AG_SIMS));
   h->ws.s_sims = (float*)p;
   h->ws.s_cap_n = h->vault_n;
   return 0;
@@ -767,8 +832,7 @@ int mmf_create(int device, mmf_handle** out) {
   mmf_handle* h = new (std::nothrow) mmf_handle();
   if (!h) return fail(MMF_ENOMEM, "out of host memory");
   h->device = device;
-  const char* conc = getenv("MMF_CONCURRENT");  // MMF_CONCURRENT=0: run the towers on one stream
-  h->concurrent = !(conc && conc[0] == '0');
+  h->opt = process_options();
   *out = h;
   g_err.clear();
   return 0;
@@ -804,18 +868,23 @@ int mmf_finalize(mmf_handle* h, int clip_eos_token_id) {
   h->eos_id = clip_eos_token_id;
   int ready = h->ready;  // incremental: components not re-staged keep their packed weights
   std::string missing;
-  auto attempt = [&](int bit, const char* probe, int (*fn)(mmf_handle*)) -> int {
-    if (!has(h, probe)) return 0;
+  // a re-staged component replaces its packed weights: its previous buffers are freed first
+  auto attempt = [&](int bit, int group, const char* key, int (*fn)(mmf_handle*)) -> int {
+    if (!has(h, key)) return 0;
+    ready &= ~bit;
+    h->ready = ready;
+    CHK(free_group(h, group));
+    h->cur_group = group;
     int r = fn(h);
     if (r) return r;
     ready |= bit;
     return 0;
   };
-  CHK(attempt(1, "roberta.embeddings.word_embeddings.weight", finalize_text));
-  CHK(attempt(2, "efficientnet.features.0.0.weight", finalize_effnet));
-  CHK(attempt(4, "clip.vision_model.embeddings.patch_embedding.weight", finalize_clip_vision));
-  CHK(attempt(8, "clip.text_model.embeddings.token_embedding.weight", finalize_clip_text));
-  CHK(attempt(16, "fusion_layer.0.weight", finalize_fusion));
+  CHK(attempt(1, AG_TEXT, "roberta.embeddings.word_embeddings.weight", finalize_text));
+  CHK(attempt(2, AG_EFF, "efficientnet.features.0.0.weight", finalize_effnet));
+  CHK(attempt(4, AG_VIS, "clip.vision_model.embeddings.patch_embedding.weight", finalize_clip_vision));
+  CHK(attempt(8, AG_CTEXT, "clip.text_model.embeddings.token_embedding.weight", finalize_clip_text));
+  CHK(attempt(16, AG_FUSION, "fusion_layer.0.weight", finalize_fusion));
   h->ready = ready;
   h->staged.clear();
   HIPCHK(hipDeviceSynchronize());
@@ -828,13 +897,12 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   if (!h || B <= 0 || Lr <= 0 || Lr > 512 || Lc <= 0 || Lc > 77)
     return fail(MMF_EINVAL, "mmf_reserve: bad shape B=%d Lr=%d Lc=%d", B, Lr, Lc);
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipDeviceSynchronize());
-  for (void* p : h->ws_allocs) (void)hipFree(p);
-  h->ws_allocs.clear();
+  CHK(free_group(h, AG_WS));
+  CHK(free_group(h, AG_SIMS));
   h->ws = Workspace();
   h->cap_b = h->cap_lr = h->cap_lc = 0;
   Workspace& w = h->ws;
-  auto A = [&](void** p, size_t bytes) { return dev_alloc(h, p, bytes, true); };
+  auto A = [&](void** p, size_t bytes) { return dev_alloc(h, p, bytes, AG_WS); };
   const size_t Mr = (size_t)B * Lr, Mv = (size_t)B * 50, Mt = (size_t)B * Lc;
   CHK(A((void**)&w.r_x, Mr * 768 * 4));
   CHK(A((void**)&w.r_y, Mr * 768 * 4));
@@ -941,6 +1009,49 @@ int mmf_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
   return run_clip_text(h, ids, mask, B, L, emb, (hipStream_t)stream);
 }
 
+namespace {
+int set_vault_rows(mmf_handle* h, std::vector<float>& u, int N) {
+  h->ready &= ~32;
+  CHK(free_group(h, AG_TITLES));  // titles belong to the previous vault
+  h->vault_title = nullptr;
+  CHK(free_group(h, AG_VAULT));
+  h->cur_group = AG_VAULT;
+  CHK(up_f32(h, &h->vault, u));
+  h->vault_n = N;
+  h->ready |= 32;
+  h->ws.s_cap_n = 0;
+  return ensure_sims(h);
+}
+}  // namespace
+
+int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, const int32_t* mask, int B, int L,
+                         float* img_emb, float* txt_emb, float* sim, void* stream) {
+  if (!h || !img || !ids || !mask || !sim) return fail(MMF_EINVAL, "null argument");
+  if ((h->ready & 12) != 12) return fail(MMF_EINVAL, "CLIP towers not loaded");
+  if (L > 77) return fail(MMF_EINVAL, "CLIP text length %d > 77", L);
+  CHK(check_cap(h, B, 1, L));
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  float* ie = img_emb ? img_emb : h->ws.v_emb;
+  float* te = txt_emb ? txt_emb : h->ws.t_emb;
+  CHK(ensure_towers(h));
+  const int concurrent = h->opt.concurrent && !h->prof;
+  hipStream_t st = s;
+  if (concurrent) {  // the text tower beside the vision tower (disjoint workspaces)
+    HIPCHK(hipEventRecord(h->fork_ev, s));
+    HIPCHK(hipStreamWaitEvent(h->tower[2], h->fork_ev, 0));
+    st = h->tower[2];
+  }
+  CHK(run_clip_text(h, ids, mask, B, L, te, st));
+  CHK(run_clip_image(h, img, B, ie, s));
+  if (concurrent) {
+    HIPCHK(hipEventRecord(h->join_ev[2], h->tower[2]));
+    HIPCHK(hipStreamWaitEvent(s, h->join_ev[2], 0));
+  }
+  HIPCHK(launch_rowdot(ie, te, sim, 1, B, 512, s));
+  return 0;
+}
+
 int mmf_set_vault(mmf_handle* h, const float* V, int N, int D) {
   if (!h || !V || N <= 0 || D != 512) return fail(MMF_EINVAL, "mmf_set_vault: need N > 0 rows of D = 512");
   HIPCHK(hipSetDevice(h->device));
@@ -948,15 +1059,17 @@ int mmf_set_vault(mmf_handle* h, const float* V, int N, int D) {
   for (int i = 0; i < N; ++i) {
     double s = 0;
     for (int d = 0; d < D; ++d) s += (double)V[(size_t)i * D + d] * V[(size_t)i * D + d];
-    const float nrm = (float)std::sqrt(s);
+    const float nrm = (float)std::sqrt(s);  // a zero row gives 0/0 = NaN, as numpy does
     for (int d = 0; d < D; ++d) u[(size_t)i * D + d] = V[(size_t)i * D + d] / nrm;
   }
-  CHK(up_f32(h, &h->vault, u));
-  h->vault_n = N;
-  h->vault_title = nullptr;
-  h->ready |= 32;
-  h->ws.s_cap_n = 0;
-  return ensure_sims(h);
+  return set_vault_rows(h, u, N);
+}
+
+int mmf_set_vault_normalized(mmf_handle* h, const float* Vhat, int N, int D) {
+  if (!h || !Vhat || N <= 0 || D != 512) return fail(MMF_EINVAL, "mmf_set_vault_normalized: need N > 0 rows of D = 512");
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<float> u(Vhat, Vhat + (size_t)N * D);
+  return set_vault_rows(h, u, N);
 }
 
 int mmf_set_vault_titles(mmf_handle* h, const int32_t* ids, const int32_t* mask, int N, int L, void* stream) {
@@ -965,8 +1078,10 @@ int mmf_set_vault_titles(mmf_handle* h, const int32_t* ids, const int32_t* mask,
   if (!(h->ready & 8)) return fail(MMF_EINVAL, "CLIP text tower not loaded");
   if (L > h->cap_lc || h->cap_b <= 0) return fail(MMF_EINVAL, "reserve CLIP length >= %d first", L);
   HIPCHK(hipSetDevice(h->device));
+  CHK(free_group(h, AG_TITLES));
+  h->vault_title = nullptr;
   float* t;
-  CHK(dev_alloc(h, (void**)&t, (size_t)N * 512 * 4));
+  CHK(dev_alloc(h, (void**)&t, (size_t)N * 512 * 4, AG_TITLES));
   hipStream_t s = (hipStream_t)stream;
   for (int i = 0; i < N; i += h->cap_b) {
     const int n = std::min(h->cap_b, N - i);
@@ -981,7 +1096,8 @@ int mmf_vault_topk(mmf_handle* h, const float* q, int B, int k, float thresh, fl
                    const float* temb, float* tsim, void* stream) {
   if (!h || !q) return fail(MMF_EINVAL, "null argument");
   if (!(h->ready & 32)) return fail(MMF_EINVAL, "vault not loaded");
-  if (k < 1 || k > 8) return fail(MMF_EINVAL, "top_k must be in [1, 8]");
+  if (k < 1 || k > h->vault_n) return fail(MMF_EINVAL, "top_k must be in [1, N=%d]", h->vault_n);
+  if (k > 8 && h->vault_n > 16384) return fail(MMF_EINVAL, "top_k > 8 needs a vault of <= 16384 rows");
   CHK(check_cap(h, B, 1, 1));
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
@@ -1015,14 +1131,8 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   if (!img_clip) img_clip = img_eff;
   Workspace& w = h->ws;
   // the per-kernel profiling pass runs the towers sequentially so event intervals are clean
-  const int concurrent = h->concurrent && !h->prof;
-  if (concurrent && !h->tower[0]) {
-    for (int i = 0; i < 3; ++i) {
-      HIPCHK(hipStreamCreateWithFlags(&h->tower[i], hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
-    }
-    HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-  }
+  const int concurrent = h->opt.concurrent && !h->prof;
+  if (concurrent) CHK(ensure_towers(h));
   // fork: the four towers only share read-only inputs and write disjoint workspaces/outputs
   hipStream_t st_text = s, st_eff = s, st_ctxt = s;
   if (concurrent) {
@@ -1092,6 +1202,35 @@ int mmf_profile_end(mmf_handle* h, int max_kinds, int* counts, double* ms, doubl
 
 const char* mmf_profile_kind_name(int kind) { return prof_kind_name(kind); }
 
+int mmf_set_option(mmf_handle* h, const char* name, int value) {
+  if (!name) return fail(MMF_EINVAL, "null option name");
+  Options& o = h ? h->opt : process_options();
+  for (const OptName& n : kOptNames)
+    if (!strcmp(n.name, name)) {
+      o.*(n.field) = value;
+      return 0;
+    }
+  return fail(MMF_EINVAL, "unknown option '%s'", name);
+}
+
+int mmf_get_option(mmf_handle* h, const char* name, int* value) {
+  if (!name || !value) return fail(MMF_EINVAL, "null argument");
+  const Options& o = h ? h->opt : process_options();
+  for (const OptName& n : kOptNames)
+    if (!strcmp(n.name, name)) {
+      *value = o.*(n.field);
+      return 0;
+    }
+  return fail(MMF_EINVAL, "unknown option '%s'", name);
+}
+
+int64_t mmf_device_bytes(mmf_handle* h) {
+  if (!h) return 0;
+  int64_t t = 0;
+  for (size_t b : h->group_bytes) t += (int64_t)b;
+  return t;
+}
+
 int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual, float* c32,
                   void* c16, int ldc, int M, int N, int K, int act, void* stream) {
   GemmArgs g{};
@@ -1109,6 +1248,7 @@ int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* b
   g.N = N;
   g.K = K;
   g.act = act;
+  apply_options(process_options(), &g);
   if (!A || !W || (!c32 && !c16)) return fail(MMF_EINVAL, "null argument");
   hipError_t e = launch_gemm(g, (hipStream_t)stream);
   if (e != hipSuccess) return fail(MMF_EIO, "gemm: %s", hipGetErrorString(e));
@@ -1134,6 +1274,7 @@ int mmf_gemm_bf16_ex(const void* A, int lda, const void* W, int ldw, const float
   g.N = N;
   g.K = K;
   g.act = act;
+  apply_options(process_options(), &g);
   if (!A || !W || !c16) return fail(MMF_EINVAL, "null argument");
   if (ascale && rows_per_batch <= 0) return fail(MMF_EINVAL, "rows_per_batch must be > 0 with ascale");
   hipError_t e = launch_gemm(g, (hipStream_t)stream);

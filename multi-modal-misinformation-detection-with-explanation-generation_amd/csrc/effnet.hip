@@ -711,7 +711,7 @@ int dwconv_nchunks(int H, int W, int C, int stride) {
 }
 
 hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part, int B,
-                         int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s) {
+                         int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct) {
   int T, CW, tiles_x, ntiles;
   dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
   if (C % CW) return hipErrorInvalidValue;
@@ -727,8 +727,7 @@ hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf
                        C, CW, T, tiles_x);                                                                    \
     return hipGetLastError();                                                                                 \
   }
-  const char* ct = getenv("MMF_DW_CT");  // MMF_DW_CT=0: runtime-geometry kernels only (A/B)
-  if (!(ct && *ct == '0')) {
+  if (ct) {  // ct = 0: runtime-geometry kernels only (A/B option "dw_ct")
     MMF_DWCT(3, 1, 16, 32, 4)
     MMF_DWCT(3, 1, 14, 48, 2)
     MMF_DWCT(5, 1, 14, 48, 2)
@@ -757,7 +756,7 @@ bool expand_dw_applicable(int cin, int cexp) { return cin <= 64 && (cin % 8) == 
 
 hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const float* be, const float* w,
                             const float* bias, bf16_t* out, float* pool_part, int B, int H, int W, int C, int k,
-                            int stride, int* nchunks_out, hipStream_t s) {
+                            int stride, int* nchunks_out, hipStream_t s, int ct) {
   int T, CW, tiles_x, ntiles;
   dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
   if (!expand_dw_applicable(cin, C) || CW != 48) return hipErrorInvalidValue;
@@ -774,8 +773,7 @@ hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const fl
                        pool_part, H, W, C, CW, T, tiles_x);                                                   \
     return hipGetLastError();                                                                                 \
   }
-  const char* ct = getenv("MMF_DW_CT");
-  if (!(ct && *ct == '0')) {
+  if (ct) {
     MMF_EDWCT(3, 2, 1, 8, 2)
     MMF_EDWCT(3, 1, 1, 14, 2)
     MMF_EDWCT(5, 1, 2, 14, 2)
@@ -789,7 +787,7 @@ hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const fl
                        pool_part, H, W, C, CW, T, tiles_x);                                                      \
     return hipGetLastError();                                                                                    \
   }
-  // runtime-geometry fallbacks (MMF_DW_CT=0)
+  // runtime-geometry kernels (option dw_ct = 0)
   MMF_EDW(3, 2, 1) MMF_EDW(3, 1, 1) MMF_EDW(5, 2, 1) MMF_EDW(5, 1, 2) MMF_EDW(3, 2, 2)
 #undef MMF_EDW
   return hipErrorInvalidValue;

@@ -287,7 +287,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   const rsrc_t rres = make_rsrc(g.res32 ? (const void*)g.res32 : (const void*)g.res16,
                                 ((uint32_t)(M - 1) * g.ldr + N) * (g.res32 ? 4u : 2u));
   const rsrc_t rc32 = make_rsrc(g.c32, out_elems * 4u);
-  const rsrc_t rc16 = make_rsrc(g.c16, (g.probe & 1) ? 0u : out_elems * 2u);  // probe 1: drop bf16 stores
+  const rsrc_t rc16 = make_rsrc(g.c16, out_elems * 2u);
 
   int t = wgid;
   if (t >= tiles) return;
@@ -315,10 +315,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
     for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
 
     for (int kt = 0; kt < nk; ++kt) {
-      if (!(g.probe & 4)) {  // probe 4: no operand staging in the K loop (LDS-read + MFMA bound)
-        if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
-        else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
-      }
+      if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
+      else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
       const bf16_t* Xs = lds + cur * STAGE;
       const bf16_t* Ws = Xs + BM * BK;
       if constexpr (BN == 192) {
@@ -370,7 +368,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
     // branch and no load that has to wait on the stores issued before it -- bias columns were
     // fetched at tile start and residual rows are loaded one fragment row AHEAD of the stores (one
     // vmcnt counter covers loads and stores in issue order).
-    if (!g.c16 && !g.c32) continue;  // nothing to store (MMF_GEMM_NOSTORE probe)
     if (!has_res && !g.c32) {
       // bf16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
       // fragment of each pair so every lane stores 16 contiguous bytes (half the store issues)
@@ -384,9 +381,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
           for (int h2 = 0; h2 < 2; ++h2) {
             float v[4] = {acc[i + h2][j][0] + bias_r[i + h2].x, acc[i + h2][j][1] + bias_r[i + h2].y,
                           acc[i + h2][j][2] + bias_r[i + h2].z, acc[i + h2][j][3] + bias_r[i + h2].w};
-            if (ACT != ACT_NONE && !(g.probe & 2)) {  // probe 2: skip the activation
-              act4<ACT>(v);
-            }
+            if (ACT != ACT_NONE) act4<ACT>(v);
             pk[h2] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
           }
           const bool odd = fg & 1;
@@ -395,9 +390,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
           const int n8 = n0 + wn * TN + (odd ? (i + 1) * 16 + (fg - 1) * 4 : i * 16 + fg * 4);
           const uint4 o = pair_rows16(pk[0], pk[1]);
           const uint32_t off = (m * (uint32_t)g.ldc + n8) * 2u;
-          if (g.probe & 16) {  // probe 16: compute everything, issue no store
-            asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
-          } else if (full8) {
+          if (full8) {
             buf_store_u4(rc16, n8 < N ? off : kOOB, o);
           } else {  // N % 8 == 4: the last group of a row holds only 4 valid columns
             buf_store_u4(rc16, n8 + 8 <= N ? off : kOOB, o);
@@ -451,207 +444,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Ring-pipelined persistent GEMM for bf16-only outputs (the encoder QKV / out-proj / FFN GEMMs):
-// 256 x BN tiles, 8 waves, operands staged by LDS-DMA into an NS-slot ring of 32-deep K-slices.
-//  * slot image: [rows][32] bf16 (64-B rows); 16-B chunk c of row R lives at physical chunk
-//    c ^ ((-(R >> 2)) & 3), which puts the 16 lanes of every ds_read_b128 lane group on 16
-//    distinct 16-B bank slots (the DMA writes lane-linearly, so the XOR is applied to the source
-//    address, and the fragment reads apply the same involution).
-//  * NS-2 slices stay in flight across every barrier: counted `s_waitcnt vmcnt(N)` + raw
-//    s_barrier, never vmcnt(0) in steady state (a K-step no longer waits on the DMA it issued
-//    itself, which cost ~30 % of the main loop in the 2-stage kernel above).
-//  * the slice sequence runs on across this workgroup's tiles, so the next tile's first slices
-//    load under the current tile's last MFMAs, and a tile's epilogue stores stay in flight for
-//    the next NS-2 slices (their count is part of N) instead of being drained at the next barrier.
-//  * bias vector (fp32, zero-padded) lives in the same LDS array, loaded once per launch.
-// ---------------------------------------------------------------------------------------------
-constexpr int RBK = 32;
-constexpr int kRingMaxN = 4096;
-
-template <int N>
-MMF_DEV void vm_wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
-  __builtin_amdgcn_s_barrier();
-}
-
-MMF_DEV int rswz(int row, int c) { return row * RBK + ((c ^ ((-(row >> 2)) & 3)) << 3); }
-
-// LDS read the compiler cannot see: hipcc (ROCm 7.2) places `s_waitcnt vmcnt(0)` before any
-// ds_read that may alias an in-flight LDS-DMA, which in the epilogue would drain the slices the
-// ring keeps in flight.  Only for LDS bytes no DMA ever writes (the bias area).
-MMF_DEV float4 lds_read_f4_opaque(const float* p) {
-  const uint32_t off = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const float*)p);
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(off) : "memory");
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-
-// DMA `nseg` 1-KB segments (16 rows x 64 B) starting at segment `seg0` of a [rows][32] slot image
-MMF_DEV void ring_segs(const bf16_t* __restrict__ G, int ld, int row0, int rowmax, int k0, bf16_t* img, int seg0,
-                       int nseg, int lane) {
-  for (int j = 0; j < nseg; ++j) {
-    const int seg = seg0 + j;
-    const int r = seg * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ ((-(r >> 2)) & 3);  // logical chunk landing at physical chunk (lane & 3)
-    int grow = row0 + r;
-    grow = grow < rowmax ? grow : rowmax - 1;  // clamped rows are loaded but never stored
-    const bf16_t* src = G + (size_t)grow * ld + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (lds_void_t*)((__attribute__((address_space(3))) bf16_t*)img + seg * 512), 16,
-                                     0, 0);
-  }
-}
-
-template <int BN, int WGM, int WGN, int NS, int ACT>
-__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tilesN, int tiles) {
-  constexpr int BM = 256;
-  constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16, NP = NI / 2;
-  constexpr int SLOT = (BM + BN) * RBK;  // bf16 elements per ring slot
-  constexpr int SEGA = BM / 16, SEGW = BN / 16;
-  constexpr int ALO = SEGA / 8, WLO = SEGW / 8, WHI = (SEGW + 7) / 8, WNHI = SEGW - 8 * WLO;
-  constexpr int LLO = ALO + WLO, LHI = ALO + WHI;  // DMA instructions per slice (per wave class)
-  constexpr int S_EPI = MI * NP;                   // vector-memory instructions of one epilogue
-  static_assert(WGM * WGN == 8 && SEGA % 8 == 0 && NI % 2 == 0, "geometry");
-  static_assert((NS - 2) * LHI + S_EPI < 64, "vmcnt field");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[NS * SLOT + 2 * kRingMaxN];
-  float* const lds_bias = reinterpret_cast<float*>(lds + NS * SLOT);
-
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, xq = nwg >> 3, xr = nwg & 7;
-  const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (bid >> 3);
-  if (wgid >= tiles) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int M = g.M, N = g.N, nk = g.K / RBK;
-  const bool hi_wave = wave < WNHI;
-  const int wseg0 = hi_wave ? wave * WHI : WNHI * WHI + (wave - WNHI) * WLO;
-  const int wnseg = hi_wave ? WHI : WLO;
-  const uint32_t out_elems = (uint32_t)(M - 1) * g.ldc + N;
-  const rsrc_t rc16 = make_rsrc(g.c16, (g.probe & 1) ? 0u : out_elems * 2u);  // probe 1: drop stores
-
-  for (int n = tid; n < kRingMaxN; n += 512) lds_bias[n] = (g.bias && n < N) ? g.bias[n] : 0.0f;
-
-  const int ntl = (tiles - wgid + nwg - 1) / nwg;  // tiles of this workgroup: wgid + i * nwg
-  const int total = ntl * nk;                       // K-slices it consumes
-  int iss = 0, iss_tile = wgid, iss_k = 0, iss_slot = 0;
-  auto issue = [&]() {
-    if (iss < total) {
-      const int tm = iss_tile / tilesN, tn = iss_tile - tm * tilesN;
-      bf16_t* img = lds + iss_slot * SLOT;
-      ring_segs(g.A, g.lda, tm * BM, M, iss_k * RBK, img, wave * ALO, ALO, lane);
-      ring_segs(g.W, g.ldw, tn * BN, N, iss_k * RBK, img + BM * RBK, wseg0, wnseg, lane);
-      if (++iss_k == nk) iss_k = 0, iss_tile += nwg;
-    }
-    ++iss;
-    iss_slot = (iss_slot + 1 == NS) ? 0 : iss_slot + 1;
-  };
-  // wait for slice q+1 at the end of slice q; `sw`: the last epilogue's stores are younger than it
-  auto wait_next = [&](int q, bool sw) {
-    if (q + NS - 1 >= total) {
-      vm_wait_barrier<0>();  // tail: fewer slices in flight than the counts below assume
-    } else if (hi_wave) {
-      if (sw) vm_wait_barrier<(NS - 2) * LHI + S_EPI>();
-      else vm_wait_barrier<(NS - 2) * LHI>();
-    } else {
-      if (sw) vm_wait_barrier<(NS - 2) * LLO + S_EPI>();
-      else vm_wait_barrier<(NS - 2) * LLO>();
-    }
-  };
-
-#pragma unroll
-  for (int i = 0; i < NS - 1; ++i) issue();
-  if (NS - 1 >= total) vm_wait_barrier<0>();
-  else if (hi_wave) vm_wait_barrier<(NS - 2) * LHI>();
-  else vm_wait_barrier<(NS - 2) * LLO>();
-
-  int q = 0, slot = 0, sw = 0;
-  for (int t = wgid; t < tiles; t += nwg) {
-    const int tm = t / tilesN, tn = t - tm * tilesN;
-    const int m0 = tm * BM, n0 = tn * BN;
-    f32x4 acc[NI][MI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int kk = 0; kk < nk; ++kk, ++q) {
-      issue();  // slice q + NS - 1 into the slot slice q - 1 was read from (freed by the last barrier)
-      const bf16_t* Xs = lds + slot * SLOT;
-      const bf16_t* Ws = Xs + BM * RBK;
-      bf16x8 wf[NI], xf[MI];
-#pragma unroll
-      for (int i = 0; i < NI; ++i) wf[i] = as_bf16x8(*reinterpret_cast<const uint4*>(Ws + rswz(wn * TN + i * 16 + fr, fg)));
-#pragma unroll
-      for (int j = 0; j < MI; ++j) xf[j] = as_bf16x8(*reinterpret_cast<const uint4*>(Xs + rswz(wm * TM + j * 16 + fr, fg)));
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
-      wait_next(q, sw > 0);
-      if (sw > 0) --sw;
-      slot = (slot + 1 == NS) ? 0 : slot + 1;
-    }
-
-    // epilogue: bias (LDS) + activation, bf16, paired 16-B stores (lanes l and l^16 own adjacent
-    // 4-column groups of one row; one fragment of each pair is swapped across them)
-    float4 bias_r[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) bias_r[i] = lds_read_f4_opaque(lds_bias + n0 + wn * TN + i * 16 + fg * 4);
-#pragma unroll
-    for (int j = 0; j < MI; ++j) {
-      const uint32_t m = m0 + wm * TM + j * 16 + fr;
-#pragma unroll
-      for (int i = 0; i < NI; i += 2) {
-        uint2 pk[2];
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const float4 b = bias_r[i + h2];
-          float v[4] = {acc[i + h2][j][0] + b.x, acc[i + h2][j][1] + b.y, acc[i + h2][j][2] + b.z,
-                        acc[i + h2][j][3] + b.w};
-          if (ACT != ACT_NONE) {
-            act4<ACT>(v);
-          }
-          pk[h2] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-        }
-        const bool odd = fg & 1;
-        const uint2 send = odd ? pk[0] : pk[1];
-        uint2 recv;
-        recv.x = __shfl_xor(send.x, 16, 64);
-        recv.y = __shfl_xor(send.y, 16, 64);
-        const int n8 = n0 + wn * TN + (odd ? (i + 1) * 16 + (fg - 1) * 4 : i * 16 + fg * 4);
-        const uint4 o = odd ? make_uint4(recv.x, recv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, recv.x, recv.y);
-        buf_store_u4(rc16, n8 < N ? (m * (uint32_t)g.ldc + n8) * 2u : kOOB, o);  // N % 8 == 0 here
-      }
-    }
-    sw = NS - 2;
-  }
-}
-
-template <int BN, int WGM, int WGN, int NS>
-hipError_t run_ring(const GemmArgs& a, hipStream_t s) {
-  const int tilesM = (a.M + 255) / 256, tilesN = (a.N + BN - 1) / BN;
-  const int tiles = tilesM * tilesN;
-  const int grid = tiles < 256 ? tiles : 256;
-#define MMF_RING_CASE(ACT)                                                                                        \
-  case ACT:                                                                                                       \
-    hipLaunchKernelGGL((gemm_ring_kernel<BN, WGM, WGN, NS, ACT>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles); \
-    break;
-  switch (a.act) {
-    MMF_RING_CASE(ACT_NONE)
-    MMF_RING_CASE(ACT_GELU)
-    MMF_RING_CASE(ACT_QUICK_GELU)
-    MMF_RING_CASE(ACT_SILU)
-    MMF_RING_CASE(ACT_RELU)
-    default:
-      return hipErrorInvalidValue;
-  }
-#undef MMF_RING_CASE
-  return hipGetLastError();
-}
-
 template <int BM, int BN, int WGM, int WGN>
 hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
@@ -659,8 +451,7 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int per_cu = (BM == 128) ? 2 : 1;  // co-resident workgroups per CU (LDS / VGPR budget)
   const int grid = tiles < 256 * per_cu ? tiles : 256 * per_cu;
   const dim3 blk(64 * WGM * WGN);
-  const char* gme = getenv("MMF_GEMM_GROUPM");  // tile-order override (tools/ab_env.py)
-  const int gm = (gme && *gme) ? atoi(gme) : 0;
+  const int gm = a.group_m;  // tile-order option (handle option "gemm_group_m"; 0 = row-major)
 #define MMF_GLDS_CASE(ACT)                                                                                  \
   case ACT:                                                                                                 \
     hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT>), dim3(grid), blk, 0, s, a, tilesN, tiles, tilesM, \
@@ -754,22 +545,13 @@ static bool glds_ok(const GemmArgs& a) {
   return (a.K % BK) == 0 && !a.ascale && rows * a.ldc * 4 < lim && rows * (a.ldr > 0 ? a.ldr : 0) * 4 < lim;
 }
 
-// ring kernel: bf16-only output, K % 32 == 0, whole 8-column groups, bias vector fits its LDS area
-static bool ring_ok(const GemmArgs& a) {
-  const size_t lim = (size_t)1 << 31;
-  return a.c16 && !a.c32 && !a.res32 && !a.res16 && !a.ascale && (a.K % RBK) == 0 && (a.N % 8) == 0 &&
-         a.N <= kRingMaxN && ((size_t)a.M + 256) * a.ldc * 2 < lim;
-}
-
 static int forced_config(const GemmArgs& a) {
-  // MMF_GEMM_CONFIG=<n>: benchmarking override (tools/gemm_bench.py); ignored if inapplicable
-  const char* e = getenv("MMF_GEMM_CONFIG");
-  if (!e || !*e) return -1;
-  const int c = atoi(e);
+  // handle option "gemm_config" (benchmarking override, tools/gemm_bench.py); ignored if inapplicable
+  if (a.force_cfg <= 0) return -1;
+  const int c = a.force_cfg - 1;
   if (c >= 4 && c <= 8 && !glds_ok(a)) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
-  if (c >= 10 && c <= 12 && !ring_ok(a)) return -1;
-  return (c >= 0 && c <= 12) ? c : -1;
+  return (c >= 0 && c <= 9) ? c : -1;
 }
 
 int gemm_config(const GemmArgs& a) {
@@ -779,23 +561,6 @@ int gemm_config(const GemmArgs& a) {
   if (a.N <= 32) return 0;
   if (a.N <= 64) return 1;
   if (a.M <= 512) return 2;  // skinny-M (projections, M = batch)
-  // ring kernel: opt-in (MMF_GEMM_RING=1) -- measured 5-15 % slower than the 2-stage kernel on
-  // the encoder shapes (BK = 32 slices cost more barriers / fragment restarts than the deeper
-  // prefetch recovers)
-  const char* re = getenv("MMF_GEMM_RING");
-  if (ring_ok(a) && a.N >= 128 && re && *re == '1') {
-    const long tm = (a.M + 255) / 256;
-    const int bns[3] = {256, 192, 128}, cfg[3] = {10, 11, 12};
-    const double eff[3] = {1.0, 0.97, 0.88};
-    int best = 10;
-    double bc = 1e30;
-    for (int i = 0; i < 3; ++i) {
-      const long tiles = tm * ((a.N + bns[i] - 1) / bns[i]);
-      const double c = (double)((tiles + 255) / 256) * bns[i] / eff[i];
-      if (c < bc) { bc = c; best = cfg[i]; }
-    }
-    return best;
-  }
   if (glds_ok(a) && a.N >= 128) {
     // persistent 256-row LDS-DMA tiles: pick the column tile that minimises whole "rounds" of
     // 256 CUs x per-tile time (wider tiles are more efficient per flop)
@@ -821,8 +586,7 @@ int gemm_splitk_factor(const GemmArgs& a) {
   // slices of 256 (4 K-steps) when that gives >= 2 of them; the partial planes need N % 4 == 0
   // and 16-B aligned rows for the reduction's float4 accesses
   if (a.ascale || (a.K % 256) || a.K < 512 || (a.N & 3) || (a.ldc & 3) || (a.ldr & 3)) return 1;
-  const char* e = getenv("MMF_GEMM_SPLITK");  // benchmarking override: 0 disables
-  if (e && *e == '0') return 1;
+  if (a.no_splitk) return 1;  // handle option "gemm_splitk" = 0 (A/B tests)
   return a.K / 256;
 }
 
@@ -830,19 +594,14 @@ const char* gemm_config_name(int c) {
   static const char* names[] = {"gemm_bf16<256,32,4,1>",  "gemm_bf16<256,64,4,1>",  "gemm_bf16<64,128,1,4>",
                                 "gemm_bf16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
                                 "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
-                                "pw_conv",                "gemm_ring<256,256,ns4>", "gemm_ring<256,192,ns5>",
-                                "gemm_ring<256,128,ns5>"};
-  return (c >= 0 && c < 13) ? names[c] : "gemm_bf16<?>";
+                                "pw_conv"};
+  return (c >= 0 && c < 10) ? names[c] : "gemm_bf16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
   if (a0.M <= 0 || a0.N <= 0 || a0.K <= 0) return hipSuccess;
   if ((a0.K & 7) || (a0.N & 3) || (a0.lda & 7) || (a0.ldw & 7) || (a0.ldc & 3)) return hipErrorInvalidValue;
-  GemmArgs a = a0;
-  const char* pr = getenv("MMF_GEMM_PROBE");  // benchmarking probe bits (tools/gemm_bench.py)
-  a.probe = (pr && *pr) ? atoi(pr) : 0;
-  const char* ns = getenv("MMF_GEMM_NOSTORE");  // benchmarking probe: main loop only, no epilogue traffic
-  if (ns && *ns == '1') a.c16 = nullptr, a.c32 = nullptr, a.res32 = nullptr, a.res16 = nullptr;
+  const GemmArgs& a = a0;
   switch (gemm_config(a)) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);
@@ -857,9 +616,6 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
     case 7: return run_glds<128, 192, 2, 2>(a, s);
     case 8: return run_glds<128, 128, 2, 2>(a, s);
     case 9: return launch_pw(a, s);
-    case 10: return run_ring<256, 2, 4, 4>(a, s);
-    case 11: return run_ring<192, 4, 2, 5>(a, s);
-    case 12: return run_ring<128, 4, 2, 5>(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

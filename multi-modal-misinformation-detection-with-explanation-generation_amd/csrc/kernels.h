@@ -19,7 +19,9 @@ struct GemmArgs {
   const float* ascale;           // per-(batch, k) fp32 scale of A (SE excitation) or null
   int rows_per_batch;            // rows of A per batch item when ascale != null
   int M, N, K, act;
-  int probe;                     // benchmarking probes (0 in production; see gemm.hip)
+  int force_cfg;                 // 0 = automatic tile choice, c + 1 = instantiation c (A/B option)
+  int no_splitk;                 // 1 = never split K on the skinny-M path (A/B option)
+  int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
 };
@@ -106,8 +108,10 @@ hipError_t launch_effnet_stem_f32(const float* x_nchw, const float* w, const flo
 hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
                                  const float* wd, const float* bd, bf16_t* out, float* pool_part, int B,
                                  int* nchunks_out, hipStream_t s);
+// ct = 0 forces the runtime-geometry kernels (A/B option "dw_ct"; the default uses the
+// compile-time tile geometries)
 hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part,
-                         int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s);
+                         int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s);
 hipError_t launch_gap_classifier(const bf16_t* x, int HW, int C, const float* w, const float* b, float* logits,
@@ -118,6 +122,6 @@ hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t
 bool expand_dw_applicable(int cin, int cexp);
 hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const float* be, const float* w,
                             const float* bias, bf16_t* out, float* pool_part, int B, int H, int W, int C, int k,
-                            int stride, int* nchunks_out, hipStream_t s);
+                            int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 // number of pool-partial chunks launch_dwconv uses for an output of Ho x Wo with C channels
 int dwconv_nchunks(int H, int W, int C, int stride);

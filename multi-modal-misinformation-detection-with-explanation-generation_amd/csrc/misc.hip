@@ -201,8 +201,18 @@ __global__ __launch_bounds__(256) void vault_sims_kernel(const float* q, const f
   }
 }
 
-// (value desc, index desc) order, i.e. numpy argsort()[-k:][::-1] for distinct values
-MMF_DEV bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia > ib); }
+// Ranking of the reference's np.argsort(sims)[-k:][::-1] (misinfo_forensics.py:449): value
+// descending; numpy sorts NaN (a zero-norm vault row: 0/0 in the renormalisation, :443-445) after
+// every number, so the reversed tail puts NaN rows FIRST.  Exact ties: numpy's default sort is not
+// stable (its tie order is data- and platform-dependent); ties are ordered here by
+// descending index = what a stable argsort would give.  Index -1 marks an empty slot (always worst).
+MMF_DEV bool better(float a, int ia, float b, int ib) {
+  if (ib < 0) return ia >= 0;
+  if (ia < 0) return false;
+  const bool na = a != a, nb = b != b;
+  if (na || nb) return na && (!nb || ia > ib);
+  return a > b || (a == b && ia > ib);
+}
 
 template <int K>
 __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, int N, float thresh, float* sims,
@@ -276,6 +286,54 @@ __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, 
   }
 }
 
+// top-k for k > 8 (search_vault's top_k is a free parameter): one 1024-thread block per query
+// row sorts all N similarities (padded to P, a power of two) in LDS with a bitonic network under
+// the same `better` order, then writes the first k.  N <= P <= 16384 (128 KB of LDS).
+template <int P>
+__global__ __launch_bounds__(1024) void vault_sort_topk_kernel(const float* S, int B, int N, int k, float thresh,
+                                                               float* sims, int32_t* idx, float* disc,
+                                                               int disc_stride, const float* temb,
+                                                               const float* title, int D, float* tsim) {
+  __shared__ float key[P];
+  __shared__ int id[P];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float* s = S + (size_t)row * N;
+  for (int i = tid; i < P; i += 1024) {
+    key[i] = i < N ? s[i] : -INFINITY;
+    id[i] = i < N ? i : -1;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P / 2; i += 1024) {
+        const int lo = 2 * stride * (i / stride) + (i % stride), hi = lo + stride;
+        const bool desc = (lo & size) == 0;  // descending segments; the final pass is all-descending
+        const float a = key[lo], b = key[hi];
+        const int ia = id[lo], ib = id[hi];
+        if (desc ? better(b, ib, a, ia) : better(a, ia, b, ib)) {
+          key[lo] = b; key[hi] = a;
+          id[lo] = ib; id[hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const bool hit = key[0] > thresh;
+  if (tid < k) {
+    if (sims) sims[(size_t)row * k + tid] = key[tid];
+    if (idx) idx[(size_t)row * k + tid] = id[tid];
+  }
+  if (tid == 0 && disc) disc[(size_t)row * disc_stride] = hit ? key[0] : 0.f;
+  if (tsim && tid < 64) {
+    float d = 0.f;
+    if (hit && temb && title) {
+      for (int c = tid; c < D; c += 64) d = fmaf(temb[(size_t)row * D + c], title[(size_t)id[0] * D + c], d);
+      d = wave_sum(d);
+    }
+    if (tid == 0) tsim[row] = d;
+  }
+}
+
 }  // namespace
 
 hipError_t launch_text_heads(const float* x, int row_stride, const float* w1a, const float* b1a, const float* w2a,
@@ -316,9 +374,20 @@ hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, 
     hipLaunchKernelGGL(vault_topk_kernel<KK>, grid, blk, 0, s, S, B, N, thresh, sims, idx, disc, disc_stride, \
                        text_emb, title_emb, D, text_sim);                                                      \
     break;
+  if (k < 1 || k > N) return hipErrorInvalidValue;
   switch (k) {
     TOPK_CASE(1) TOPK_CASE(2) TOPK_CASE(3) TOPK_CASE(4) TOPK_CASE(5) TOPK_CASE(6) TOPK_CASE(7) TOPK_CASE(8)
-    default: return hipErrorInvalidValue;
+    default: {
+#define SORT_CASE(PP)                                                                                            \
+  if (N <= PP) {                                                                                                 \
+    hipLaunchKernelGGL(vault_sort_topk_kernel<PP>, dim3(B), dim3(1024), 0, s, S, B, N, k, thresh, sims, idx, disc, \
+                       disc_stride, text_emb, title_emb, D, text_sim);                                          \
+    return hipGetLastError();                                                                                    \
+  }
+      SORT_CASE(2048) SORT_CASE(4096) SORT_CASE(8192) SORT_CASE(16384)
+#undef SORT_CASE
+      return hipErrorInvalidValue;
+    }
   }
 #undef TOPK_CASE
   return hipGetLastError();

@@ -9,7 +9,7 @@ from typing import Dict, Optional
 import numpy as np
 import torch
 
-from . import hip
+from . import hip, io_utils
 from .hip import check, ptr, stream_ptr
 
 SCORE_KEYS = ("ai_score", "misinfo_score", "deepfake_score", "clip_similarity", "vault_discrepancy")
@@ -62,15 +62,32 @@ class Engine:
     def ready(self) -> int:
         return self.lib.mmf_ready(self.h)
 
+    # ------------------------------------------------------------------ options / accounting
+    def set_option(self, name: str, value: int) -> None:
+        """A/B switches of the library (include/mmf_hip.h: mmf_set_option)."""
+        check(self.lib.mmf_set_option(self.h, name.encode(), int(value)), f"mmf_set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int()
+        check(self.lib.mmf_get_option(self.h, name.encode(), ctypes.byref(v)), f"mmf_get_option({name})")
+        return v.value
+
+    @property
+    def device_bytes(self) -> int:
+        """Device memory owned by this handle (weights, workspaces, vault)."""
+        return int(self.lib.mmf_device_bytes(self.h))
+
     def reserve(self, max_batch: int, max_text_len: int = 128, max_clip_len: int = 77) -> None:
         check(self.lib.mmf_reserve(self.h, max_batch, max_text_len, max_clip_len), "mmf_reserve")
         self.max_batch, self.max_text_len, self.max_clip_len = max_batch, max_text_len, max_clip_len
 
     # ------------------------------------------------------------------ vault
     def set_vault(self, embeddings: np.ndarray, title_ids=None, title_mask=None) -> None:
-        v = np.ascontiguousarray(_as_np(embeddings), dtype=np.float32)
-        check(self.lib.mmf_set_vault(self.h, v.ctypes.data_as(ctypes.c_void_p), v.shape[0], v.shape[1]),
-              "mmf_set_vault")
+        """Rows normalised once, exactly as the reference does on every search call (numpy, in the
+        vault's own dtype: io_utils.vault_unit_rows), then uploaded as float32."""
+        v = np.ascontiguousarray(io_utils.vault_unit_rows(_as_np(embeddings)), dtype=np.float32)
+        check(self.lib.mmf_set_vault_normalized(self.h, v.ctypes.data_as(ctypes.c_void_p), v.shape[0], v.shape[1]),
+              "mmf_set_vault_normalized")
         self.vault_n = v.shape[0]
         if title_ids is not None:
             ids = self._i32(title_ids)
@@ -130,6 +147,19 @@ class Engine:
         check(self.lib.mmf_clip_text(self.h, ptr(ids), ptr(mask), ids.shape[0], ids.shape[1], ptr(e),
                                      stream_ptr()), "mmf_clip_text")
         return e
+
+    def clip_consistency(self, img, ids, mask, out: Optional[dict] = None) -> dict:
+        """analyze_consistency over a batch: {img_emb, txt_emb [B,512] unit, sim [B]} (one call,
+        the CLIP text tower on a concurrent stream)."""
+        img = self._u8(img)
+        ids, mask = self._i32(ids), self._i32(mask)
+        B = img.shape[0]
+        if out is None:
+            out = {"img_emb": self._f32(B, 512), "txt_emb": self._f32(B, 512), "sim": self._f32(B)}
+        check(self.lib.mmf_clip_consistency(self.h, ptr(img), ptr(ids), ptr(mask), B, ids.shape[1],
+                                            ptr(out["img_emb"]), ptr(out["txt_emb"]), ptr(out["sim"]), stream_ptr()),
+              "mmf_clip_consistency")
+        return out
 
     def vault_topk(self, q_unit: torch.Tensor, k: int = 5, thresh: float = 0.85, text_emb=None):
         q = q_unit.contiguous()

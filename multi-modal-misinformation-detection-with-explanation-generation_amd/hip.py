@@ -29,7 +29,9 @@ SIGNATURES = {
     "mmf_effnet_forward_f32": (_I, [_P, _P, _I, _P, _P, _P]),
     "mmf_clip_image": (_I, [_P, _P, _I, _P, _P]),
     "mmf_clip_text": (_I, [_P, _P, _P, _I, _I, _P, _P]),
+    "mmf_clip_consistency": (_I, [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
     "mmf_set_vault": (_I, [_P, _P, _I, _I]),
+    "mmf_set_vault_normalized": (_I, [_P, _P, _I, _I]),
     "mmf_set_vault_titles": (_I, [_P, _P, _P, _I, _I, _P]),
     "mmf_vault_topk": (_I, [_P, _P, _I, _I, _F, _P, _P, _P, _P, _P, _P]),
     "mmf_fusion": (_I, [_P, _P, _I, _P, _P, _P, _P, _P]),
@@ -37,7 +39,10 @@ SIGNATURES = {
     "mmf_profile_begin": (_I, [_P]),
     "mmf_profile_end": (_I, [_P, _I, _P, _P, _P, _P]),
     "mmf_profile_kind_name": (ctypes.c_char_p, [_I]),
-    "mmf_gemm_bf16":(_I, [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "mmf_set_option": (_I, [_P, ctypes.c_char_p, _I]),
+    "mmf_get_option": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_I)]),
+    "mmf_device_bytes": (ctypes.c_int64, [_P]),
+    "mmf_gemm_bf16": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "mmf_gemm_bf16_ex": (_I, [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P]),
     "mmf_attention_bf16": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }
@@ -74,6 +79,18 @@ def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = load().mmf_last_error().decode(errors="replace")
         raise MMFError(f"{what or 'mmf call'} failed ({rc}): {msg}")
+
+
+def set_process_option(name: str, value: int) -> None:
+    """Process-wide default of a library option (mmf_set_option with a NULL handle): used by the
+    handle-less ops and by handles created afterwards."""
+    check(load().mmf_set_option(None, name.encode(), int(value)), f"mmf_set_option({name})")
+
+
+def get_process_option(name: str) -> int:
+    v = ctypes.c_int()
+    check(load().mmf_get_option(None, name.encode(), ctypes.byref(v)), f"mmf_get_option({name})")
+    return v.value
 
 
 def ptr(t) -> int | None:

@@ -107,7 +107,7 @@ class _SafeUnpickler(pickle.Unpickler):
 
 
 def load_vault(path: str):
-    """Returns (embeddings float32 [N, D], metadata list of {title, url, date}) or (None, None)
+    """Returns (embeddings [N, D] in the stored dtype, metadata list of {title, url, date}) or (None, None)
     for an unknown format, following misinfo_forensics.py:222-246.  Accepts the reference's
     pickle (restricted unpickler), .npz, or .json."""
     if path.endswith(".npz"):
@@ -130,4 +130,14 @@ def load_vault(path: str):
                  "url": paths[i] if i < len(paths) else "N/A", "date": "N/A"} for i in range(len(texts))]
     else:
         return None, None
-    return np.ascontiguousarray(np.asarray(emb, dtype=np.float32)), meta
+    return np.ascontiguousarray(np.asarray(emb)), meta  # stored dtype kept (search renormalises in it)
+
+
+def vault_unit_rows(emb) -> np.ndarray:
+    """misinfo_forensics.py:443-445 as written: ``V / np.linalg.norm(V, axis=1, keepdims=True)`` in
+    the vault's own dtype (a float16 vault renormalises in float16; a zero row becomes NaN, which
+    the device ranking then places first, as numpy's argsort does).  The reference recomputes this
+    on every search call; it is done once, when the vault is set."""
+    v = np.asarray(emb)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return v / np.linalg.norm(v, axis=1, keepdims=True)

@@ -102,6 +102,8 @@ def generate_embeddings_database(model_path: str = "clip_detective_best.pth",
     process group (one process per GPU); world = 1 runs single-process."""
     if processor is None:
         raise RuntimeError("a CLIP processor/tokenizer is required (pass processor=)")
+    if not os.path.isabs(model_path):  # train_clip_detective.py:476-477 (stored in the metadata)
+        model_path = os.path.join(os.getcwd(), model_path)
     if encode is None:
         if engine is None:
             from .engine import Engine

@@ -100,14 +100,15 @@ def roberta_spec(prefix: str = "") -> "OrderedDict":
     return d
 
 
-def effnet_spec(prefix: str = "", num_classes: int = 2) -> "OrderedDict":
+def effnet_spec(prefix: str = "", num_classes: int = 2, conv_gain: float = 1.3) -> "OrderedDict":
     d: OrderedDict = OrderedDict()
 
-    # Conv init N(0, (1.3^2)/fan_in): between torchvision's kaiming fan_out init (the random
-    # network collapses to an input-independent output) and He fan_in (chaotic: any rounding is
-    # amplified to O(1e-2) in the deepfake score).  See DESIGN.md "Numerics".
+    # Conv init N(0, conv_gain^2 / fan_in).  The default 1.3 sits between torchvision's kaiming
+    # fan_out init (the random network collapses to an input-independent output) and He fan_in
+    # (gain sqrt 2: chaotic, rounding is amplified in the deepfake score); the parity tests also run
+    # the He draw (DESIGN.md "Numerics").
     def conv(name, cout, cin_g, k):
-        d[f"{name}.weight"] = ((cout, cin_g, k, k), ("he", cin_g * k * k, 1.3))
+        d[f"{name}.weight"] = ((cout, cin_g, k, k), ("he", cin_g * k * k, conv_gain))
 
     conv(f"{prefix}features.0.0", EFFNET_STEM, 3, 3)
     _bn(d, f"{prefix}features.0.1", EFFNET_STEM)
@@ -134,7 +135,7 @@ def effnet_spec(prefix: str = "", num_classes: int = 2) -> "OrderedDict":
     return d
 
 
-def detector_spec() -> "OrderedDict":
+def detector_spec(effnet_gain: float = 1.3) -> "OrderedDict":
     """Full ``MultiModalMisinfoDetector`` state dict (misinfo_forensics.py:43-108)."""
     d: OrderedDict = OrderedDict()
     d.update(roberta_spec("roberta."))
@@ -144,7 +145,7 @@ def detector_spec() -> "OrderedDict":
         s0, s3 = 1 / math.sqrt(3 * ROBERTA["hidden"]), 1 / math.sqrt(3 * 256)
         _lin(d, f"{head}.0", 256, ROBERTA["hidden"], s0, bstd=s0)
         _lin(d, f"{head}.3", 2, 256, s3, bstd=s3)
-    d.update(effnet_spec("efficientnet."))
+    d.update(effnet_spec("efficientnet.", conv_gain=effnet_gain))
     _lin(d, "fusion_layer.0", 64, 5, 0.5, bstd=0.1)
     _lin(d, "fusion_layer.3", 32, 64, 0.2, bstd=0.1)
     _lin(d, "fusion_layer.5", 2, 32, 0.3, bstd=0.1)
@@ -228,8 +229,8 @@ def generate(spec, seed: int = 0, names: Iterable[str] | None = None) -> Dict[st
     return out
 
 
-def synthetic_detector_state(seed: int = 0) -> Dict[str, np.ndarray]:
-    return generate(detector_spec(), seed)
+def synthetic_detector_state(seed: int = 0, effnet_gain: float = 1.3) -> Dict[str, np.ndarray]:
+    return generate(detector_spec(effnet_gain), seed)
 
 
 def synthetic_clip_state(seed: int = 0) -> Dict[str, np.ndarray]:

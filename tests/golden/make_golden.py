@@ -2,6 +2,7 @@
 
     python tests/golden/make_golden.py            # writes tests/golden/golden.npz + golden.json
     python tests/golden/make_golden.py --video    # writes tests/golden/golden_video.json
+    python tests/golden/make_golden.py --vault-edge  # writes tests/golden/golden_vault_edge.json
 
 What runs: ``/root/reference/misinfo_forensics.py`` and ``clip_similarity_engine.py`` are
 imported unmodified.  Because the build container has no network, weights or tokenizer
@@ -179,6 +180,52 @@ def video_fixtures(S) -> dict:
     return js
 
 
+def vault_edge_fixtures(S) -> dict:
+    """The reference's search_vault (misinfo_forensics.py:410-491) on the vault_edge.py cases.  The
+    query image features are planted through the CLIP proxy (get_image_features returns the case's
+    raw query; the reference normalises it itself), so only the vault arithmetic and ranking run."""
+    import vault_edge as VE
+    mf = S["mf"]
+    saved = (mf.vault_embeddings, mf.vault_metadata, mf.clip_model)
+    meta = [{"title": f"Guardian article {j}", "url": f"https://example.org/a/{j}", "date": "N/A"}
+            for j in range(VE.N)]
+    out = {"numpy": np.__version__, "cases": {}}
+
+    class PlantedQuery:
+        q = None
+
+        def get_image_features(self, **kw):
+            return torch.as_tensor(self.q)[None]
+
+    proxy = PlantedQuery()
+    try:
+        mf.clip_model, mf.vault_metadata = proxy, meta
+        for name in VE.CASES:
+            vault, q = VE.case(name)
+            mf.vault_embeddings = vault
+            res = []
+            for i in range(VE.NQ):
+                proxy.q = q[i]
+                for top_k in (5, 12):
+                    r = mf.search_vault(S["pil"][0], top_k=top_k)
+                    res.append({"query": i, "top_k": top_k, "vault_discrepancy": r["vault_discrepancy"],
+                                "text_similarity": r["text_similarity"],
+                                "idx": [int(m["title"].split()[-1]) for m in r["matches"]],
+                                "sims": [m["similarity"] for m in r["matches"]]})
+            out["cases"][name] = {"dtype": str(vault.dtype), "vault_crc": crc(vault), "results": res}
+    finally:
+        mf.vault_embeddings, mf.vault_metadata, mf.clip_model = saved
+    return out
+
+
+def main_vault_edge():
+    S = setup()
+    js = vault_edge_fixtures(S)
+    with open(os.path.join(HERE, "golden_vault_edge.json"), "w") as f:
+        json.dump(js, f, indent=1)
+    print("wrote", os.path.join(HERE, "golden_vault_edge.json"))
+
+
 def main_video():
     S = setup()
     js = video_fixtures(S)
@@ -301,5 +348,7 @@ def main():
 if __name__ == "__main__":
     if "--video" in sys.argv:
         main_video()
+    elif "--vault-edge" in sys.argv:
+        main_vault_edge()
     else:
         main()

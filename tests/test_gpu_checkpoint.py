@@ -1,0 +1,175 @@
+"""Checkpoint paths of the reference on the HIP engine (F4 / B1):
+
+* the constructor overlay of ``forensics_master_final.pth`` (misinfo_forensics.py:175-186,
+  load_state_dict(full_model_state_dict, strict=False));
+* ``test_fusion_model``'s post-construction load (train_fusion_judge.py:294-297: build
+  MisinfoForensics(), then ``detector.load_state_dict(checkpoint['full_model_state_dict'])``
+  strictly) and a head-level load (misinfo_forensics.py:274);
+
+each checked against the fp32 oracle on the LOADED weights (a different synthetic draw than the
+constructor's, so stale device weights cannot pass) at the north-star 1e-3.  The checkpoint has the
+schema train_fusion_judge.py:259-267 writes."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+B = 16
+
+
+def _inputs():
+    import mmf_amd.synthetic as syn
+    rid, rm = syn.roberta_ids(B, 128, 61, [128, 90, 33, 7])
+    cid, cm = syn.clip_ids(B, 77, 61, [77, 40, 12, 3])
+    return rid, rm, cid, cm, syn.images(B, 61)
+
+
+@pytest.fixture(scope="module")
+def trained():
+    import mmf_amd.weights as W
+    return W.synthetic_detector_state(7)  # the "trained" weights the checkpoint carries
+
+
+@pytest.fixture(scope="module")
+def ckpt_path(tmp_path_factory, trained):
+    full = {k: torch.as_tensor(v) for k, v in trained.items()}
+    fusion = {k[len("fusion_layer."):]: v for k, v in full.items() if k.startswith("fusion_layer.")}
+    p = tmp_path_factory.mktemp("ck") / "forensics_master_final.pth"
+    torch.save({"epoch": 7, "fusion_layer_state_dict": fusion, "full_model_state_dict": full,
+                "optimizer_state_dict": {"state": {}, "param_groups": [{"lr": 1e-3, "weight_decay": 0.01,
+                                                                        "params": list(range(6))}]},
+                "scheduler_state_dict": {"last_epoch": 7, "_step_count": 8}, "loss": 0.1234, "accuracy": 95.38},
+               str(p))
+    return str(p)
+
+
+def _oracle(det, clip_sd, inp):
+    from oracle.pipeline import batched_scores
+    rid, rm, cid, cm, imgs = inp
+    with torch.no_grad():
+        return batched_scores(det, clip_sd, rid, rm, cid, cm, imgs, None)
+
+
+def _check(mf, ref, inp, what):
+    rid, rm, cid, cm, imgs = inp
+    out = mf.analyze_batch(rid, rm, cid, cm, imgs)
+    torch.cuda.synchronize()
+    s, p = out["scores"].cpu().numpy(), out["probs"].cpu().numpy()
+    d = np.abs(s - ref["scores"]).max(0)
+    print(f"{what}: max |d score| per signal {np.array2string(d, precision=6)}, "
+          f"probs {np.abs(p - ref['probs']).max():.2e}")
+    np.testing.assert_allclose(s, ref["scores"], atol=TOL, err_msg=what)
+    np.testing.assert_allclose(p, ref["probs"], atol=TOL, err_msg=what)
+
+
+def _mf(det_sd, clip_sd, fusion_weights):
+    from misinfo_forensics import MisinfoForensics
+    return MisinfoForensics(fusion_weights=fusion_weights, faiss_index_path="/nonexistent", detector_state=det_sd,
+                            clip_state=clip_sd, max_batch=B, verbose=False)
+
+
+def test_constructor_overlay(det_sd, clip_sd, trained, ckpt_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    inp = _inputs()
+    mf = _mf(det_sd, clip_sd, ckpt_path)
+    _check(mf, _oracle(trained, clip_sd, inp), inp, "constructor overlay")
+    mf.engine.close()
+
+
+def test_post_construction_load(det_sd, clip_sd, trained, ckpt_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    inp = _inputs()
+    mf = _mf(det_sd, clip_sd, "/nonexistent")
+    _check(mf, _oracle(det_sd, clip_sd, inp), inp, "constructor weights")
+    det = mf.detector
+    up0 = dict(det.uploads)
+    bytes0 = mf.engine.device_bytes
+    ck = torch.load(ckpt_path, map_location=mf.device, weights_only=True)
+    det.load_state_dict(ck["full_model_state_dict"])  # strict, as train_fusion_judge.py:297
+    assert sorted(det.stale_components()) == ["effnet", "fusion", "text"]
+    _check(mf, _oracle(trained, clip_sd, inp), inp, "after detector.load_state_dict")
+    assert all(det.uploads[c] == up0[c] + 1 for c in up0), det.uploads
+    assert mf.engine.device_bytes == bytes0  # the replaced weights were freed
+    # forward_text / forward_image (misinfo_forensics.py:92-104) see the loaded weights too
+    ref = _oracle(trained, clip_sd, inp)
+    ai, _ = det.forward_text(torch.as_tensor(inp[0]).cuda(), torch.as_tensor(inp[1]).cuda())
+    np.testing.assert_allclose(torch.softmax(ai.cpu(), 1)[:, 1].numpy(), ref["scores"][:, 0], atol=TOL)
+    # a head-level load (misinfo_forensics.py:274) re-packs the text component only
+    heads0 = {k[len("ai_head."):]: torch.as_tensor(v) for k, v in det_sd.items() if k.startswith("ai_head.")}
+    det.ai_head.load_state_dict(heads0)
+    assert det.stale_components() == ["text"]
+    ai, _ = det.forward_text(torch.as_tensor(inp[0]).cuda(), torch.as_tensor(inp[1]).cuda())
+    mixed = dict(trained)
+    mixed.update({k: v for k, v in det_sd.items() if k.startswith("ai_head.")})
+    ref2 = _oracle(mixed, clip_sd, inp)
+    np.testing.assert_allclose(torch.softmax(ai.cpu(), 1)[:, 1].numpy(), ref2["scores"][:, 0], atol=TOL)
+    assert det.stale_components() == []
+    mf.engine.close()
+
+
+def test_reload_cycles_keep_device_memory_flat(det_sd, clip_sd, trained):
+    """Ten alternating full reloads + fusion-only updates (a training loop's optimizer steps):
+    the handle's device bytes do not grow."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    mf = _mf(det_sd, clip_sd, "/nonexistent")
+    det = mf.detector
+    a = {k: torch.as_tensor(v) for k, v in trained.items()}
+    b = {k: torch.as_tensor(v) for k, v in det_sd.items()}
+    b0 = mf.engine.device_bytes
+    s = {"ai_score": 0.4, "misinfo_score": 0.6, "deepfake_score": 0.2, "clip_similarity": 0.1,
+         "vault_discrepancy": 0.0}
+    for i in range(10):
+        det.load_state_dict(a if i % 2 == 0 else b)
+        det.sync()
+        with torch.no_grad():
+            det.fusion_layer[0].weight.mul_(1.001)
+        mf.fusion_verdict(s)
+    torch.cuda.synchronize()
+    assert mf.engine.device_bytes == b0
+    assert det.uploads["fusion"] >= 21 and det.uploads["text"] >= 11
+    mf.engine.close()
+
+
+@pytest.mark.parametrize("gain", [1.3, 2 ** 0.5])
+def test_full_size_bench_workload_vs_oracle(clip_sd, gain):
+    """All 256 rows of the benchmark's workload (B = 256, L = 128 text, 77-token captions, 224^2
+    images, the bench's planted vault) against the fp32 oracle, with the default EfficientNet draw
+    and with He fan_in convs (gain sqrt 2, the draw DESIGN.md §4 flags as rounding-sensitive).
+    Prints the max |delta| per score."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    import mmf_amd.weights as W
+    from mmf_amd.engine import Engine
+    from oracle.pipeline import batched_scores
+    det = W.synthetic_detector_state(0, effnet_gain=gain)
+    Bf = 256
+    eng = Engine(0, det, clip_sd, max_batch=Bf)
+    rid, rm = syn.roberta_ids(Bf, 128, 1234)
+    cid, cm = syn.clip_ids(Bf, 77, 1234)
+    imgs = syn.images(Bf, 1234)
+    vault = syn.vault(2170, 512, 77)
+    emb = eng.clip_image(imgs).cpu().numpy()
+    for i, r in enumerate(range(0, 2170, 70)[: Bf // 8]):
+        vault[r] = emb[i * 8] * 2.0
+    eng.set_vault(vault)
+    out = eng.analyze_batch(rid, rm, cid, cm, imgs)
+    torch.cuda.synchronize()
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    with torch.no_grad():
+        ref = batched_scores(det, clip_sd, rid, rm, cid, cm, imgs, vault)
+    d = np.abs(got["scores"] - ref["scores"]).max(0)
+    names = ("ai", "misinfo", "deepfake", "clip_sim", "vault_disc")
+    print(f"gain {gain:.3f}: max |d| " + ", ".join(f"{n} {v:.2e}" for n, v in zip(names, d)) +
+          f"; probs {np.abs(got['probs'] - ref['probs']).max():.2e}")
+    np.testing.assert_allclose(got["scores"], ref["scores"], atol=TOL)
+    np.testing.assert_allclose(got["probs"], ref["probs"], atol=TOL)
+    np.testing.assert_array_equal(got["verdict"], (ref["probs"][:, 1] > 0.5).astype(np.int32))
+    hit = ref["scores"][:, 4] > 0  # planted rows: a clear top-1 (random rows' top-2 gaps can be < 1e-3)
+    assert hit.sum() >= Bf // 8
+    np.testing.assert_array_equal(got["top_idx"][hit, 0], ref["top_idx"][hit, 0])
+    eng.close()

@@ -83,13 +83,21 @@ def test_gemm_bf16_only_output(lib, M, N, K, act):
     assert (out[:, N:] == 7.0).all(), "wrote past N"
 
 
-@pytest.mark.parametrize("cfg", [3, 4, 5, 6, 7, 8, 10, 11, 12])
+@pytest.fixture
+def gemm_config(lib):
+    """Force a GEMM instantiation for the handle-less ops of one test (process default option)."""
+    import mmf_amd.hip as hip
+    yield lambda c: hip.set_process_option("gemm_config", c)
+    hip.set_process_option("gemm_config", -1)
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("M,N,K,act,res", [(1000, 2304, 768, 1, False), (777, 392, 512, 0, True),
                                            (130, 136, 64, 2, False)])
-def test_gemm_forced_configs(lib, monkeypatch, cfg, M, N, K, act, res):
-    """Every tile instantiation (MMF_GEMM_CONFIG override) on ragged M/N, both epilogues."""
+def test_gemm_forced_configs(lib, gemm_config, cfg, M, N, K, act, res):
+    """Every tile instantiation (process option gemm_config) on ragged M/N, both epilogues."""
     import mmf_amd.hip as hip
-    monkeypatch.setenv("MMF_GEMM_CONFIG", str(cfg))
+    gemm_config(cfg)
     g = torch.Generator().manual_seed(cfg * 1000 + M)
     A = _bf16(torch.randn(M, K, generator=g))
     W = _bf16(torch.randn(N, K, generator=g) * 0.05)
@@ -112,33 +120,6 @@ def test_gemm_forced_configs(lib, monkeypatch, cfg, M, N, K, act, res):
     assert (out[:, N:] == 7.0).all(), "wrote past N"
     if res:
         assert (c32.cpu()[:, :N] - ref).abs().max().item() / scale < 2e-5
-
-
-@pytest.mark.parametrize("cfg", [10, 11, 12])
-@pytest.mark.parametrize("M,N,K,act,bias", [(9000, 2312, 512, 2, True), (3000, 520, 128, 0, True),
-                                            (5000, 776, 768, 1, False)])
-def test_gemm_ring_kernel(lib, monkeypatch, cfg, M, N, K, act, bias):
-    """Ring-pipelined GEMM (bf16-only outputs, NS-slot LDS-DMA ring, counted vmcnt): > 256 tiles
-    (the slice sequence and the epilogue-store window cross persistent rounds), K = 128 (fewer
-    slices than ring slots: tail waits), ragged M / N, null bias (LDS bias zero-filled)."""
-    import mmf_amd.hip as hip
-    monkeypatch.setenv("MMF_GEMM_CONFIG", str(cfg))
-    g = torch.Generator().manual_seed(cfg * 7 + M + N)
-    A = _bf16(torch.randn(M, K, generator=g))
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
-    b = torch.randn(N, generator=g) if bias else torch.zeros(N)
-    ref = _act(A.float() @ W.float().T + b, act)
-    dev = torch.device("cuda")
-    Ad, Wd = A.to(dev), W.to(dev)
-    bd = b.to(dev) if bias else None
-    c16 = torch.full((M, N + 8), 7.0, device=dev, dtype=torch.bfloat16)
-    hip.check(lib.mmf_gemm_bf16(Ad.data_ptr(), K, Wd.data_ptr(), K, hip.ptr(bd), None, None,
-                                c16.data_ptr(), N + 8, M, N, K, act, hip.stream_ptr()))
-    torch.cuda.synchronize()
-    scale = ref.abs().max().item()
-    out = c16.cpu().float()
-    assert ((out[:, :N] - ref).abs() <= ref.abs() * 2 ** -7 + 1e-5 * scale).all()
-    assert (out[:, N:] == 7.0).all(), "wrote past N"
 
 
 def _attn_ref(qkv, mask, B, L, H, causal):

@@ -96,21 +96,21 @@ def test_batch_invariance_full_size(engine, det_sd):
     assert ((s[:, :3] >= 0) & (s[:, :3] <= 1)).all() and (np.abs(s[:, 3]) <= 1 + 1e-5).all()
 
 
-def test_fused_expand_dwconv_bit_identical(engine, monkeypatch):
+def test_fused_expand_dwconv_bit_identical(engine):
     """The fused MBConv front (1x1 expand computed per tile into the depthwise conv's LDS tile)
     produces bit-identical EfficientNet outputs to the separate expand GEMM + depthwise launches
     (same MFMA operand order over K, same bias / SiLU / bf16 rounding), on a full 256 batch."""
     import mmf_amd.synthetic as syn
     imgs = syn.images(256, 17)
-    monkeypatch.setenv("MMF_FUSE_EXPAND", "0")
+    engine.set_option("fuse_expand", 0)
     lg0, _ = engine.effnet_forward(imgs)
-    monkeypatch.setenv("MMF_FUSE_EXPAND", "1")
+    engine.set_option("fuse_expand", 1)
     lg1, _ = engine.effnet_forward(imgs)
     torch.cuda.synchronize()
     assert torch.equal(lg0, lg1)
 
 
-def test_fused_stem_dwconv_matches_separate(engine, monkeypatch):
+def test_fused_stem_dwconv_matches_separate(engine):
     """Stem fused into the stage-1 depthwise conv (stem recomputed per halo tile on the MFMA with
     hi/lo-split bf16 operands) vs the separate fp32-FMA stem kernel + depthwise launch.  The two
     stems round differently in the last fp32 bits, which flips occasional bf16 roundings of the
@@ -118,9 +118,9 @@ def test_fused_stem_dwconv_matches_separate(engine, monkeypatch):
     tight bound on the logits; both entry points (uint8 pixels, normalised fp32 NCHW)."""
     import mmf_amd.synthetic as syn
     imgs = syn.images(64, 23)
-    monkeypatch.setenv("MMF_FUSE_STEM", "0")
+    engine.set_option("fuse_stem", 0)
     lg0, s0 = engine.effnet_forward(imgs)
-    monkeypatch.setenv("MMF_FUSE_STEM", "1")
+    engine.set_option("fuse_stem", 1)
     lg1, s1 = engine.effnet_forward(imgs)
     torch.cuda.synchronize()
     np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
@@ -129,25 +129,25 @@ def test_fused_stem_dwconv_matches_separate(engine, monkeypatch):
         mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
         std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
         x = ((torch.as_tensor(imgs[:16]).permute(0, 3, 1, 2).float() / 255.0) - mean) / std
-        monkeypatch.setenv("MMF_FUSE_STEM", "0")
+        engine.set_option("fuse_stem", 0)
         _, f0 = engine.effnet_forward_f32(x)
-        monkeypatch.setenv("MMF_FUSE_STEM", "1")
+        engine.set_option("fuse_stem", 1)
         _, f1 = engine.effnet_forward_f32(x)
         torch.cuda.synchronize()
         np.testing.assert_allclose(f1.cpu().numpy(), f0.cpu().numpy(), atol=TOL)
 
 
-def test_compile_time_dwconv_matches_runtime_geometry(engine, monkeypatch):
+def test_compile_time_dwconv_matches_runtime_geometry(engine):
     """Depthwise kernels with compile-time tile geometry and output runs (dw_compute_ct, the
-    default) vs the runtime-geometry kernels (MMF_DW_CT=0).  Conv outputs are computed in the same
+    default) vs the runtime-geometry kernels (option dw_ct = 0).  Conv outputs are computed in the same
     order; the SE pool partial sums are grouped differently, and those 1-ulp differences flip bf16
     roundings downstream, so the comparison is at the north-star tolerance on deepfake_score (both
     paths are also checked against the fp32 oracle by test_effnet_signal for the default)."""
     import mmf_amd.synthetic as syn
     imgs = syn.images(64, 19)
-    monkeypatch.setenv("MMF_DW_CT", "0")
+    engine.set_option("dw_ct", 0)
     _, s0 = engine.effnet_forward(imgs)
-    monkeypatch.setenv("MMF_DW_CT", "1")
+    engine.set_option("dw_ct", 1)
     _, s1 = engine.effnet_forward(imgs)
     torch.cuda.synchronize()
     np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
@@ -205,21 +205,20 @@ def test_splitk_compact_layers_match_unsplit(engine, golden):
     """The compact last encoder layers and projections (M = batch, K = 512..3072) run split-K
     (fp32 partials over 256-deep K slices + a reduction with the same bias/act/residual order);
     against the unsplit kernel only the fp32 summation order differs."""
-    import os
     import mmf_amd.synthetic as syn
     B = 64
     rid, rm = syn.roberta_ids(B, 128, 21, [128, 77, 12])
     cid, cm = syn.clip_ids(B, 77, 21, [77, 33, 6])
     imgs = syn.images(B, 21)
     outs = []
-    for v in ("0", "1"):
-        os.environ["MMF_GEMM_SPLITK"] = v
+    for v in (0, 1):
+        engine.set_option("gemm_splitk", v)
         try:
             o = engine.analyze_batch(rid, rm, cid, cm, imgs)
             torch.cuda.synchronize()
             outs.append({k: t.cpu().numpy() for k, t in o.items()})
         finally:
-            os.environ.pop("MMF_GEMM_SPLITK", None)
+            engine.set_option("gemm_splitk", 1)
     a, b = outs
     np.testing.assert_allclose(a["scores"], b["scores"], atol=2e-4)
     np.testing.assert_allclose(a["probs"], b["probs"], atol=2e-4)

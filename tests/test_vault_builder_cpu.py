@@ -96,8 +96,9 @@ def test_vault_builder_schema_and_sharded_allgather(tmp_path, capsys):
     assert disk["text_contents"] == [a["text_content"] for a in keep]
     assert disk["image_paths"] == [a["image_local_path"] for a in keep]
     assert disk["image_embeddings"].shape == (8, 512) and disk["text_embeddings"].shape == (8, 512)
-    assert disk["metadata"] == {"model_path": "clip_detective_best.pth", "total_articles": 9,
-                                "embedding_dim": 512, "val_accuracy": 0.75}
+    # model_path is made absolute like train_clip_detective.py:476-477 does
+    assert disk["metadata"] == {"model_path": os.path.join(os.getcwd(), "clip_detective_best.pth"),
+                                "total_articles": 9, "embedding_dim": 512, "val_accuracy": 0.75}
     np.testing.assert_allclose(np.linalg.norm(disk["image_embeddings"], axis=1), 1.0, atol=1e-5)
     with open(os.path.join(tmp, "db_summary.json")) as f:
         s = json.load(f)

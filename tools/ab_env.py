@@ -1,7 +1,7 @@
-"""Interleaved timing of environment-variable variants of libmmf_hip.so's GEMM in ONE process
-(the launchers read MMF_GEMM_* on every call), median over rounds.
+"""Interleaved timing of option variants of libmmf_hip.so's GEMM in ONE process (process options
+set with mmf_set_option on a NULL handle between calls), median over rounds.
 
-    python tools/ab_env.py "MMF_GEMM_GROUPM=0" "MMF_GEMM_GROUPM=8" [--effnet] [--rounds 7]
+    python tools/ab_env.py "gemm_group_m=0" "gemm_group_m=8" [--effnet] [--rounds 7]
 """
 import argparse
 import json
@@ -18,7 +18,7 @@ from tools.gemm_bench import EFFNET, ROUND, SHAPES  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("variants", nargs="+", help="'VAR=value[,VAR2=value]' per variant")
+    ap.add_argument("variants", nargs="+", help="'option=value[,option2=value]' per variant")
     ap.add_argument("--effnet", action="store_true")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
@@ -27,7 +27,7 @@ def main():
     dev = torch.device("cuda")
     shapes = ([(n, M, N, K, act, sc, rs, rpb, "16") for n, M, N, K, act, sc, rs, rpb in EFFNET] if a.effnet else
               [(n, M, N, K, act, 0, 0, 1, out) for n, M, N, K, act, out in SHAPES + ROUND])
-    variants = [dict(kv.split("=", 1) for kv in v.split(",")) for v in a.variants]
+    variants = [{k: int(x) for k, x in (kv.split("=", 1) for kv in v.split(","))} for v in a.variants]
     for name, M, N, K, act, sc, rs, rpb, out in shapes:
         A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
@@ -47,9 +47,10 @@ def main():
                                             hip.ptr(c32), hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
         times = [[] for _ in variants]
         for _ in range(a.rounds):
-            for i, env in enumerate(variants):
-                old = {k: os.environ.get(k) for k in env}
-                os.environ.update(env)
+            for i, opts in enumerate(variants):
+                old = {k: hip.get_process_option(k) for k in opts}
+                for k, v in opts.items():
+                    hip.set_process_option(k, v)
                 call()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -59,10 +60,7 @@ def main():
                 torch.cuda.synchronize()
                 times[i].append(e0.elapsed_time(e1) / a.iters * 1e3)
                 for k, v in old.items():
-                    if v is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = v
+                    hip.set_process_option(k, v)
         med = [statistics.median(t) for t in times]
         row = {"shape": name, "M": M, "N": N, "K": K}
         for v, m in zip(a.variants, med):

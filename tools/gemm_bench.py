@@ -1,9 +1,10 @@
 """Micro-benchmark of libmmf_hip's bf16 GEMM on the encoder shapes of the hot path.
 
-    python tools/gemm_bench.py [--configs 3,4,5] [--iters 20]
+    python tools/gemm_bench.py [--configs auto,4,6] [--iters 20] [--round] [--effnet]
 
-Prints TFLOP/s per (shape, tile config) measured with HIP events (torch.cuda.Event on the
-stream the kernel is launched on); MMF_GEMM_CONFIG forces the tile instantiation.
+Prints TFLOP/s (TB/s for the EfficientNet 1x1 convolutions) per (shape, tile config), measured with
+HIP events on the stream the kernel is launched on; the process option "gemm_config"
+(mmf_set_option with a NULL handle) forces the tile instantiation.
 """
 import argparse
 import json
@@ -29,7 +30,6 @@ SHAPES = [
 # one persistent round of 256x256 tiles (256 tiles) at growing K: per-K-step slope vs fixed cost
 ROUND = [("round_k%d" % k, 8192, 2048, k, 0, "16") for k in (256, 512, 768, 1536, 3072, 6144)]
 
-
 # EfficientNet-B0 1x1 convolutions at B=256: (name, M, N, K, act, SE scale, bf16 residual, rows/image)
 EFFNET = [
     ("e2.1", 256 * 12544, 96, 16, 3, 0, 0, 12544), ("e2.2", 256 * 3136, 144, 24, 3, 0, 0, 3136),
@@ -43,6 +43,22 @@ EFFNET = [
 ]
 
 
+def timed_us(call, iters):
+    for _ in range(3):
+        call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def force(cfg):
+    hip.set_process_option("gemm_config", -1 if cfg == "auto" else int(cfg))
+
+
 def effnet(a, lib, dev):
     for name, M, N, K, act, sc, rs, rpb in EFFNET:
         A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
@@ -54,21 +70,12 @@ def effnet(a, lib, dev):
         byts = 2.0 * M * (K + N + (N if rs else 0))
         row = {"shape": name, "M": M, "N": N, "K": K, "MB": round(byts / 1e6, 1)}
         for cfg in a.configs.split(","):
-            os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
-
-            def call():
-                hip.check(lib.mmf_gemm_bf16_ex(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R),
-                                               hip.ptr(S), rpb, C.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
-            call()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                call()
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) / a.iters * 1e3
+            force(cfg)
+            us = timed_us(lambda: hip.check(lib.mmf_gemm_bf16_ex(
+                A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R), hip.ptr(S), rpb, C.data_ptr(), N, M,
+                N, K, act, hip.stream_ptr())), a.iters)
             row[cfg] = f"{us:.1f}us {byts / us / 1e6:.2f}TB/s"
-        os.environ["MMF_GEMM_CONFIG"] = ""
+        force("auto")
         print(json.dumps(row), flush=True)
 
 
@@ -76,110 +83,39 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="auto,3,4,5,6")
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--noout", action="store_true", help="also time each shape with no epilogue stores")
     ap.add_argument("--kscale", default="", help="comma list of K multipliers to time (fixed-cost probe)")
     ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
     ap.add_argument("--round", action="store_true", help="one 256-tile round at K = 256 .. 6144")
-    ap.add_argument("--nodefer", action="store_true", help="also time each config with MMF_GEMM_DEFER=0")
-    ap.add_argument("--env", default="", help="extra timed pass per config with these VAR=VAL[;VAR=VAL] set")
-    ap.add_argument("--probe", default="", help="MMF_GEMM_PROBE bits for an extra timed pass (1: drop bf16 stores)")
+    ap.add_argument("--group-m", default="", help="extra timed pass per config per gemm_group_m value (comma list)")
     a = ap.parse_args()
-    if a.effnet:
-        effnet(a, hip.load(), torch.device("cuda"))
-        return
-    global SHAPES
-    if a.round:
-        SHAPES = ROUND
-    if a.kscale:
-        SHAPES = [(f"{n}_k{m}", M, N, K * int(m), act, out) for n, M, N, K, act, out in SHAPES
-                  for m in a.kscale.split(",")]
     lib = hip.load()
     dev = torch.device("cuda")
-    res = []
-    for name, M, N, K, act, out in SHAPES:
+    if a.effnet:
+        effnet(a, lib, dev)
+        return
+    shapes = ROUND if a.round else SHAPES
+    if a.kscale:
+        shapes = [(f"{n}_k{m}", M, N, K * int(m), act, out) for n, M, N, K, act, out in shapes
+                  for m in a.kscale.split(",")]
+    for name, M, N, K, act, out in shapes:
         A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
         bias = torch.randn(N, device=dev)
         c32 = torch.empty(M, N, device=dev) if "32" in out else None
         c16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if "16" in out else None
-        R = torch.randn(M, N, device=dev) if "r" in out else None
-        row = {"shape": name, "M": M, "N": N, "K": K}
-        for cfg in a.configs.split(","):
-            os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
 
-            def call():
-                hip.check(lib.mmf_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R),
-                                            hip.ptr(c32), hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
-            for _ in range(3):
-                call()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                call()
-            e1.record()
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / a.iters
-            row[cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
-        for spec in [e for e in a.env.split("/") if e]:
-            kv = dict(x.split("=") for x in spec.split(";"))
-            os.environ.update(kv)
+        def call():
+            hip.check(lib.mmf_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None, hip.ptr(c32),
+                                        hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
+        row = {"shape": name, "M": M, "N": N, "K": K}
+        for gm in [""] + [g for g in a.group_m.split(",") if g]:
+            hip.set_process_option("gemm_group_m", int(gm or 0))
             for cfg in a.configs.split(","):
-                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
-                call()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    call()
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / a.iters
-                row[spec + ":" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
-            for k in kv:
-                os.environ[k] = ""
-        if a.probe:
-            os.environ["MMF_GEMM_PROBE"] = a.probe
-            for cfg in a.configs.split(","):
-                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
-                call()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    call()
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / a.iters
-                row["probe_" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
-            os.environ["MMF_GEMM_PROBE"] = ""
-        if a.nodefer:
-            os.environ["MMF_GEMM_DEFER"] = "0"
-            for cfg in a.configs.split(","):
-                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
-                call()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    call()
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / a.iters
-                row["nodefer_" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
-            os.environ["MMF_GEMM_DEFER"] = ""
-        if a.noout:
-            os.environ["MMF_GEMM_NOSTORE"] = "1"
-            for cfg in a.configs.split(","):
-                os.environ["MMF_GEMM_CONFIG"] = "" if cfg == "auto" else cfg
-                call()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    call()
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / a.iters
-                row["noout_" + cfg] = round(2.0 * M * N * K / (ms / 1e3) / 1e12, 1)
-            os.environ["MMF_GEMM_NOSTORE"] = ""
-        os.environ["MMF_GEMM_CONFIG"] = ""
-        res.append(row)
+                force(cfg)
+                us = timed_us(call, a.iters)
+                row[(f"gm{gm}:" if gm else "") + cfg] = round(2.0 * M * N * K / (us / 1e6) / 1e12, 1)
+        hip.set_process_option("gemm_group_m", 0)
+        force("auto")
         print(json.dumps(row), flush=True)
 
 
