@@ -78,15 +78,16 @@ def build_inputs(eng, B, rank, n_vault=2170):
 
 
 def cpu_baseline(seconds: float, batch: int = 256):
-    """Oracle (fp32 PyTorch CPU restatement, test infrastructure) on bounded samples, all of this
-    process's affinity cores:
+    """Oracle (fp32 PyTorch CPU restatement, test infrastructure) on bounded samples, all of the
+    host cores this process may use (affinity, capped by the cgroup CPU quota):
     (i) reference-faithful per-pair analyze() (B=1, ViT twice, numpy vault renormalised per call);
     (ii) batched (B up to 256, ViT once, vault normalised once), the best a CPU port could do."""
     from oracle import pipeline as P
     import mmf_amd.synthetic as syn
     import mmf_amd.weights as W
-    cores = len(os.sched_getaffinity(0))
+    cores = benchrun.usable_cpus()
     torch.set_num_threads(cores)
+    benchrun.progress(f"cpu baseline on {cores} threads (affinity {len(os.sched_getaffinity(0))})")
     det, clip = W.synthetic_detector_state(0), W.synthetic_clip_state(0)
     n = 64
     rid, rm = syn.roberta_ids(max(n, batch), 128, 7)
@@ -104,6 +105,7 @@ def cpu_baseline(seconds: float, batch: int = 256):
             done += 1
         dt = time.perf_counter() - t0
         per_pair = dt / done
+        benchrun.progress(f"cpu mode (i): {done} pairs in {dt:.1f} s")
         # batched mode: bounded to ~20 s from the per-pair time (a batch runs ~2x more efficiently)
         b2 = int(min(batch, max(8, 20.0 / (0.5 * per_pair))))
         t1 = time.perf_counter()
@@ -126,6 +128,7 @@ def config_lines(eng, t, steps, warmup, det):
     lib, h, dev = eng.lib, eng.h, eng.device
     out = {}
     B = t["rid"].shape[0]
+    benchrun.progress("configs[1..3]")
     # configs[1]: RoBERTa-base dual-head text-only forward, L=128, B=256
     ai, mi, sc = (torch.empty(B, 2, device=dev) for _ in range(3))
 
@@ -181,11 +184,13 @@ def main():
     from mmf_amd.engine import Engine
 
     B = a.batch
+    benchrun.progress(f"rank {rank}/{world}: building the engine")
     det = W.synthetic_detector_state(0)
     eng = Engine(local, det, W.synthetic_clip_state(0), max_batch=B)
     t = build_inputs(eng, B, rank)
     sync = torch.cuda.synchronize
 
+    benchrun.progress("timed region: PCIe-inclusive (headline)")
     # headline: inputs from pinned host memory every step, results back to the host
     host = {k: v.cpu().pin_memory() for k, v in t.items()}
     pipe = eng.host_pipeline(B, host["rid"].shape[1], host["cid"].shape[1])
@@ -193,6 +198,7 @@ def main():
     value = benchrun.whole_job_rate(world, B, a.steps, dt)
     h2d = sum(v.numel() * v.element_size() for v in host.values())
 
+    benchrun.progress(f"headline {value:.1f} pairs/s; timed region: HBM-resident")
     # secondary: inputs already resident in HBM
     out = eng.alloc_outputs(B)
 
@@ -203,6 +209,7 @@ def main():
 
     roofline = None
     if not a.no_profile:
+        benchrun.progress("per-kernel event-timed pass")
         from mmf_amd.profiling import kernel_roofline
         roofline = kernel_roofline(eng, step, a.steps)
     configs = None
@@ -215,7 +222,7 @@ def main():
         res = {"metric": "text+image pairs/sec through full analyze() 5-signal path, batch=256",
                "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
                "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
                "data": "synthetic (seeded token ids, structured uint8 images, 2170-row vault); random-init weights",
                "config": {"workload": "Full MisinfoForensics.analyze() 5-signal pipeline incl. Truth-Vault lookup "
                                       "(BASELINE configs[4]), text L=128, caption L=77, 224x224 images; inputs H2D "

@@ -52,7 +52,7 @@ const char* mmf_version(void);
  * load_state_dict (misinfo_forensics.py:175-186, 260-317); the data are copied. */
 int mmf_load_tensor(mmf_handle* h, const char* name, int dtype, int ndim, const int64_t* shape,
                     const void* host_data);
-/* Pack staged tensors into device layouts (fused QKV, BatchNorm folded into convs, bf16 GEMM
+/* Pack staged tensors into device layouts (fused QKV, BatchNorm folded into convs, fp16 GEMM
  * operands).  Components whose tensors are all present become available; `clip_eos_token_id`
  * selects the HF EOS-pooling rule (2 = argmax(ids), else first index of that id;
  * TF clip:561-582). */
@@ -158,20 +158,20 @@ int mmf_get_option(mmf_handle* h, const char* name, int* value);
 int64_t mmf_device_bytes(mmf_handle* h);
 
 /* Low-level op exported for unit tests of the GEMM kernel: C = act(A @ W^T + bias) + residual.
- * A bf16 [M,K] (lda), W bf16 [N,K] (ldw), bias fp32 [N] or NULL, residual fp32 [M,N] (ldc) or NULL,
- * act 0 none 1 gelu-erf 2 quick_gelu 3 silu 4 relu; outputs fp32 (c32) and/or bf16 (c16) [M,N] ldc. */
-int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual,
+ * A fp16 [M,K] (lda), W fp16 [N,K] (ldw), bias fp32 [N] or NULL, residual fp32 [M,N] (ldc) or NULL,
+ * act 0 none 1 gelu-erf 2 quick_gelu 3 silu 4 relu; outputs fp32 (c32) and/or fp16 (c16) [M,N] ldc. */
+int mmf_gemm_f16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual,
                   float* c32, void* c16, int ldc, int M, int N, int K, int act, void* stream);
 
-/* The same with the EfficientNet operands of the 1x1 convolutions: bf16 residual res16 [M,N] (ldc)
+/* The same with the EfficientNet operands of the 1x1 convolutions: fp16 residual res16 [M,N] (ldc)
  * and a per-(image, k) fp32 scale ascale [M / rows_per_batch, K] applied to A (SE excitation). */
-int mmf_gemm_bf16_ex(const void* A, int lda, const void* W, int ldw, const float* bias, const void* res16,
+int mmf_gemm_f16_ex(const void* A, int lda, const void* W, int ldw, const float* bias, const void* res16,
                      const float* ascale, int rows_per_batch, void* c16, int ldc, int M, int N, int K, int act,
                      void* stream);
 
-/* Low-level attention op for tests: qkv bf16 [B*L, 3*H*64] (q|k|v), mask int32 [B,L] or NULL,
- * causal 0/1 -> out bf16 [B*L, H*64].  L <= 512. */
-int mmf_attention_bf16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,
+/* Low-level attention op for tests: qkv fp16 [B*L, 3*H*64] (q|k|v), mask int32 [B,L] or NULL,
+ * causal 0/1 -> out fp16 [B*L, H*64].  L <= 512. */
+int mmf_attention_f16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,
                        void* stream);
 
 #ifdef __cplusplus

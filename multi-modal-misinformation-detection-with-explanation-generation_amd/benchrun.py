@@ -9,7 +9,9 @@ the MAX over ranks (one all_reduce of one float) -- the only collective traffic.
 """
 from __future__ import annotations
 
+import math
 import os
+import sys
 import time
 from typing import Callable, Optional
 
@@ -73,3 +75,34 @@ def max_over_ranks(x: float, dist=None, device: Optional[torch.device] = None) -
 def whole_job_rate(world: int, units_per_rank_step: int, steps: int, seconds: float) -> float:
     """Units all ranks processed / whole-job time (weak scaling: per-rank work fixed)."""
     return world * units_per_rank_step * steps / seconds
+
+
+def usable_cpus() -> int:
+    """Host cores this process may actually run on: its affinity set, capped by a cgroup CPU quota
+    and by OMP_NUM_THREADS when either is set (a container's share of a large host can show every
+    CPU of the machine in the affinity mask; the GPU pool states its per-GPU share that way)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:  # cgroup v2: "<quota> <period>" or "max <period>"
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                n = min(n, max(1, math.ceil(q / per)))
+        except (OSError, ValueError):
+            pass
+    return n
+
+
+def progress(msg: str) -> None:
+    """One line to stderr per bench phase (the JSON result stays the only stdout line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)

@@ -6,7 +6,7 @@
 // One workgroup (4 waves) per (sequence, head).  K and V of the whole head live in LDS row-major
 // ([key][64], 16-B chunks XOR-swizzled by key & 7, both staged with 16-B stores); each wave takes
 // 16-query tiles:
-//   S^T = K Q^T (v_mfma_f32_16x16x32_bf16 with K as the A operand, Q fragments straight from
+//   S^T = K Q^T (v_mfma_f32_16x16x32_f16 with K as the A operand, Q fragments straight from
 //         global/L2): each lane ends with 4 consecutive KEYS of one query
 //   fp32 masked softmax in registers (a query's keys sit in 4 lanes -> 2 xor-shuffles)
 //   O^T = V^T P^T with P^T taken straight from the softmax registers as the MFMA B operand: the
@@ -30,17 +30,17 @@ MMF_DEV int kv_swz(int key, int kc) { return key * 64 + ((kc ^ (key & 7)) << 3);
 // key-tile loops carry no runtime bounds: the K-fragment reads of a query tile batch up ahead of
 // its MFMAs instead of sitting in one basic block per key tile.
 template <int LK>
-__global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restrict__ qkv, int ld,
-                                                        const int32_t* __restrict__ mask, bf16_t* __restrict__ out,
+__global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restrict__ qkv, int ld,
+                                                        const int32_t* __restrict__ mask, f16_t* __restrict__ out,
                                                         int ldo, int L, int H, int causal) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[LK * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[LK * 64];
+  __shared__ __attribute__((aligned(16))) f16_t Ks[LK * 64];
+  __shared__ __attribute__((aligned(16))) f16_t Vs[LK * 64];
   __shared__ __attribute__((aligned(16))) float kbias[LK];
 
   const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
   const int D = H * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bf16_t* base = qkv + (size_t)bi * L * ld;
+  const f16_t* base = qkv + (size_t)bi * L * ld;
 
   const int fr = lane & 15, fg = lane >> 4;
   const int nqt = (L + 15) >> 4;
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
     }
   }
   // Q fragments: row q = qt*16 + fr, dims 32*ks + 8*fg .. +7, for qt = wave + 4*it
-  bf16x8 qfa[NQT][2];
+  f16x8 qfa[NQT][2];
 #pragma unroll
   for (int it = 0; it < NQT; ++it) {
     const int q = (wave + 4 * it) * 16 + fr;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
     for (int ks = 0; ks < 2; ++ks) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (q < L) v = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + h * 64 + ks * 32 + fg * 8);
-      qfa[it][ks] = as_bf16x8(v);
+      qfa[it][ks] = as_f16x8(v);
     }
   }
 #pragma unroll
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
   __syncthreads();
 
   static_assert(NQT == 2, "two query tiles per wave");
-  bf16x8 qf[2] = {qfa[0][0], qfa[0][1]};
+  f16x8 qf[2] = {qfa[0][0], qfa[0][1]};
 #pragma unroll 1
   for (int it = 0; it < NQT; ++it) {
     const int qt = wave + 4 * it;
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int key = j * 16 + fr, kc = ks * 4 + fg;
-        const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
+        const f16x8 kf = as_f16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
         s[j] = mfma16x16x32(kf, qf[ks], s[j]);
       }
     }
@@ -138,11 +138,11 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
 #pragma unroll
     for (int kb = 0; kb < LK / 32; ++kb) {
       {
-        const uint4 pk = make_uint4(pack2bf(s[2 * kb][0] * inv, s[2 * kb][1] * inv),
-                                    pack2bf(s[2 * kb][2] * inv, s[2 * kb][3] * inv),
-                                    pack2bf(s[2 * kb + 1][0] * inv, s[2 * kb + 1][1] * inv),
-                                    pack2bf(s[2 * kb + 1][2] * inv, s[2 * kb + 1][3] * inv));
-        const bf16x8 pf = as_bf16x8(pk);
+        const uint4 pk = make_uint4(pack2h(s[2 * kb][0] * inv, s[2 * kb][1] * inv),
+                                    pack2h(s[2 * kb][2] * inv, s[2 * kb][3] * inv),
+                                    pack2h(s[2 * kb + 1][0] * inv, s[2 * kb + 1][1] * inv),
+                                    pack2h(s[2 * kb + 1][2] * inv, s[2 * kb + 1][3] * inv));
+        const f16x8 pf = as_f16x8(pk);
         // A operand V^T[d = dt*16 + fr][keys 32kb + 4fg + 0..3 | 32kb + 16 + 4fg + 0..3]: lane
         // 4q + p of each 16-lane group addresses key row (.. + q), dims dt*16 + 4p .. +3
         const int key0 = kb * 32 + fg * 4 + (fr >> 2), p = fr & 3;
@@ -152,16 +152,16 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
           const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + kv_swz(key0, c) + e));
           const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + kv_swz(key0 + 16, c) + e));
           const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
-          o[dt] = mfma16x16x32(as_bf16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
+          o[dt] = mfma16x16x32(as_f16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
         }
       }
     }
     if (qq < L) {
-      bf16_t* dst = out + ((size_t)bi * L + qq) * ldo + h * 64 + fg * 4;
+      f16_t* dst = out + ((size_t)bi * L + qq) * ldo + h * 64 + fg * 4;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         *reinterpret_cast<uint2*>(dst + dt * 16) =
-            make_uint2(pack2bf(o[dt][0], o[dt][1]), pack2bf(o[dt][2], o[dt][3]));
+            make_uint2(pack2h(o[dt][0], o[dt][1]), pack2h(o[dt][2], o[dt][3]));
     }
     qf[0] = qfa[1][0];
     qf[1] = qfa[1][1];
@@ -172,23 +172,23 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const bf16_t* __restr
 // head's K and V (up to 2 x 64 KB) stay resident in LDS (one workgroup per CU) and each 16-query
 // tile walks the keys in 128-key chunks with an online softmax (running max / sum per query, O
 // rescaled when the max grows).  The S^T / P^T-in-registers / transposed-V formulation is the one
-// of attention_kernel above; P is rounded to bf16 unnormalised (<= 1) and O divided by the sum at
+// of attention_kernel above; P is rounded to fp16 unnormalised (<= 1) and O divided by the sum at
 // the end.
 constexpr int LLONG = 512, KCH = 128;
 
-__global__ __launch_bounds__(256) void attention_long_kernel(const bf16_t* __restrict__ qkv, int ld,
+__global__ __launch_bounds__(256) void attention_long_kernel(const f16_t* __restrict__ qkv, int ld,
                                                              const int32_t* __restrict__ mask,
-                                                             bf16_t* __restrict__ out, int ldo, int L, int H,
+                                                             f16_t* __restrict__ out, int ldo, int L, int H,
                                                              int causal) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[LLONG * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[LLONG * 64];
+  __shared__ __attribute__((aligned(16))) f16_t Ks[LLONG * 64];
+  __shared__ __attribute__((aligned(16))) f16_t Vs[LLONG * 64];
   __shared__ __attribute__((aligned(16))) float kbias[LLONG];
 
   const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
   const int D = H * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Lk = (L + 31) & ~31;
-  const bf16_t* base = qkv + (size_t)bi * L * ld;
+  const f16_t* base = qkv + (size_t)bi * L * ld;
   const int fr = lane & 15, fg = lane >> 4;
   const int nqt = (L + 15) >> 4;
 
@@ -221,12 +221,12 @@ __global__ __launch_bounds__(256) void attention_long_kernel(const bf16_t* __res
 #pragma unroll 1
   for (int qt = wave; qt < nqt; qt += 4) {
     const int qq = qt * 16 + fr;
-    bf16x8 qf[2];
+    f16x8 qf[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (qq < L) v = *reinterpret_cast<const uint4*>(base + (size_t)qq * ld + h * 64 + ks * 32 + fg * 8);
-      qf[ks] = as_bf16x8(v);
+      qf[ks] = as_f16x8(v);
     }
     float m = -INFINITY, sum = 0.f;
     f32x4 o[4];
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void attention_long_kernel(const bf16_t* __res
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
             const int key = k0 + j * 16 + fr, kc = ks * 4 + fg;
-            const bf16x8 kf = as_bf16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
+            const f16x8 kf = as_f16x8(*reinterpret_cast<const uint4*>(Ks + kv_swz(key, kc)));
             s[j] = mfma16x16x32(kf, qf[ks], s[j]);
           }
         }
@@ -290,10 +290,10 @@ __global__ __launch_bounds__(256) void attention_long_kernel(const bf16_t* __res
 #pragma unroll
       for (int kb = 0; kb < KCH / 32; ++kb) {
         if (2 * kb < nkt) {
-          const uint4 pk = make_uint4(pack2bf(s[2 * kb][0], s[2 * kb][1]), pack2bf(s[2 * kb][2], s[2 * kb][3]),
-                                      pack2bf(s[2 * kb + 1][0], s[2 * kb + 1][1]),
-                                      pack2bf(s[2 * kb + 1][2], s[2 * kb + 1][3]));
-          const bf16x8 pf = as_bf16x8(pk);
+          const uint4 pk = make_uint4(pack2h(s[2 * kb][0], s[2 * kb][1]), pack2h(s[2 * kb][2], s[2 * kb][3]),
+                                      pack2h(s[2 * kb + 1][0], s[2 * kb + 1][1]),
+                                      pack2h(s[2 * kb + 1][2], s[2 * kb + 1][3]));
+          const f16x8 pf = as_f16x8(pk);
           const int key0 = k0 + kb * 32 + fg * 4 + (fr >> 2), p = fr & 3;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) {
@@ -302,25 +302,25 @@ __global__ __launch_bounds__(256) void attention_long_kernel(const bf16_t* __res
             const i16x4 hi =
                 __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + kv_swz(key0 + 16, c) + e));
             const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
-            o[dt] = mfma16x16x32(as_bf16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
+            o[dt] = mfma16x16x32(as_f16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
           }
         }
       }
     }
     if (qq < L) {
       const float inv = sum > 0.f ? 1.0f / sum : 0.f;
-      bf16_t* dst = out + ((size_t)bi * L + qq) * ldo + h * 64 + fg * 4;
+      f16_t* dst = out + ((size_t)bi * L + qq) * ldo + h * 64 + fg * 4;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         *reinterpret_cast<uint2*>(dst + dt * 16) =
-            make_uint2(pack2bf(o[dt][0] * inv, o[dt][1] * inv), pack2bf(o[dt][2] * inv, o[dt][3] * inv));
+            make_uint2(pack2h(o[dt][0] * inv, o[dt][1] * inv), pack2h(o[dt][2] * inv, o[dt][3] * inv));
     }
   }
 }
 
 }  // namespace
 
-hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, bf16_t* out, int ldo, int B, int L,
+hipError_t launch_attention(const f16_t* qkv, int ldqkv, const int32_t* mask, f16_t* out, int ldo, int B, int L,
                             int H, int causal, hipStream_t s) {
   if (L <= 0 || L > LLONG || (ldqkv & 7) || (ldo & 3)) return hipErrorInvalidValue;
   if (L > LMAX) {

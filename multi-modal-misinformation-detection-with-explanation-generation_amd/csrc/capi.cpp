@@ -40,12 +40,12 @@ int fail(int code, const char* fmt, ...) {
     if (r_ != 0) return r_;  \
   } while (0)
 
-uint16_t f2bf_host(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+// float -> IEEE fp16 bits, round-to-nearest-even (the compiler's _Float16 conversion)
+uint16_t f2h_host(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t b;
+  std::memcpy(&b, &h, 2);
+  return b;
 }
 
 struct HostT {
@@ -54,7 +54,7 @@ struct HostT {
   size_t numel() const { return f.size(); }
 };
 
-struct Lin16 { bf16_t* w = nullptr; float* b = nullptr; int out = 0, in = 0; };
+struct Lin16 { f16_t* w = nullptr; float* b = nullptr; int out = 0, in = 0; };
 struct LNp { float* g = nullptr; float* b = nullptr; };
 struct EncLayer { Lin16 qkv, o, fc1, fc2; LNp ln1, ln2; };
 
@@ -73,17 +73,17 @@ struct Workspace {
   // RoBERTa
   float *r_x = nullptr, *r_y = nullptr;
   uint16_t* r_lo = nullptr;  // fp16 low part of the split post-LN residual stream (hi = r_xb)
-  bf16_t *r_xb = nullptr, *r_qkv = nullptr, *r_ctx = nullptr, *r_h = nullptr;
+  f16_t *r_xb = nullptr, *r_qkv = nullptr, *r_ctx = nullptr, *r_h = nullptr;
   // CLIP vision
-  bf16_t *v_col = nullptr, *v_xb = nullptr, *v_qkv = nullptr, *v_ctx = nullptr, *v_h = nullptr, *v_cls = nullptr;
+  f16_t *v_col = nullptr, *v_xb = nullptr, *v_qkv = nullptr, *v_ctx = nullptr, *v_h = nullptr, *v_cls = nullptr;
   float *v_patch = nullptr, *v_x = nullptr, *v_emb = nullptr, *v_xc = nullptr;
-  bf16_t* v_ctxc = nullptr;
+  f16_t* v_ctxc = nullptr;
   // CLIP text
-  bf16_t *t_xb = nullptr, *t_qkv = nullptr, *t_ctx = nullptr, *t_h = nullptr, *t_pool = nullptr, *t_ctxc = nullptr;
+  f16_t *t_xb = nullptr, *t_qkv = nullptr, *t_ctx = nullptr, *t_h = nullptr, *t_pool = nullptr, *t_ctxc = nullptr;
   float *t_x = nullptr, *t_emb = nullptr, *t_xc = nullptr;
   int32_t* t_eos = nullptr;
   // EfficientNet
-  bf16_t *e_a = nullptr, *e_b = nullptr, *e_exp = nullptr, *e_dw = nullptr;
+  f16_t *e_a = nullptr, *e_b = nullptr, *e_exp = nullptr, *e_dw = nullptr;
   float *e_pool = nullptr, *e_scale = nullptr;
   // split-K partials of the skinny-M GEMMs, one per tower (the towers run on concurrent streams)
   float *sk_text = nullptr, *sk_vit = nullptr, *sk_ctext = nullptr;
@@ -157,16 +157,16 @@ struct mmf_handle {
   Lin16 e_head;
   float *e_cls_w = nullptr, *e_cls_b = nullptr;
   // CLIP vision
-  bf16_t* v_patch_w = nullptr;
+  f16_t* v_patch_w = nullptr;
   float *v_cls = nullptr, *v_pos = nullptr;
   LNp v_pre, v_post;
   EncLayer v_layers[12];
-  bf16_t* v_proj = nullptr;
+  f16_t* v_proj = nullptr;
   // CLIP text
   float *t_tok = nullptr, *t_pos = nullptr;
   EncLayer t_layers[12];
   LNp t_final;
-  bf16_t* t_proj = nullptr;
+  f16_t* t_proj = nullptr;
   // fusion
   float *f_w0 = nullptr, *f_b0 = nullptr, *f_w3 = nullptr, *f_b3 = nullptr, *f_w5 = nullptr, *f_b5 = nullptr;
   // vault
@@ -270,9 +270,9 @@ int upload(mmf_handle* h, T** dst, const std::vector<T>& v) {
 }
 
 int up_f32(mmf_handle* h, float** dst, const std::vector<float>& v) { return upload(h, dst, v); }
-int up_bf16(mmf_handle* h, bf16_t** dst, const std::vector<float>& v) {
+int up_f16(mmf_handle* h, f16_t** dst, const std::vector<float>& v) {
   std::vector<uint16_t> b(v.size());
-  for (size_t i = 0; i < v.size(); ++i) b[i] = f2bf_host(v[i]);
+  for (size_t i = 0; i < v.size(); ++i) b[i] = f2h_host(v[i]);
   return upload(h, dst, b);
 }
 
@@ -304,7 +304,7 @@ int load_ln(mmf_handle* h, LNp* ln, const std::string& p, int n) {
 }
 int load_lin(mmf_handle* h, Lin16* l, const std::string& p, int out, int in, bool bias) {
   GET(w, p + ".weight", (size_t)out * in);
-  CHK(up_bf16(h, &l->w, w->f));
+  CHK(up_f16(h, &l->w, w->f));
   if (bias) CHK(load_f32(h, &l->b, p + ".bias", out));
   l->out = out;
   l->in = in;
@@ -320,7 +320,7 @@ int load_qkv(mmf_handle* h, Lin16* l, const std::string& q, const std::string& k
     std::memcpy(w.data() + (size_t)i * H * H, tw->f.data(), sizeof(float) * H * H);
     std::memcpy(b.data() + (size_t)i * H, tb->f.data(), sizeof(float) * H);
   }
-  CHK(up_bf16(h, &l->w, w));
+  CHK(up_f16(h, &l->w, w));
   CHK(up_f32(h, &l->b, b));
   l->out = 3 * H;
   l->in = H;
@@ -407,7 +407,7 @@ int finalize_effnet(mmf_handle* h) {
       int i = 0;
       if (B.expand != 1) {
         CHK(fold_bn(h, bp + "0.0", bp + "0.1", B.cexp, B.cin, &w, &b));
-        CHK(up_bf16(h, &B.e.w, w));
+        CHK(up_f16(h, &B.e.w, w));
         CHK(up_f32(h, &B.e.b, b));
         B.e.out = B.cexp;
         B.e.in = B.cin;
@@ -425,7 +425,7 @@ int finalize_effnet(mmf_handle* h) {
       }
       CHK(load_f32(h, &B.b2, se + "fc2.bias", B.cexp));
       CHK(fold_bn(h, bp + std::to_string(i + 2) + ".0", bp + std::to_string(i + 2) + ".1", B.cout, B.cexp, &w, &b));
-      CHK(up_bf16(h, &B.p.w, w));
+      CHK(up_f16(h, &B.p.w, w));
       CHK(up_f32(h, &B.p.b, b));
       B.p.out = B.cout;
       B.p.in = B.cexp;
@@ -433,7 +433,7 @@ int finalize_effnet(mmf_handle* h) {
     }
   }
   CHK(fold_bn(h, p + "8.0", p + "8.1", 1280, 320, &w, &b));
-  CHK(up_bf16(h, &h->e_head.w, w));
+  CHK(up_f16(h, &h->e_head.w, w));
   CHK(up_f32(h, &h->e_head.b, b));
   h->e_head.out = 1280;
   h->e_head.in = 320;
@@ -460,7 +460,7 @@ int finalize_clip_vision(mmf_handle* h) {
   const std::string p = "clip.vision_model.";
   {
     GET(w, p + "embeddings.patch_embedding.weight", (size_t)768 * 3072);
-    CHK(up_bf16(h, &h->v_patch_w, w->f));  // [768][3*32*32] = (c, ky, kx) columns
+    CHK(up_f16(h, &h->v_patch_w, w->f));  // [768][3*32*32] = (c, ky, kx) columns
   }
   CHK(load_f32(h, &h->v_cls, p + "embeddings.class_embedding", 768));
   CHK(load_f32(h, &h->v_pos, p + "embeddings.position_embedding.weight", 50 * 768));
@@ -468,7 +468,7 @@ int finalize_clip_vision(mmf_handle* h) {
   CHK(finalize_clip_layers(h, h->v_layers, p + "encoder.layers.", 768, 3072));
   CHK(load_ln(h, &h->v_post, p + "post_layernorm", 768));
   GET(pw, "clip.visual_projection.weight", (size_t)512 * 768);
-  return up_bf16(h, &h->v_proj, pw->f);
+  return up_f16(h, &h->v_proj, pw->f);
 }
 
 int finalize_clip_text(mmf_handle* h) {
@@ -478,7 +478,7 @@ int finalize_clip_text(mmf_handle* h) {
   CHK(finalize_clip_layers(h, h->t_layers, p + "encoder.layers.", 512, 2048));
   CHK(load_ln(h, &h->t_final, p + "final_layer_norm", 512));
   GET(pw, "clip.text_projection.weight", (size_t)512 * 512);
-  return up_bf16(h, &h->t_proj, pw->f);
+  return up_f16(h, &h->t_proj, pw->f);
 }
 
 int finalize_fusion(mmf_handle* h) {
@@ -493,7 +493,7 @@ int finalize_fusion(mmf_handle* h) {
 // ---------------------------------------------------------------------------------------------
 // forward sequences
 // ---------------------------------------------------------------------------------------------
-GemmArgs gemm_args(const bf16_t* A, int lda, const Lin16& l, int M) {
+GemmArgs gemm_args(const f16_t* A, int lda, const Lin16& l, int M) {
   GemmArgs g{};
   g.A = A;
   g.lda = lda;
@@ -523,28 +523,28 @@ int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   return 0;
 }
 
-int attn(mmf_handle* h, const bf16_t* qkv, int ld, const int32_t* mask, bf16_t* out, int ldo, int B, int L, int H,
+int attn(mmf_handle* h, const f16_t* qkv, int ld, const int32_t* mask, f16_t* out, int ldo, int B, int L, int H,
          int causal, hipStream_t s) {
   ProfScope ps(h, s, PK_ATTN, 4.0 * B * H * (double)L * L * 64, (double)B * L * H * 64 * 2 * 4);
   HIPCHK(launch_attention(qkv, ld, mask, out, ldo, B, L, H, causal, s));
   return 0;
 }
 
-int lnorm(mmf_handle* h, const float* x, int ldx, const LNp& p, float* y32, int ldy32, bf16_t* y16, int ldy16,
+int lnorm(mmf_handle* h, const float* x, int ldx, const LNp& p, float* y32, int ldy32, f16_t* y16, int ldy16,
           int rows, int C, hipStream_t s) {
   ProfScope ps(h, s, PK_LN, 8.0 * rows * C, (double)rows * C * (4 + (y32 ? 4 : 0) + (y16 ? 2 : 0)));
   HIPCHK(launch_layernorm(x, ldx, nullptr, 0, p.g, p.b, 1e-5f, y32, ldy32, y16, ldy16, rows, C, s));
   return 0;
 }
 
-int add_ln(mmf_handle* h, float* x, int ldx, const bf16_t* y, int ldy, const LNp& p, float* s32, float* o32,
-           bf16_t* o16, int ldo, int rows, int C, hipStream_t s) {
+int add_ln(mmf_handle* h, float* x, int ldx, const f16_t* y, int ldy, const LNp& p, float* s32, float* o32,
+           f16_t* o16, int ldo, int rows, int C, hipStream_t s) {
   ProfScope ps(h, s, PK_LN, 9.0 * rows * C, (double)rows * C * (4 + 2 + (s32 ? 4 : 0) + (o32 ? 4 : 0) + 2));
   HIPCHK(launch_add_ln(x, ldx, y, ldy, p.g, p.b, 1e-5f, s32, o32, o16, ldo, rows, C, s));
   return 0;
 }
 
-int add_ln_hilo(mmf_handle* h, bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy, const LNp& p, int rows,
+int add_ln_hilo(mmf_handle* h, f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const LNp& p, int rows,
                 hipStream_t s) {
   ProfScope ps(h, s, PK_LN, 9.0 * rows * 768, (double)rows * 768 * (2 + 2 + 2 + 2 + 2));
   HIPCHK(launch_add_ln_hilo(hi, lo, ld, y, ldy, p.g, p.b, 1e-5f, rows, 768, s));
@@ -578,9 +578,9 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
     // run on B compact CLS rows (strided A / residual reads) instead of B*L rows
     const bool last = (i == 11);
     if (!last) {
-      // out-proj and FFN-2 write their bf16 branch output y; the residual add happens in fp32
+      // out-proj and FFN-2 write their fp16 branch output y; the residual add happens in fp32
       // inside add+LN (y lives in r_h, free until FFN-1, then in r_ctx, free after out-proj)
-      bf16_t* y = w.r_h;
+      f16_t* y = w.r_h;
       g = gemm_args(w.r_ctx, 768, Ly.o, M);
       g.c16 = y;
       CHK(gemm(h, g, s));
@@ -626,10 +626,10 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
 // pre-LN CLIP encoder over x (fp32 residual, in place) with xb = LN1_0(x) already computed
 // Only one row per sequence is consumed after the last layer (CLS for the ViT, EOS for the text
 // tower: TF clip:561-582, 650-651): the last layer's out-proj / MLP run on those B rows, gathered
-// into compact buffers (xc fp32, ctxc bf16); on return xc holds them (before the final LN).
-int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, bf16_t* xb, bf16_t* qkv,
-                     bf16_t* ctx, bf16_t* hid, const int32_t* mask, int causal, int B, int L,
-                     const int32_t* last_rows, float* xc, bf16_t* ctxc, float* skws, size_t sk_elems,
+// into compact buffers (xc fp32, ctxc fp16); on return xc holds them (before the final LN).
+int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, f16_t* xb, f16_t* qkv,
+                     f16_t* ctx, f16_t* hid, const int32_t* mask, int causal, int B, int L,
+                     const int32_t* last_rows, float* xc, f16_t* ctxc, float* skws, size_t sk_elems,
                      hipStream_t s) {
   const int M = B * L;
   for (int i = 0; i < 12; ++i) {
@@ -655,7 +655,7 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
       CHK(gemm(h, g, s));
       break;
     }
-    // out-proj / FFN-2 write their bf16 branch output y (out-proj into `hid`, free until FFN-1;
+    // out-proj / FFN-2 write their fp16 branch output y (out-proj into `hid`, free until FFN-1;
     // FFN-2 into `ctx`, free after out-proj); add+LN adds it to the fp32 residual stream x in place
     g = gemm_args(ctx, H, Ly.o, M);
     g.c16 = hid;
@@ -731,8 +731,8 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
 int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score, int score_stride,
                hipStream_t s) {
   Workspace& w = h->ws;
-  bf16_t* cur = w.e_a;
-  bf16_t* nxt = w.e_b;
+  f16_t* cur = w.e_a;
+  f16_t* nxt = w.e_b;
   // option fuse_stem = 0: separate stem launch + stage-1 depthwise (A/B and parity tests)
   const EffBlock& b0 = h->e_blocks.front();
   const bool fuse_stem = h->opt.fuse_stem && b0.expand == 1 && b0.cexp == 32 && b0.k == 3 && b0.stride == 1;
@@ -743,7 +743,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
   }
   int H = 112, W = 112;
   for (const EffBlock& b : h->e_blocks) {
-    const bf16_t* src = cur;
+    const f16_t* src = cur;
     int nch = 0;
     const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
     // option fuse_expand = 0: separate expand launch (A/B)
@@ -778,7 +778,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
     if (b.residual) g.res16 = cur;
     g.c16 = nxt;
     CHK(gemm(h, g, s));
-    bf16_t* t = cur;
+    f16_t* t = cur;
     cur = nxt;
     nxt = t;
     H = Ho;
@@ -1231,18 +1231,18 @@ int64_t mmf_device_bytes(mmf_handle* h) {
   return t;
 }
 
-int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual, float* c32,
+int mmf_gemm_f16(const void* A, int lda, const void* W, int ldw, const float* bias, const float* residual, float* c32,
                   void* c16, int ldc, int M, int N, int K, int act, void* stream) {
   GemmArgs g{};
-  g.A = (const bf16_t*)A;
+  g.A = (const f16_t*)A;
   g.lda = lda;
-  g.W = (const bf16_t*)W;
+  g.W = (const f16_t*)W;
   g.ldw = ldw;
   g.bias = bias;
   g.res32 = residual;
   g.ldr = ldc;
   g.c32 = c32;
-  g.c16 = (bf16_t*)c16;
+  g.c16 = (f16_t*)c16;
   g.ldc = ldc;
   g.M = M;
   g.N = N;
@@ -1255,20 +1255,20 @@ int mmf_gemm_bf16(const void* A, int lda, const void* W, int ldw, const float* b
   return 0;
 }
 
-int mmf_gemm_bf16_ex(const void* A, int lda, const void* W, int ldw, const float* bias, const void* res16,
+int mmf_gemm_f16_ex(const void* A, int lda, const void* W, int ldw, const float* bias, const void* res16,
                      const float* ascale, int rows_per_batch, void* c16, int ldc, int M, int N, int K, int act,
                      void* stream) {
   GemmArgs g{};
-  g.A = (const bf16_t*)A;
+  g.A = (const f16_t*)A;
   g.lda = lda;
-  g.W = (const bf16_t*)W;
+  g.W = (const f16_t*)W;
   g.ldw = ldw;
   g.bias = bias;
-  g.res16 = (const bf16_t*)res16;
+  g.res16 = (const f16_t*)res16;
   g.ldr = ldc;
   g.ascale = ascale;
   g.rows_per_batch = rows_per_batch;
-  g.c16 = (bf16_t*)c16;
+  g.c16 = (f16_t*)c16;
   g.ldc = ldc;
   g.M = M;
   g.N = N;
@@ -1282,10 +1282,10 @@ int mmf_gemm_bf16_ex(const void* A, int lda, const void* W, int ldw, const float
   return 0;
 }
 
-int mmf_attention_bf16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,
+int mmf_attention_f16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,
                        void* stream) {
   if (!qkv || !out) return fail(MMF_EINVAL, "null argument");
-  hipError_t e = launch_attention((const bf16_t*)qkv, 3 * H * 64, mask, (bf16_t*)out, H * 64, B, L, H, causal,
+  hipError_t e = launch_attention((const f16_t*)qkv, 3 * H * 64, mask, (f16_t*)out, H * 64, B, L, H, causal,
                                   (hipStream_t)stream);
   if (e != hipSuccess) return fail(MMF_EIO, "attention: %s", hipGetErrorString(e));
   return 0;

@@ -1,5 +1,5 @@
 // EfficientNet-B0 (torchvision spec, eval) pieces that are not 1x1 convolutions.  Activations are
-// NHWC bf16 so channels are the contiguous, coalesced axis; every BatchNorm is folded into the
+// NHWC fp16 so channels are the contiguous, coalesced axis; every BatchNorm is folded into the
 // preceding convolution's weights/bias at load time (mmf_finalize).  These kernels are HBM-bound
 // (SURVEY.md §8d): each reads its input once and writes its output once.
 //   stem      uint8 HWC -> ImageNet normalise -> conv3x3 s2 (3->32) + BN + SiLU
@@ -18,7 +18,7 @@ namespace {
 // F32 = true: input is an already-normalised fp32 NCHW tensor (detector.forward_image signature,
 // misinfo_forensics.py:102-104) instead of uint8 HWC pixels.
 template <bool F32>
-__global__ __launch_bounds__(256) void stem_kernel(const void* src, const float* w, const float* bias, bf16_t* out,
+__global__ __launch_bounds__(256) void stem_kernel(const void* src, const float* w, const float* bias, f16_t* out,
                                                    int B) {
   const uint8_t* img = (const uint8_t*)src;
   const float* xf = (const float*)src;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const void* src, const float*
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = act_apply(acc[q * 8 + j], ACT_SILU);
-    dst[q] = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+    dst[q] = make_uint4(pack2h(o[0], o[1]), pack2h(o[2], o[3]), pack2h(o[4], o[5]), pack2h(o[6], o[7]));
   }
 }
 
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const void* src, const float*
 // so the pool partial of a channel stays in one thread and is reduced across px in a fixed order
 // (deterministic, no atomics): one partial per (image, tile, channel).
 template <int K, int S>
-MMF_DEV void dw_compute(const bf16_t* tile, const float* sw, const float* sb, float* red, bf16_t* __restrict__ out,
+MMF_DEV void dw_compute(const f16_t* tile, const float* sw, const float* sb, float* red, f16_t* __restrict__ out,
                         float* __restrict__ pool_part, int bi, int c0, int oy0, int ox0, int Ho, int Wo, int C,
                         int CW, int T, int IT) {
   const int tid = threadIdx.x, NG = CW / 8;
@@ -95,10 +95,10 @@ MMF_DEV void dw_compute(const bf16_t* tile, const float* sw, const float* sb, fl
           const uint4 v = *reinterpret_cast<const uint4*>(tile + ((size_t)((oy * S + ky) * IT + ox * S + kx) * NG + g) * 8);
           const float4 w0 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8);
           const float4 w1 = *reinterpret_cast<const float4*>(sw + (ky * K + kx) * CW + g * 8 + 4);
-          acc[0] = fmaf(lo_bf(v.x), w0.x, acc[0]); acc[1] = fmaf(hi_bf(v.x), w0.y, acc[1]);
-          acc[2] = fmaf(lo_bf(v.y), w0.z, acc[2]); acc[3] = fmaf(hi_bf(v.y), w0.w, acc[3]);
-          acc[4] = fmaf(lo_bf(v.z), w1.x, acc[4]); acc[5] = fmaf(hi_bf(v.z), w1.y, acc[5]);
-          acc[6] = fmaf(lo_bf(v.w), w1.z, acc[6]); acc[7] = fmaf(hi_bf(v.w), w1.w, acc[7]);
+          acc[0] = fmaf(lo_h(v.x), w0.x, acc[0]); acc[1] = fmaf(hi_h(v.x), w0.y, acc[1]);
+          acc[2] = fmaf(lo_h(v.y), w0.z, acc[2]); acc[3] = fmaf(hi_h(v.y), w0.w, acc[3]);
+          acc[4] = fmaf(lo_h(v.z), w1.x, acc[4]); acc[5] = fmaf(hi_h(v.z), w1.y, acc[5]);
+          acc[6] = fmaf(lo_h(v.w), w1.z, acc[6]); acc[7] = fmaf(hi_h(v.w), w1.w, acc[7]);
         }
       }
 #pragma unroll
@@ -107,8 +107,8 @@ MMF_DEV void dw_compute(const bf16_t* tile, const float* sw, const float* sb, fl
         psum[j] += acc[j];
       }
       *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox) * C + c0 + g * 8) =
-          make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]), pack2bf(acc[4], acc[5]),
-                     pack2bf(acc[6], acc[7]));
+          make_uint4(pack2h(acc[0], acc[1]), pack2h(acc[2], acc[3]), pack2h(acc[4], acc[5]),
+                     pack2h(acc[6], acc[7]));
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[px * CW + g * 8 + j] = psum[j];
@@ -125,12 +125,12 @@ MMF_DEV void dw_compute(const bf16_t* tile, const float* sw, const float* sb, fl
 
 // Compile-time-geometry variant of dw_compute: T x T output tile, CW channels, and each work item
 // (channel group g, output row oy, run of R consecutive outputs) walks the input row segment of a
-// kernel row once -- ((R-1)S + K) LDS reads / bf16 unpacks per kernel row instead of R*K -- and
+// kernel row once -- ((R-1)S + K) LDS reads / fp16 unpacks per kernel row instead of R*K -- and
 // reuses the kernel row's weights for all R outputs (K reads instead of R*K).  Per output the
 // VALU work drops by ~30 % at K = 5, R = 7, and every tile offset is an immediate.
 // Items = NG * T * (T / R) over the first (256 / NG) * NG threads (each keeps its channel group).
 template <int K, int S, int T, int CW, int R>
-MMF_DEV void dw_compute_ct(const bf16_t* tile, const float* sw, const float* sb, float* red, bf16_t* __restrict__ out,
+MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, float* red, f16_t* __restrict__ out,
                            float* __restrict__ pool_part, int bi, int c0, int oy0, int ox0, int Ho, int Wo, int C) {
   constexpr int NG = CW / 8, IT = (T - 1) * S + K, NR = T / R, ITEMS = NG * T * NR, IC = (R - 1) * S + K;
   constexpr int STRIDE = (256 / NG) * NG;  // active threads: a thread's channel group g never changes
@@ -159,12 +159,12 @@ MMF_DEV void dw_compute_ct(const bf16_t* tile, const float* sw, const float* sb,
           wk[kx][0] = w0.x; wk[kx][1] = w0.y; wk[kx][2] = w0.z; wk[kx][3] = w0.w;
           wk[kx][4] = w1.x; wk[kx][5] = w1.y; wk[kx][6] = w1.z; wk[kx][7] = w1.w;
         }
-        const bf16_t* row = tile + ((size_t)((oy * S + ky) * IT + ox * S) * NG + g) * 8;
+        const f16_t* row = tile + ((size_t)((oy * S + ky) * IT + ox * S) * NG + g) * 8;
 #pragma unroll
         for (int col = 0; col < IC; ++col) {
           const uint4 v = *reinterpret_cast<const uint4*>(row + col * NG * 8);
-          const float f[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
-                              lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+          const float f[8] = {lo_h(v.x), hi_h(v.x), lo_h(v.y), hi_h(v.y),
+                              lo_h(v.z), hi_h(v.z), lo_h(v.w), hi_h(v.w)};
 #pragma unroll
           for (int o = 0; o < R; ++o) {
             const int kx = col - o * S;
@@ -183,8 +183,8 @@ MMF_DEV void dw_compute_ct(const bf16_t* tile, const float* sw, const float* sb,
 #pragma unroll
           for (int j = 0; j < 8; ++j) psum[j] += acc[o][j];
           *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox + o) * C + c0 + g * 8) =
-              make_uint4(pack2bf(acc[o][0], acc[o][1]), pack2bf(acc[o][2], acc[o][3]), pack2bf(acc[o][4], acc[o][5]),
-                         pack2bf(acc[o][6], acc[o][7]));
+              make_uint4(pack2h(acc[o][0], acc[o][1]), pack2h(acc[o][2], acc[o][3]), pack2h(acc[o][4], acc[o][5]),
+                         pack2h(acc[o][6], acc[o][7]));
         }
       }
     }
@@ -221,8 +221,8 @@ MMF_DEV_HOST_INLINE int dw_tile_bytes(int IT, int CW, bool alias_red) {
 // grid (tiles_y * tiles_x, C / CW, B); block 256 threads (PX * NG of them active in phase 2)
 // TT / CWT / R > 0: compile-time tile edge, channel width and output run (dw_compute_ct); 0: runtime
 template <int K, int S, int TT, int CWT, int R>
-__global__ __launch_bounds__(256, 3) void dwconv_kernel(const bf16_t* __restrict__ in, const float* __restrict__ w,
-                                                     const float* __restrict__ bias, bf16_t* __restrict__ out,
+__global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict__ in, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, f16_t* __restrict__ out,
                                                      float* __restrict__ pool_part, int H, int W, int C, int CW_,
                                                      int T_, int tiles_x) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const bf16_t* __restrict
   const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   const int oy0 = ty0 * T, ox0 = tx0 * T;
-  bf16_t* tile = (bf16_t*)dw_smem;                                 // [IT][IT][CW]
+  f16_t* tile = (f16_t*)dw_smem;                                 // [IT][IT][CW]
   float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, TT > 0));  // [K*K][CW]
   float* sb = sw + K * K * CW;                                     // [CW]
   float* red = TT > 0 ? (float*)dw_smem : sb + CW;                 // [PX][CW]
@@ -297,15 +297,15 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const bf16_t* __restrict
 // writing and re-reading Cexp channels.  Used where Cin <= 64 (the high-resolution stages 2-4,
 // where that tensor dominates the image tower's traffic); elsewhere expand is its own launch.
 //  expand: E[pix][c] = SiLU(be[c] + sum_k X[pix][k] We[c][k]) as D = We . X^T on
-//          v_mfma_f32_16x16x32_bf16 (A = We rows of this channel group, B = 16 tile pixels), each
+//          v_mfma_f32_16x16x32_f16 (A = We rows of this channel group, B = 16 tile pixels), each
 //          lane ends with 4 consecutive channels of one pixel -> 8-B LDS writes; pixels outside the
 //          image are written as 0 (the depthwise conv zero-pads E, not X).
 // grid (tiles, Cexp / CW, B); block 256 threads; KS = ceil(Cin / 32) <= 2
 template <int K, int S, int KS, int TT, int R>
-__global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restrict__ x, int Cin,
-                                                        const bf16_t* __restrict__ we, const float* __restrict__ be,
+__global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restrict__ x, int Cin,
+                                                        const f16_t* __restrict__ we, const float* __restrict__ be,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
-                                                        bf16_t* __restrict__ out, float* __restrict__ pool_part, int H,
+                                                        f16_t* __restrict__ out, float* __restrict__ pool_part, int H,
                                                         int W, int C, int CW_, int T_, int tiles_x) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
   constexpr int PAD = (K - 1) / 2, KP = KS * 32;
@@ -317,12 +317,12 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restr
   const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   const int oy0 = ty0 * T, ox0 = tx0 * T;
-  bf16_t* tile = (bf16_t*)dw_smem;                                 // [IT][IT][CW]
+  f16_t* tile = (f16_t*)dw_smem;                                 // [IT][IT][CW]
   float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, TT > 0));  // [K*K][CW]
   float* sb = sw + K * K * CW;                                     // [CW]
   float* red = TT > 0 ? (float*)dw_smem : sb + CW;                 // [PX][CW]
   float* sbe = TT > 0 ? sb + CW : red + (256 / NG) * CW;           // [CW] expand bias
-  bf16_t* swe = (bf16_t*)(sbe + CW);                        // [CW][KP] expand weights (zero-padded K)
+  f16_t* swe = (f16_t*)(sbe + CW);                        // [CW][KP] expand weights (zero-padded K)
 
   // this wave's input-pixel fragments first: their HBM latency overlaps the weight staging
   constexpr int MAXRF = 6;  // ceil(ceil(IT^2 / 16) / 4) for IT <= 19 (host-checked)
@@ -374,8 +374,8 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restr
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          const bf16x8 wf = as_bf16x8(*reinterpret_cast<const uint4*>(swe + (nf * 16 + fr) * KP + ks * 32 + fg * 8));
-          acc = mfma16x16x32(wf, as_bf16x8(xr[it][ks]), acc);
+          const f16x8 wf = as_f16x8(*reinterpret_cast<const uint4*>(swe + (nf * 16 + fr) * KP + ks * 32 + fg * 8));
+          acc = mfma16x16x32(wf, as_f16x8(xr[it][ks]), acc);
         }
         if (pix < npix) {
           const int cl = nf * 16 + fg * 4;
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restr
           act4<ACT_SILU>(e);
 #pragma unroll
           for (int r = 0; r < 4; ++r) e[r] = inimg ? e[r] : 0.f;
-          *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + cl) = make_uint2(pack2bf(e[0], e[1]), pack2bf(e[2], e[3]));
+          *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + cl) = make_uint2(pack2h(e[0], e[1]), pack2h(e[2], e[3]));
         }
       }
     }
@@ -401,19 +401,19 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const bf16_t* __restr
 // of the image tower -- never touches HBM: the block reads a 37x37x3 uint8 image patch instead.
 //  stem on the MFMA as a K = 27 (padded to 32) GEMM: D[ch][pix] = W[ch][k] . P[k][pix] with
 //  k = (ky, kx, c) so that each ky contributes 9 CONTIGUOUS floats of one patch row (HWC);
-//  operands split as bf16 hi + lo (x = xh + xl, w = wh + wl; wl.xh + wh.xl + wh.xh, fp32
-//  accumulation) so the conv keeps ~16 mantissa bits, well under the bf16 rounding of its output.
+//  operands split as fp16 hi + lo (x = xh + xl, w = wh + wl; wl.xh + wh.xl + wh.xh, fp32
+//  accumulation) so the conv keeps ~20 mantissa bits, well under the fp16 rounding of its output.
 // grid (49, 1, B); block 256
 constexpr int SD_T = 16, SD_IT = 18, SD_PR = 2 * SD_IT + 1, SD_PW = SD_PR * 3;
 
 template <bool F32>
 __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const float* __restrict__ ws,
                                                       const float* __restrict__ bs, const float* __restrict__ wd,
-                                                      const float* __restrict__ bd, bf16_t* __restrict__ out,
+                                                      const float* __restrict__ bd, f16_t* __restrict__ out,
                                                       float* __restrict__ pool_part) {
   constexpr int CW = 32, NPIX = SD_IT * SD_IT, NMT = (NPIX + 15) / 16;
   __shared__ __attribute__((aligned(16))) float patch[(SD_PR * SD_PW + 255) / 256 * 256];  // image patch, HWC
-  __shared__ __attribute__((aligned(16))) bf16_t tile[NPIX * CW];      // stem output tile (+halo)
+  __shared__ __attribute__((aligned(16))) f16_t tile[NPIX * CW];      // stem output tile (+halo)
   __shared__ __attribute__((aligned(16))) float sw[9 * CW];
   __shared__ __attribute__((aligned(16))) float sb[CW];
   float* red = patch;  // pool-partial slots [64][32]: the patch is dead once the stem tile is built
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
   const float bd0 = tid < CW ? bd[tid] : 0.f;
   // stem weight fragments (A operand: row = output channel nt*16 + fr, k = fg*8 + e), split hi/lo
   int offk[8];
-  bf16x8 whi[2], wlo[2];
+  f16x8 whi[2], wlo[2];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int k = fg * 8 + e, ky = k / 9, r9 = k - ky * 9;
@@ -449,11 +449,11 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
     uint32_t h[4], l[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      h[q] = pack2bf(wv[2 * q], wv[2 * q + 1]);
-      l[q] = pack2bf(wv[2 * q] - lo_bf(h[q]), wv[2 * q + 1] - hi_bf(h[q]));
+      h[q] = pack2h(wv[2 * q], wv[2 * q + 1]);
+      l[q] = pack2h(wv[2 * q] - lo_h(h[q]), wv[2 * q + 1] - hi_h(h[q]));
     }
-    whi[nt] = as_bf16x8(make_uint4(h[0], h[1], h[2], h[3]));
-    wlo[nt] = as_bf16x8(make_uint4(l[0], l[1], l[2], l[3]));
+    whi[nt] = as_f16x8(make_uint4(h[0], h[1], h[2], h[3]));
+    wlo[nt] = as_f16x8(make_uint4(l[0], l[1], l[2], l[3]));
   }
   float4 sbias[2];
 #pragma unroll
@@ -504,11 +504,11 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
     uint32_t h[4], l[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      h[q] = pack2bf(xv[2 * q], xv[2 * q + 1]);
-      l[q] = pack2bf(xv[2 * q] - lo_bf(h[q]), xv[2 * q + 1] - hi_bf(h[q]));
+      h[q] = pack2h(xv[2 * q], xv[2 * q + 1]);
+      l[q] = pack2h(xv[2 * q] - lo_h(h[q]), xv[2 * q + 1] - hi_h(h[q]));
     }
-    const bf16x8 xhi = as_bf16x8(make_uint4(h[0], h[1], h[2], h[3]));
-    const bf16x8 xlo = as_bf16x8(make_uint4(l[0], l[1], l[2], l[3]));
+    const f16x8 xhi = as_f16x8(make_uint4(h[0], h[1], h[2], h[3]));
+    const f16x8 xlo = as_f16x8(make_uint4(l[0], l[1], l[2], l[3]));
     const int gy = oy0 - 1 + sy, gx = ox0 - 1 + sx;  // stem output coords of this pixel
     const bool inimg = gy >= 0 && gy < 112 && gx >= 0 && gx < 112;
 #pragma unroll
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
       act4<ACT_SILU>(e4);
       if (p < NPIX)
         *reinterpret_cast<uint2*>(tile + p * CW + nt * 16 + fg * 4) =
-            inimg ? make_uint2(pack2bf(e4[0], e4[1]), pack2bf(e4[2], e4[3])) : make_uint2(0, 0);
+            inimg ? make_uint2(pack2h(e4[0], e4[1]), pack2h(e4[2], e4[3])) : make_uint2(0, 0);
     }
   }
   __syncthreads();
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
   }
 }
 
-__global__ __launch_bounds__(256) void gap_classifier_kernel(const bf16_t* x, int HW, int C, const float* w,
+__global__ __launch_bounds__(256) void gap_classifier_kernel(const f16_t* x, int HW, int C, const float* w,
                                                              const float* b, float* logits, float* score,
                                                              int score_stride) {
   __shared__ float red[2][4];
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(256) void gap_classifier_kernel(const bf16_t* x, in
   // 8 channels per thread (16-B loads), pixels summed in order; 7 rows of loads in flight
   for (int c8 = tid * 8; c8 < C; c8 += 256 * 8) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const bf16_t* xp = x + (size_t)bi * HW * C + c8;
+    const f16_t* xp = x + (size_t)bi * HW * C + c8;
     int p = 0;
     for (; p + 7 <= HW; p += 7) {
       uint4 v[7];
@@ -632,14 +632,14 @@ __global__ __launch_bounds__(256) void gap_classifier_kernel(const bf16_t* x, in
       for (int u = 0; u < 7; ++u) v[u] = *reinterpret_cast<const uint4*>(xp + (size_t)(p + u) * C);
 #pragma unroll
       for (int u = 0; u < 7; ++u) {
-        s[0] += lo_bf(v[u].x); s[1] += hi_bf(v[u].x); s[2] += lo_bf(v[u].y); s[3] += hi_bf(v[u].y);
-        s[4] += lo_bf(v[u].z); s[5] += hi_bf(v[u].z); s[6] += lo_bf(v[u].w); s[7] += hi_bf(v[u].w);
+        s[0] += lo_h(v[u].x); s[1] += hi_h(v[u].x); s[2] += lo_h(v[u].y); s[3] += hi_h(v[u].y);
+        s[4] += lo_h(v[u].z); s[5] += hi_h(v[u].z); s[6] += lo_h(v[u].w); s[7] += hi_h(v[u].w);
       }
     }
     for (; p < HW; ++p) {
       const uint4 v = *reinterpret_cast<const uint4*>(xp + (size_t)p * C);
-      s[0] += lo_bf(v.x); s[1] += hi_bf(v.x); s[2] += lo_bf(v.y); s[3] += hi_bf(v.y);
-      s[4] += lo_bf(v.z); s[5] += hi_bf(v.z); s[6] += lo_bf(v.w); s[7] += hi_bf(v.w);
+      s[0] += lo_h(v.x); s[1] += hi_h(v.x); s[2] += lo_h(v.y); s[3] += hi_h(v.y);
+      s[4] += lo_h(v.z); s[5] += hi_h(v.z); s[6] += lo_h(v.w); s[7] += hi_h(v.w);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(256) void gap_classifier_kernel(const bf16_t* x, in
 
 }  // namespace
 
-hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, bf16_t* out, int B,
+hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, f16_t* out, int B,
                               hipStream_t s) {
   const size_t total = (size_t)B * 112 * 112;
   hipLaunchKernelGGL(stem_kernel<false>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const void*)img, w,
@@ -673,7 +673,7 @@ hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* b
 }
 
 hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
-                                 const float* wd, const float* bd, bf16_t* out, float* pool_part, int B,
+                                 const float* wd, const float* bd, f16_t* out, float* pool_part, int B,
                                  int* nchunks_out, hipStream_t s) {
   *nchunks_out = 49;  // = dwconv_nchunks(112, 112, 32, 1): the SE reads the same partial layout
   const dim3 grid(49, 1, B), blk(256);
@@ -682,7 +682,7 @@ hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const fl
   return hipGetLastError();
 }
 
-hipError_t launch_effnet_stem_f32(const float* x, const float* w, const float* bias, bf16_t* out, int B,
+hipError_t launch_effnet_stem_f32(const float* x, const float* w, const float* bias, f16_t* out, int B,
                                   hipStream_t s) {
   const size_t total = (size_t)B * 112 * 112;
   hipLaunchKernelGGL(stem_kernel<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const void*)x, w,
@@ -710,7 +710,7 @@ int dwconv_nchunks(int H, int W, int C, int stride) {
   return n;
 }
 
-hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part, int B,
+hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16_t* out, float* pool_part, int B,
                          int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct) {
   int T, CW, tiles_x, ntiles;
   dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
@@ -754,8 +754,8 @@ hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf
 
 bool expand_dw_applicable(int cin, int cexp) { return cin <= 64 && (cin % 8) == 0 && (cexp % 48) == 0; }
 
-hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const float* be, const float* w,
-                            const float* bias, bf16_t* out, float* pool_part, int B, int H, int W, int C, int k,
+hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const float* be, const float* w,
+                            const float* bias, f16_t* out, float* pool_part, int B, int H, int W, int C, int k,
                             int stride, int* nchunks_out, hipStream_t s, int ct) {
   int T, CW, tiles_x, ntiles;
   dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
@@ -800,7 +800,7 @@ hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const fl
   return hipGetLastError();
 }
 
-hipError_t launch_gap_classifier(const bf16_t* x, int HW, int C, const float* w, const float* b, float* logits,
+hipError_t launch_gap_classifier(const f16_t* x, int HW, int C, const float* w, const float* b, float* logits,
                                  float* score, int score_stride, int B, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;  // 16-B channel groups
   hipLaunchKernelGGL(gap_classifier_kernel, dim3(B), dim3(256), 0, s, x, HW, C, w, b, logits, score, score_stride);

@@ -1,4 +1,4 @@
-// bf16 MFMA GEMM for gfx950: C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ residual), fp32 accumulate.
+// fp16 MFMA GEMM for gfx950: C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ residual), fp32 accumulate.
 //
 // Used for every dense contraction of the hot path: RoBERTa / CLIP QKV, out-proj, FFN (SURVEY.md
 // §2.1), the CLIP patch embedding (im2col GEMM), the CLIP projections and the EfficientNet 1x1
@@ -6,11 +6,11 @@
 //
 // Design (CDNA4, 64-wide waves):
 //  * 256 threads = 4 waves in a WGM x WGN grid; each wave owns a (BM/WGM) x (BN/WGN) output block
-//    of 16x16 tiles computed with v_mfma_f32_16x16x32_bf16.
+//    of 16x16 tiles computed with v_mfma_f32_16x16x32_f16.
 //  * Operands are "swapped" (MFMA A-operand = W rows, B-operand = A rows) so that each lane ends
-//    with 4 CONSECUTIVE output columns of one row -> 16-B fp32 / 8-B bf16 epilogue stores and
+//    with 4 CONSECUTIVE output columns of one row -> 16-B fp32 / 8-B fp16 epilogue stores and
 //    vector bias/residual loads.
-//  * BK = 64: LDS tiles [rows][64] bf16 (128-B rows) with an XOR swizzle (16-B chunk ^= row & 7)
+//  * BK = 64: LDS tiles [rows][64] fp16 (128-B rows) with an XOR swizzle (16-B chunk ^= row & 7)
 //    that makes the 16-lane ds_read_b128 fragment reads conflict-free; double-buffered, register
 //    staged (next tile's global loads issued before the MFMAs, written to LDS after them).
 //  * XCD-aware bijective block remap so consecutive tiles of one row panel share an XCD's L2.
@@ -37,9 +37,9 @@ struct Cfg {
 MMF_DEV int swz(int row, int kc) { return row * BK + ((kc ^ (row & 7)) << 3); }
 
 template <int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) {
+__global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
   using C = Cfg<BM, BN, WGM, WGN>;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
+  __shared__ __attribute__((aligned(16))) f16_t lds[2 * (BM + BN) * BK];
   auto Xs = [&](int buf) { return lds + buf * (BM + BN) * BK; };
   auto Ws = [&](int buf) { return lds + buf * (BM + BN) * BK + BM * BK; };
 
@@ -76,10 +76,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
           const float* s = g.ascale + (size_t)(m / g.rows_per_batch) * K + k;
           const float4 s0 = *reinterpret_cast<const float4*>(s);
           const float4 s1 = *reinterpret_cast<const float4*>(s + 4);
-          v.x = pack2bf(lo_bf(v.x) * s0.x, hi_bf(v.x) * s0.y);
-          v.y = pack2bf(lo_bf(v.y) * s0.z, hi_bf(v.y) * s0.w);
-          v.z = pack2bf(lo_bf(v.z) * s1.x, hi_bf(v.z) * s1.y);
-          v.w = pack2bf(lo_bf(v.w) * s1.z, hi_bf(v.w) * s1.w);
+          v.x = pack2h(lo_h(v.x) * s0.x, hi_h(v.x) * s0.y);
+          v.y = pack2h(lo_h(v.y) * s0.z, hi_h(v.y) * s0.w);
+          v.z = pack2h(lo_h(v.z) * s1.x, hi_h(v.z) * s1.y);
+          v.w = pack2h(lo_h(v.w) * s1.z, hi_h(v.w) * s1.w);
         }
       }
       xr[i] = v;
@@ -122,16 +122,16 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
     if (kt + 1 < nk) load_regs(kt + 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 wf[C::NI], xf[C::MI];
+      f16x8 wf[C::NI], xf[C::MI];
 #pragma unroll
       for (int i = 0; i < C::NI; ++i) {
         const int row = wn * C::TN + i * 16 + fr;
-        wf[i] = as_bf16x8(*reinterpret_cast<const uint4*>(Ws(buf) + swz(row, ks * 4 + fg)));
+        wf[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws(buf) + swz(row, ks * 4 + fg)));
       }
 #pragma unroll
       for (int j = 0; j < C::MI; ++j) {
         const int row = wm * C::TM + j * 16 + fr;
-        xf[j] = as_bf16x8(*reinterpret_cast<const uint4*>(Xs(buf) + swz(row, ks * 4 + fg)));
+        xf[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs(buf) + swz(row, ks * 4 + fg)));
       }
 #pragma unroll
       for (int i = 0; i < C::NI; ++i)
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
     __syncthreads();
   }
 
-  // epilogue: lane holds C[m][n..n+3].  All loads (bias, bf16 residual) are issued before the
+  // epilogue: lane holds C[m][n..n+3].  All loads (bias, fp16 residual) are issued before the
   // first store and from clamped addresses (no divergent region around them): with one in-order
   // vmcnt a load issued after a store waits for that store, and a store's data VGPRs cannot be
   // rewritten until it completes, so interleaving them serialises the tail on store latency
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
         const float4 rr = *reinterpret_cast<const float4*>(g.res32 + (size_t)m * g.ldr + n);
         v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
       } else if (g.res16) {
-        v[0] += lo_bf(r16[i][j].x); v[1] += hi_bf(r16[i][j].x); v[2] += lo_bf(r16[i][j].y); v[3] += hi_bf(r16[i][j].y);
+        v[0] += lo_h(r16[i][j].x); v[1] += hi_h(r16[i][j].x); v[2] += lo_h(r16[i][j].y); v[3] += hi_h(r16[i][j].y);
       }
       acc[i][j] = f32x4{v[0], v[1], v[2], v[3]};
     }
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
     for (int j = 0; j < C::MI; ++j)
 #pragma unroll
       for (int i = 0; i < C::NI; ++i) {
-        o[i][j] = make_uint2(pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3]));
+        o[i][j] = make_uint2(pack2h(acc[i][j][0], acc[i][j][1]), pack2h(acc[i][j][2], acc[i][j][3]));
         asm volatile("" : "+v"(o[i][j].x), "+v"(o[i][j].y)::"memory");
       }
 #pragma unroll
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g, int tilesN) 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 template <int ROWS, int NW>
-MMF_DEV void glds_tile(const bf16_t* __restrict__ G, int ld, int row0, int rowmax, int k0, bf16_t* tile, int wave,
+MMF_DEV void glds_tile(const f16_t* __restrict__ G, int ld, int row0, int rowmax, int k0, f16_t* tile, int wave,
                        int lane) {
   constexpr int PER_WAVE = ROWS / (8 * NW);  // 1-KB segments (8 rows x 128 B) per wave
   static_assert(PER_WAVE * 8 * NW == ROWS, "rows must split evenly over the waves");
@@ -233,9 +233,9 @@ MMF_DEV void glds_tile(const bf16_t* __restrict__ G, int ld, int row0, int rowma
     const int c = (lane & 7) ^ (lane >> 3);  // logical chunk stored at physical slot (lane & 7) of row r
     int grow = row0 + r;
     grow = grow < rowmax ? grow : rowmax - 1;  // clamped rows are loaded but never stored
-    const bf16_t* src = G + (size_t)grow * ld + k0 + c * 8;
+    const f16_t* src = G + (size_t)grow * ld + k0 + c * 8;
     __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (lds_void_t*)((__attribute__((address_space(3))) bf16_t*)tile + seg * 512),
+                                     (lds_void_t*)((__attribute__((address_space(3))) f16_t*)tile + seg * 512),
                                      16, 0, 0);
   }
 }
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int STAGE = (BM + BN) * BK;
   static_assert(NW == 8 || NW == 4, "4 or 8 waves");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) f16_t lds[2 * STAGE];
 
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   auto stage = [&](int buf, int tile, int kt) {
     int tm_, tn_;
     tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);
-    bf16_t* nb = lds + buf * STAGE;
+    f16_t* nb = lds + buf * STAGE;
     glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
     glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
   };
@@ -317,23 +317,23 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
       else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
-      const bf16_t* Xs = lds + cur * STAGE;
-      const bf16_t* Ws = Xs + BM * BK;
+      const f16_t* Xs = lds + cur * STAGE;
+      const f16_t* Ws = Xs + BM * BK;
       if constexpr (BN == 192) {
         // 256x192 (wave tile 64x96): all 20 fragment reads of the K-step first, then its 48 MFMAs,
         // then the barrier -- pinned with sched_barriers (hipcc otherwise interleaves 2 reads +
         // lgkmcnt(0) per 8 MFMAs and sinks MFMAs below the barrier's vmcnt(0)).  Measured: these
         // GEMMs 3 % faster; the same schedule on the 256x256 tiles (24 reads, 64 MFMAs) 3-10 %
         // slower, so they keep the compiler's interleave below.
-        bf16x8 wf[2][NI], xf[2][MI];
+        f16x8 wf[2][NI], xf[2][MI];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
           for (int i = 0; i < NI; ++i)
-            wf[ks][i] = as_bf16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
+            wf[ks][i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
 #pragma unroll
           for (int j = 0; j < MI; ++j)
-            xf[ks][j] = as_bf16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
+            xf[ks][j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -346,13 +346,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
       } else {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          bf16x8 wf[NI], xf[MI];
+          f16x8 wf[NI], xf[MI];
 #pragma unroll
           for (int i = 0; i < NI; ++i)
-            wf[i] = as_bf16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
+            wf[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
 #pragma unroll
           for (int j = 0; j < MI; ++j)
-            xf[j] = as_bf16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
+            xf[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
 #pragma unroll
           for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
     // fetched at tile start and residual rows are loaded one fragment row AHEAD of the stores (one
     // vmcnt counter covers loads and stores in issue order).
     if (!has_res && !g.c32) {
-      // bf16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
+      // fp16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
       // fragment of each pair so every lane stores 16 contiguous bytes (half the store issues)
 #pragma unroll
       for (int j = 0; j < MI; ++j) {
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
             float v[4] = {acc[i + h2][j][0] + bias_r[i + h2].x, acc[i + h2][j][1] + bias_r[i + h2].y,
                           acc[i + h2][j][2] + bias_r[i + h2].z, acc[i + h2][j][3] + bias_r[i + h2].w};
             if (ACT != ACT_NONE) act4<ACT>(v);
-            pk[h2] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+            pk[h2] = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
           }
           const bool odd = fg & 1;
           // even fg: cols (16i + 4fg) .. +7 of fragment i; odd fg: cols (16(i+1) + 4(fg-1)) .. +7
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
             r[i] = buf_load_f4(rres, e * 4u);
           } else {
             const uint2 rr = buf_load_u2(rres, e * 2u);  // zeros when there is no residual
-            r[i] = make_float4(lo_bf(rr.x), hi_bf(rr.x), lo_bf(rr.y), hi_bf(rr.y));
+            r[i] = make_float4(lo_h(rr.x), hi_h(rr.x), lo_h(rr.y), hi_h(rr.y));
           }
         }
       };
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
           v[0] += rcur[i].x; v[1] += rcur[i].y; v[2] += rcur[i].z; v[3] += rcur[i].w;
           const uint32_t e = n < N ? m * (uint32_t)g.ldc + n : (kOOB >> 2);
           if (g.c32) buf_store_f4(rc32, e * 4u, make_float4(v[0], v[1], v[2], v[3]));
-          if (g.c16) buf_store_u2(rc16, e * 2u, make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3])));
+          if (g.c16) buf_store_u2(rc16, e * 2u, make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3])));
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) rcur[i] = rnext[i];
@@ -473,11 +473,11 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
 template <int BM, int BN, int WGM, int WGN>
 hipError_t run(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN), dim3(256), 0, s, a, tilesN);
+  hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN), dim3(256), 0, s, a, tilesN);
   return hipGetLastError();
 }
 
-// Split-K reduction: C = act(sum_z P[z] + bias) (+ residual), the epilogue of gemm_bf16_kernel
+// Split-K reduction: C = act(sum_z P[z] + bias) (+ residual), the epilogue of gemm_f16_kernel
 // in the same order; one thread per 4 consecutive columns.  res32 may alias c32 (in place).
 template <int ACT>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int S, GemmArgs g) {
@@ -503,11 +503,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
   } else if (g.res16) {
     const uint2 r = *reinterpret_cast<const uint2*>(g.res16 + (size_t)m * g.ldr + n);
-    v[0] += lo_bf(r.x); v[1] += hi_bf(r.x); v[2] += lo_bf(r.y); v[3] += hi_bf(r.y);
+    v[0] += lo_h(r.x); v[1] += hi_h(r.x); v[2] += lo_h(r.y); v[3] += hi_h(r.y);
   }
   if (g.c32) *reinterpret_cast<float4*>(g.c32 + (size_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
   if (g.c16)
-    *reinterpret_cast<uint2*>(g.c16 + (size_t)m * g.ldc + n) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+    *reinterpret_cast<uint2*>(g.c16 + (size_t)m * g.ldc + n) = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
 }
 
 // Skinny-M GEMMs with a deep K (the compact last encoder layers and projections, M = batch): the
@@ -520,7 +520,7 @@ hipError_t run_splitk(const GemmArgs& a, int S, hipStream_t s) {
   p.A = a.A; p.lda = a.lda; p.W = a.W; p.ldw = a.ldw;
   p.c32 = a.ws; p.ldc = a.N;
   p.M = a.M; p.N = a.N; p.K = a.K / S;
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p, tilesN);
+  hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p, tilesN);
   const int threads = a.M * (a.N >> 2);
   const dim3 grid((threads + 255) / 256);
   switch (a.act) {
@@ -591,11 +591,11 @@ int gemm_splitk_factor(const GemmArgs& a) {
 }
 
 const char* gemm_config_name(int c) {
-  static const char* names[] = {"gemm_bf16<256,32,4,1>",  "gemm_bf16<256,64,4,1>",  "gemm_bf16<64,128,1,4>",
-                                "gemm_bf16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
+  static const char* names[] = {"gemm_f16<256,32,4,1>",  "gemm_f16<256,64,4,1>",  "gemm_f16<64,128,1,4>",
+                                "gemm_f16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
                                 "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
                                 "pw_conv"};
-  return (c >= 0 && c < 10) ? names[c] : "gemm_bf16<?>";
+  return (c >= 0 && c < 10) ? names[c] : "gemm_f16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {

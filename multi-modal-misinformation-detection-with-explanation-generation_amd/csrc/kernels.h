@@ -4,17 +4,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef uint16_t bf16_t;
+typedef uint16_t f16_t;
 
 struct GemmArgs {
-  const bf16_t* A;  int lda;     // activations [M][K] bf16
-  const bf16_t* W;  int ldw;     // weights [N][K] bf16 (PyTorch Linear layout)
+  const f16_t* A;  int lda;     // activations [M][K] fp16
+  const f16_t* W;  int ldw;     // weights [N][K] fp16 (PyTorch Linear layout)
   const float* bias;             // [N] or null
   const float* res32;            // fp32 residual [M][N] (ldr) or null
-  const bf16_t* res16;           // bf16 residual [M][N] (ldr) or null
+  const f16_t* res16;           // fp16 residual [M][N] (ldr) or null
   int ldr;
   float* c32;                    // fp32 out [M][N] (ldc) or null
-  bf16_t* c16;                   // bf16 out [M][N] (ldc) or null
+  f16_t* c16;                   // fp16 out [M][N] (ldc) or null
   int ldc;
   const float* ascale;           // per-(batch, k) fp32 scale of A (SE excitation) or null
   int rows_per_batch;            // rows of A per batch item when ascale != null
@@ -36,48 +36,48 @@ bool pw_applicable(const GemmArgs& a);
 hipError_t launch_pw(const GemmArgs& a, hipStream_t s);
 
 // LayerNorm over rows of width C (multiple of 256): y = LN(x [+ add]) * g + b.
-// x/add fp32 with row strides; writes fp32 y32 and/or bf16 y16.
+// x/add fp32 with row strides; writes fp32 y32 and/or fp16 y16.
 hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd, const float* g, const float* b,
-                            float eps, float* y32, int ldy32, bf16_t* y16, int ldy16, int rows, int C,
+                            float eps, float* y32, int ldy32, f16_t* y16, int ldy16, int rows, int C,
                             hipStream_t s);
 
-// Residual add + LayerNorm: s = x (fp32, row stride ldx) + y (bf16 GEMM output, ldy); optionally
-// s32 = s, o32 = LN(s) (both with stride ldx; may alias x); o16 = LN(s) bf16 (ldo).  C in {512, 768}.
-hipError_t launch_add_ln(const float* x, int ldx, const bf16_t* y, int ldy, const float* g, const float* b, float eps,
-                         float* s32, float* o32, bf16_t* o16, int ldo, int rows, int C, hipStream_t s);
+// Residual add + LayerNorm: s = x (fp32, row stride ldx) + y (fp16 GEMM output, ldy); optionally
+// s32 = s, o32 = LN(s) (both with stride ldx; may alias x); o16 = LN(s) fp16 (ldo).  C in {512, 768}.
+hipError_t launch_add_ln(const float* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps,
+                         float* s32, float* o32, f16_t* o16, int ldo, int rows, int C, hipStream_t s);
 
-// Fused multi-head attention, head_dim 64, L <= 128: qkv bf16 [B*L][ldqkv] with q at col h*64,
-// k at D + h*64, v at 2D + h*64 (D = H*64); mask int32 [B][L] (1 keep) or null; out bf16 [B*L][ldo].
-hipError_t launch_attention(const bf16_t* qkv, int ldqkv, const int32_t* mask, bf16_t* out, int ldo, int B,
+// Fused multi-head attention, head_dim 64, L <= 128: qkv fp16 [B*L][ldqkv] with q at col h*64,
+// k at D + h*64, v at 2D + h*64 (D = H*64); mask int32 [B][L] (1 keep) or null; out fp16 [B*L][ldo].
+hipError_t launch_attention(const f16_t* qkv, int ldqkv, const int32_t* mask, f16_t* out, int ldo, int B,
                             int L, int H, int causal, hipStream_t s);
 
-// RoBERTa embeddings + LayerNorm -> x fp32 [B*L][H], xb bf16 [B*L][H]
+// RoBERTa embeddings + LayerNorm -> x fp32 [B*L][H], xb fp16 [B*L][H]
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
-                                const float* g, const float* b, float eps, uint16_t* xlo, bf16_t* xb, int B, int L,
+                                const float* g, const float* b, float eps, uint16_t* xlo, f16_t* xb, int B, int L,
                                 int H, int pad_id, hipStream_t s);
-// RoBERTa post-LN residual stream split as hi = bf16(x) (also the GEMM operand), lo = fp16(x - hi)
-hipError_t launch_add_ln_hilo(bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy, const float* g,
+// RoBERTa post-LN residual stream split as hi = fp16(x) (also the GEMM operand), lo = fp16(x - hi)
+hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const float* g,
                               const float* b, float eps, int rows, int C, hipStream_t s);
-hipError_t launch_hilo_rows(const bf16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
+hipError_t launch_hilo_rows(const f16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
                             hipStream_t s);
-// CLIP text embeddings (tok + pos) -> x fp32, then LN1 of layer 0 -> xb bf16
+// CLIP text embeddings (tok + pos) -> x fp32, then LN1 of layer 0 -> xb fp16
 hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
-                                  const float* b, float eps, float* x, bf16_t* xb, int B, int L, int H,
+                                  const float* b, float eps, float* x, f16_t* xb, int B, int L, int H,
                                   hipStream_t s);
-// CLIP patch im2col with normalisation: img uint8 [B,224,224,3] -> A bf16 [B*49][3072]
-hipError_t launch_clip_im2col(const uint8_t* img, bf16_t* A, int B, hipStream_t s);
-// CLIP vision: x = preLN(cat(cls, patches) + pos) -> x fp32 [B*50][768], xb = LN1(x) bf16
+// CLIP patch im2col with normalisation: img uint8 [B,224,224,3] -> A fp16 [B*49][3072]
+hipError_t launch_clip_im2col(const uint8_t* img, f16_t* A, int B, hipStream_t s);
+// CLIP vision: x = preLN(cat(cls, patches) + pos) -> x fp32 [B*50][768], xb = LN1(x) fp16
 hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
                                        const float* pre_g, const float* pre_b, const float* ln1_g,
-                                       const float* ln1_b, float eps, float* x, bf16_t* xb, int B,
+                                       const float* ln1_b, float eps, float* x, f16_t* xb, int B,
                                        hipStream_t s);
 // EOS index per row (first == eos_id, or argmax when eos_id == 2)
 hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int eos_id, hipStream_t s);
-// gather rows: out bf16 [B][C] = LN(x[row_index(b)]) where row_index = b*L + (idx ? idx[b] : 0)
+// gather rows: out fp16 [B][C] = LN(x[row_index(b)]) where row_index = b*L + (idx ? idx[b] : 0)
 hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const float* g, const float* b, float eps,
-                            bf16_t* out, float* out32, int B, int C, hipStream_t s);
-// compact copies of rows b*L + (idx ? idx[b] : 0) of a bf16 and an fp32 [.,C] buffer
-hipError_t launch_gather_rows2(const bf16_t* a16, const float* a32, const int32_t* idx, int L, int C, bf16_t* o16,
+                            f16_t* out, float* out32, int B, int C, hipStream_t s);
+// compact copies of rows b*L + (idx ? idx[b] : 0) of a fp16 and an fp32 [.,C] buffer
+hipError_t launch_gather_rows2(const f16_t* a16, const float* a32, const int32_t* idx, int L, int C, f16_t* o16,
                                float* o32, int B, hipStream_t s);
 // L2-normalise rows of fp32 [B][C] in place (C multiple of 64)
 hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s);
@@ -98,30 +98,30 @@ hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, 
                              float* disc, int disc_stride, const float* text_emb, const float* title_emb, int D,
                              float* text_sim, hipStream_t s);
 
-// EfficientNet-B0 pieces (NHWC bf16 activations)
-hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, bf16_t* out, int B,
+// EfficientNet-B0 pieces (NHWC fp16 activations)
+hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, f16_t* out, int B,
                               hipStream_t s);
-hipError_t launch_effnet_stem_f32(const float* x_nchw, const float* w, const float* bias, bf16_t* out, int B,
+hipError_t launch_effnet_stem_f32(const float* x_nchw, const float* w, const float* bias, f16_t* out, int B,
                                   hipStream_t s);
 // stem fused into the stage-1 depthwise conv (3x3 s1, 32 channels at 112^2) + its SE pool partials;
 // exactly one of img (uint8 HWC) / xf32 (normalised fp32 NCHW) is non-null
 hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
-                                 const float* wd, const float* bd, bf16_t* out, float* pool_part, int B,
+                                 const float* wd, const float* bd, f16_t* out, float* pool_part, int B,
                                  int* nchunks_out, hipStream_t s);
 // ct = 0 forces the runtime-geometry kernels (A/B option "dw_ct"; the default uses the
 // compile-time tile geometries)
-hipError_t launch_dwconv(const bf16_t* in, const float* w, const float* bias, bf16_t* out, float* pool_part,
+hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16_t* out, float* pool_part,
                          int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s);
-hipError_t launch_gap_classifier(const bf16_t* x, int HW, int C, const float* w, const float* b, float* logits,
+hipError_t launch_gap_classifier(const f16_t* x, int HW, int C, const float* w, const float* b, float* logits,
                                  float* score, int score_stride, int B, hipStream_t s);
 hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);
-// fused MBConv front: expand 1x1 (we bf16 [C][cin], be fp32, BN folded) + SiLU computed per input
+// fused MBConv front: expand 1x1 (we fp16 [C][cin], be fp32, BN folded) + SiLU computed per input
 // tile into LDS, then the depthwise conv of launch_dwconv (same outputs, same pool partials)
 bool expand_dw_applicable(int cin, int cexp);
-hipError_t launch_expand_dw(const bf16_t* x, int cin, const bf16_t* we, const float* be, const float* w,
-                            const float* bias, bf16_t* out, float* pool_part, int B, int H, int W, int C, int k,
+hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const float* be, const float* w,
+                            const float* bias, f16_t* out, float* pool_part, int B, int H, int W, int C, int k,
                             int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 // number of pool-partial chunks launch_dwconv uses for an output of Ho x Wo with C channels
 int dwconv_nchunks(int H, int W, int C, int stride);

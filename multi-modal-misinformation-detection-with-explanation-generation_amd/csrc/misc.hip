@@ -319,9 +319,9 @@ __global__ __launch_bounds__(1024) void vault_sort_topk_kernel(const float* S, i
     }
   }
   const bool hit = key[0] > thresh;
-  if (tid < k) {
-    if (sims) sims[(size_t)row * k + tid] = key[tid];
-    if (idx) idx[(size_t)row * k + tid] = id[tid];
+  for (int t = tid; t < k; t += 1024) {
+    if (sims) sims[(size_t)row * k + t] = key[t];
+    if (idx) idx[(size_t)row * k + t] = id[t];
   }
   if (tid == 0 && disc) disc[(size_t)row * disc_stride] = hit ? key[0] : 0.f;
   if (tsim && tid < 64) {

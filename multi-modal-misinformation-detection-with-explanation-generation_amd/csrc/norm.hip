@@ -1,7 +1,7 @@
 // Row-wise kernels: LayerNorm, embeddings (+LN), CLIP patch im2col, EOS pooling, L2 norm.
 // One 64-lane wave per row of width C in {512, 768}: every lane holds C/256 float4 in registers,
 // so a row is read once, reduced with DPP/shuffle trees and written once (fp32 residual stream
-// and/or bf16 GEMM operand).  Variance is the two-pass mean((x-mean)^2) in fp32 like torch.
+// and/or fp16 GEMM operand).  Variance is the two-pass mean((x-mean)^2) in fp32 like torch.
 #include "common.h"
 #include "kernels.h"
 
@@ -46,19 +46,19 @@ MMF_DEV void add_row(float4 (&v)[NV], const float* x, int lane) {
   }
 }
 template <int NV>
-MMF_DEV void store_row(const float4 (&v)[NV], float* y32, bf16_t* y16, int lane) {
+MMF_DEV void store_row(const float4 (&v)[NV], float* y32, f16_t* y16, int lane) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
     if (y32) *reinterpret_cast<float4*>(y32 + c) = v[i];
-    if (y16) *reinterpret_cast<uint2*>(y16 + c) = make_uint2(pack2bf(v[i].x, v[i].y), pack2bf(v[i].z, v[i].w));
+    if (y16) *reinterpret_cast<uint2*>(y16 + c) = make_uint2(pack2h(v[i].x, v[i].y), pack2h(v[i].z, v[i].w));
   }
 }
 
 template <int NV>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx, const float* add, int ldadd,
                                                         const float* g, const float* b, float eps, float* y32,
-                                                        int ldy32, bf16_t* y16, int ldy16, int rows) {
+                                                        int ldy32, f16_t* y16, int ldy16, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   float4 v[NV];
@@ -68,21 +68,21 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx,
   store_row<NV>(v, y32 ? y32 + (size_t)row * ldy32 : nullptr, y16 ? y16 + (size_t)row * ldy16 : nullptr, lane);
 }
 
-// Residual add + LayerNorm after an out-projection / FFN-2 GEMM whose bf16 output y is the
+// Residual add + LayerNorm after an out-projection / FFN-2 GEMM whose fp16 output y is the
 // residual branch: s = x + y in fp32 (x = fp32 residual stream), then
 //   pre-LN (CLIP, TF clip:357-385):   s32 = s (the new residual stream), o16 = LN(s)
 //   post-LN (RoBERTa, TF roberta:329-399): o32 = LN(s) (the new residual stream), o16 = LN(s)
 // s32 / o32 may alias x (each wave reads its whole row before writing it).
 template <int NV>
-__global__ __launch_bounds__(256) void add_ln_kernel(const float* x, int ldx, const bf16_t* y, int ldy, const float* g,
+__global__ __launch_bounds__(256) void add_ln_kernel(const float* x, int ldx, const f16_t* y, int ldy, const float* g,
                                                      const float* b, float eps, float* s32, float* o32,
-                                                     bf16_t* o16, int ldo, int rows) {
+                                                     f16_t* o16, int ldo, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   float4 v[NV];
   uint2 a[NV];
   const float* xr = x + (size_t)row * ldx;
-  const bf16_t* yr = y + (size_t)row * ldy;
+  const f16_t* yr = y + (size_t)row * ldy;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     v[i] = *reinterpret_cast<const float4*>(xr + (i * 64 + lane) * 4);
@@ -90,48 +90,41 @@ __global__ __launch_bounds__(256) void add_ln_kernel(const float* x, int ldx, co
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    v[i].x += lo_bf(a[i].x); v[i].y += hi_bf(a[i].x); v[i].z += lo_bf(a[i].y); v[i].w += hi_bf(a[i].y);
+    v[i].x += lo_h(a[i].x); v[i].y += hi_h(a[i].x); v[i].z += lo_h(a[i].y); v[i].w += hi_h(a[i].y);
   }
   if (s32) store_row<NV>(v, s32 + (size_t)row * ldx, nullptr, lane);
   ln_row<NV>(v, g, b, eps, NV * 256, lane);
   store_row<NV>(v, o32 ? o32 + (size_t)row * ldx : nullptr, o16 + (size_t)row * ldo, lane);
 }
 
-// RoBERTa's post-LN residual stream in split precision: x = hi + lo with hi = bf16(x) (the very
-// tensor the next GEMM reads) and lo = fp16(x - hi) (|lo| <= 2^-8 |x|; ~19 significant bits in
-// all, vs 24 for fp32).  4 bytes per element like fp32, but hi doubles as the bf16 GEMM operand,
+// RoBERTa's post-LN residual stream in split precision: x = hi + lo with hi = fp16(x) (the very
+// tensor the next GEMM reads) and lo = fp16(x - hi) (|lo| <= 2^-11 |x|; ~22 significant bits for
+// |x| >~ 0.03, vs 24 for fp32).  4 bytes per element like fp32, but hi doubles as the GEMM operand,
 // so add+LN writes 4 instead of 6 bytes per element (12 -> 10 B/elem of HBM traffic).
-typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
-MMF_DEV uint32_t pack2h(float a, float b) {
-  const f16x2_t h = {(_Float16)a, (_Float16)b};
-  return __builtin_bit_cast(uint32_t, h);
-}
-MMF_DEV float lo_h(uint32_t w) { return (float)__builtin_bit_cast(f16x2_t, w).x; }
-MMF_DEV float hi_h(uint32_t w) { return (float)__builtin_bit_cast(f16x2_t, w).y; }
 
 template <int NV>
-MMF_DEV void store_row_hilo(const float4 (&v)[NV], bf16_t* hi, uint16_t* lo, int lane) {
+MMF_DEV void store_row_hilo(const float4 (&v)[NV], f16_t* hi, uint16_t* lo, int lane) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
-    const uint2 h = make_uint2(pack2bf(v[i].x, v[i].y), pack2bf(v[i].z, v[i].w));
+    const uint2 h = make_uint2(pack2h(v[i].x, v[i].y), pack2h(v[i].z, v[i].w));
     *reinterpret_cast<uint2*>(hi + c) = h;
-    *reinterpret_cast<uint2*>(lo + c) = make_uint2(pack2h(v[i].x - lo_bf(h.x), v[i].y - hi_bf(h.x)),
-                                                   pack2h(v[i].z - lo_bf(h.y), v[i].w - hi_bf(h.y)));
+    *reinterpret_cast<uint2*>(lo + c) = make_uint2(pack2h(v[i].x - lo_h(h.x), v[i].y - hi_h(h.x)),
+                                                   pack2h(v[i].z - lo_h(h.y), v[i].w - hi_h(h.y)));
   }
 }
 
 // post-LN add+LayerNorm on the split stream: s = (hi + lo) + y; (hi, lo) = split(LN(s)), in place
 template <int NV>
-__global__ __launch_bounds__(256) void add_ln_hilo_kernel(bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy,
+__global__ __launch_bounds__(256) void add_ln_hilo_kernel(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy,
                                                           const float* g, const float* b, float eps, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   float4 v[NV];
   uint2 xh[NV], xl[NV], a[NV];
-  bf16_t* hr = hi + (size_t)row * ld;
+  f16_t* hr = hi + (size_t)row * ld;
   uint16_t* lr = lo + (size_t)row * ld;
-  const bf16_t* yr = y + (size_t)row * ldy;
+  const f16_t* yr = y + (size_t)row * ldy;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
@@ -141,26 +134,26 @@ __global__ __launch_bounds__(256) void add_ln_hilo_kernel(bf16_t* hi, uint16_t* 
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    v[i].x = (lo_bf(xh[i].x) + lo_h(xl[i].x)) + lo_bf(a[i].x);
-    v[i].y = (hi_bf(xh[i].x) + hi_h(xl[i].x)) + hi_bf(a[i].x);
-    v[i].z = (lo_bf(xh[i].y) + lo_h(xl[i].y)) + lo_bf(a[i].y);
-    v[i].w = (hi_bf(xh[i].y) + hi_h(xl[i].y)) + hi_bf(a[i].y);
+    v[i].x = (lo_h(xh[i].x) + lo_h(xl[i].x)) + lo_h(a[i].x);
+    v[i].y = (hi_h(xh[i].x) + hi_h(xl[i].x)) + hi_h(a[i].x);
+    v[i].z = (lo_h(xh[i].y) + lo_h(xl[i].y)) + lo_h(a[i].y);
+    v[i].w = (hi_h(xh[i].y) + hi_h(xl[i].y)) + hi_h(a[i].y);
   }
   ln_row<NV>(v, g, b, eps, NV * 256, lane);
   store_row_hilo<NV>(v, hr, lr, lane);
 }
 
 // fp32 rows (hi + lo) of the split stream, gathered with a row stride (the last layer's CLS rows)
-__global__ __launch_bounds__(256) void hilo_rows_kernel(const bf16_t* hi, const uint16_t* lo, int row_stride,
+__global__ __launch_bounds__(256) void hilo_rows_kernel(const f16_t* hi, const uint16_t* lo, int row_stride,
                                                         float* out, int B, int C) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
-  const bf16_t* hr = hi + (size_t)row * row_stride;
+  const f16_t* hr = hi + (size_t)row * row_stride;
   const uint16_t* lr = lo + (size_t)row * row_stride;
   for (int c = lane * 4; c < C; c += 256) {
     const uint2 h = *reinterpret_cast<const uint2*>(hr + c), l = *reinterpret_cast<const uint2*>(lr + c);
     *reinterpret_cast<float4*>(out + (size_t)row * C + c) =
-        make_float4(lo_bf(h.x) + lo_h(l.x), hi_bf(h.x) + hi_h(l.x), lo_bf(h.y) + lo_h(l.y), hi_bf(h.y) + hi_h(l.y));
+        make_float4(lo_h(h.x) + lo_h(l.x), hi_h(h.x) + hi_h(l.x), lo_h(h.y) + lo_h(l.y), hi_h(h.y) + hi_h(l.y));
   }
 }
 
@@ -169,7 +162,7 @@ __global__ __launch_bounds__(256) void hilo_rows_kernel(const bf16_t* hi, const 
 template <int NV>
 __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, const float* word, const float* pos,
                                                             const float* type0, const float* g, const float* b,
-                                                            float eps, uint16_t* xlo, bf16_t* xb, int L, int pad) {
+                                                            float eps, uint16_t* xlo, f16_t* xb, int L, int pad) {
   __shared__ int s_ids[512];
   __shared__ int s_pos[512];
   const int bi = blockIdx.x, tid = threadIdx.x;
@@ -205,11 +198,11 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
   }
 }
 
-// CLIP text: x = tok[id] + pos[t] (fp32 residual stream); xb = LN1_layer0(x) (bf16)
+// CLIP text: x = tok[id] + pos[t] (fp32 residual stream); xb = LN1_layer0(x) (fp16)
 template <int NV>
 __global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids, const float* tok, const float* pos,
                                                               const float* g, const float* b, float eps, float* x,
-                                                              bf16_t* xb, int rows, int L) {
+                                                              f16_t* xb, int rows, int L) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   constexpr int C = NV * 256;
@@ -225,7 +218,7 @@ __global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids
 // CLIP patch embedding operand: A[b*49 + p][c*1024 + ky*32 + kx] = (img/255 - mean_c)/std_c.
 // One thread per (patch row, ky, 8-pixel group): the 24 interleaved RGB bytes arrive as three
 // 8-B loads (was 8 single-byte loads per channel) and leave as one 16-B store per channel.
-__global__ __launch_bounds__(256) void clip_im2col_kernel(const uint8_t* img, bf16_t* A, int B) {
+__global__ __launch_bounds__(256) void clip_im2col_kernel(const uint8_t* img, f16_t* A, int B) {
   const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t total = (size_t)B * 49 * 128;
   if (gid >= total) return;
@@ -249,7 +242,7 @@ __global__ __launch_bounds__(256) void clip_im2col_kernel(const uint8_t* img, bf
       v[j] = ((float)((wd[byte >> 2] >> ((byte & 3) * 8)) & 0xffu) * (1.0f / 255.0f) - mean) * istd;
     }
     *reinterpret_cast<uint4*>(A + rowp * 3072 + c * 1024 + ky * 32 + kx0) =
-        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+        make_uint4(pack2h(v[0], v[1]), pack2h(v[2], v[3]), pack2h(v[4], v[5]), pack2h(v[6], v[7]));
   }
 }
 
@@ -258,7 +251,7 @@ __global__ __launch_bounds__(256) void clip_vision_assemble_kernel(const float* 
                                                                    const float* pos, const float* pg,
                                                                    const float* pb, const float* g1,
                                                                    const float* b1, float eps, float* x,
-                                                                   bf16_t* xb, int rows) {
+                                                                   f16_t* xb, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   constexpr int NV = 3, C = 768;
@@ -295,7 +288,7 @@ __global__ __launch_bounds__(256) void eos_index_kernel(const int32_t* ids, int3
 
 template <int NV>
 __global__ __launch_bounds__(256) void gather_ln_kernel(const float* x, const int32_t* idx, int L, const float* g,
-                                                        const float* b, float eps, bf16_t* out, float* out32,
+                                                        const float* b, float eps, f16_t* out, float* out32,
                                                         int B) {
   const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (bi >= B) return;
@@ -307,9 +300,9 @@ __global__ __launch_bounds__(256) void gather_ln_kernel(const float* x, const in
   store_row<NV>(v, out32 ? out32 + (size_t)bi * C : nullptr, out ? out + (size_t)bi * C : nullptr, lane);
 }
 
-// rows b*L + (idx ? idx[b] : 0) of a bf16 [.,C] and an fp32 [.,C] buffer -> compact [B,C] copies
-__global__ __launch_bounds__(256) void gather_rows2_kernel(const bf16_t* a16, const float* a32, const int32_t* idx,
-                                                           int L, int C, bf16_t* o16, float* o32, int B) {
+// rows b*L + (idx ? idx[b] : 0) of a fp16 [.,C] and an fp32 [.,C] buffer -> compact [B,C] copies
+__global__ __launch_bounds__(256) void gather_rows2_kernel(const f16_t* a16, const float* a32, const int32_t* idx,
+                                                           int L, int C, f16_t* o16, float* o32, int B) {
   const int bi = blockIdx.x;
   if (bi >= B) return;
   const size_t row = (size_t)bi * L + (idx ? idx[bi] : 0);
@@ -332,7 +325,7 @@ __global__ __launch_bounds__(256) void l2norm_kernel(float* x, int B, int C) {
 }  // namespace
 
 hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd, const float* g, const float* b,
-                            float eps, float* y32, int ldy32, bf16_t* y16, int ldy16, int rows, int C,
+                            float eps, float* y32, int ldy32, f16_t* y16, int ldy16, int rows, int C,
                             hipStream_t s) {
   const dim3 grid((rows + 3) / 4);
   if (C == 768)
@@ -346,8 +339,8 @@ hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd
   return hipGetLastError();
 }
 
-hipError_t launch_add_ln(const float* x, int ldx, const bf16_t* y, int ldy, const float* g, const float* b, float eps,
-                         float* s32, float* o32, bf16_t* o16, int ldo, int rows, int C, hipStream_t s) {
+hipError_t launch_add_ln(const float* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps,
+                         float* s32, float* o32, f16_t* o16, int ldo, int rows, int C, hipStream_t s) {
   const dim3 grid((rows + 3) / 4);
   if (!o16) return hipErrorInvalidValue;
   if (C == 768)
@@ -360,7 +353,7 @@ hipError_t launch_add_ln(const float* x, int ldx, const bf16_t* y, int ldy, cons
 }
 
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
-                                const float* g, const float* b, float eps, uint16_t* xlo, bf16_t* xb, int B, int L,
+                                const float* g, const float* b, float eps, uint16_t* xlo, f16_t* xb, int B, int L,
                                 int H, int pad_id, hipStream_t s) {
   if (H != 768 || L > 512) return hipErrorInvalidValue;
   // 4 workgroups per sequence: one per sequence left the chip at 256 workgroups (~77 us at B = 256)
@@ -370,7 +363,7 @@ hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const flo
 }
 
 hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
-                                  const float* b, float eps, float* x, bf16_t* xb, int B, int L, int H,
+                                  const float* b, float eps, float* x, f16_t* xb, int B, int L, int H,
                                   hipStream_t s) {
   if (H != 512) return hipErrorInvalidValue;
   const int rows = B * L;
@@ -379,7 +372,7 @@ hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const fl
   return hipGetLastError();
 }
 
-hipError_t launch_clip_im2col(const uint8_t* img, bf16_t* A, int B, hipStream_t s) {
+hipError_t launch_clip_im2col(const uint8_t* img, f16_t* A, int B, hipStream_t s) {
   if (reinterpret_cast<uintptr_t>(img) & 7) return hipErrorInvalidValue;  // 8-B pixel-row loads
   const size_t total = (size_t)B * 49 * 128;
   hipLaunchKernelGGL(clip_im2col_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, img, A, B);
@@ -388,7 +381,7 @@ hipError_t launch_clip_im2col(const uint8_t* img, bf16_t* A, int B, hipStream_t 
 
 hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
                                        const float* pre_g, const float* pre_b, const float* ln1_g,
-                                       const float* ln1_b, float eps, float* x, bf16_t* xb, int B,
+                                       const float* ln1_b, float eps, float* x, f16_t* xb, int B,
                                        hipStream_t s) {
   const int rows = B * 50;
   hipLaunchKernelGGL(clip_vision_assemble_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, patches, cls, pos, pre_g,
@@ -403,7 +396,7 @@ hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int 
 }
 
 hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const float* g, const float* b, float eps,
-                            bf16_t* out, float* out32, int B, int C, hipStream_t s) {
+                            f16_t* out, float* out32, int B, int C, hipStream_t s) {
   const dim3 grid((B + 3) / 4);
   if (C == 768)
     hipLaunchKernelGGL(gather_ln_kernel<3>, grid, dim3(256), 0, s, x, idx, L, g, b, eps, out, out32, B);
@@ -414,7 +407,7 @@ hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const flo
   return hipGetLastError();
 }
 
-hipError_t launch_gather_rows2(const bf16_t* a16, const float* a32, const int32_t* idx, int L, int C, bf16_t* o16,
+hipError_t launch_gather_rows2(const f16_t* a16, const float* a32, const int32_t* idx, int L, int C, f16_t* o16,
                                float* o32, int B, hipStream_t s) {
   if (C & 3) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_rows2_kernel, dim3(B), dim3(256), 0, s, a16, a32, idx, L, C, o16, o32, B);
@@ -426,14 +419,14 @@ hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_add_ln_hilo(bf16_t* hi, uint16_t* lo, int ld, const bf16_t* y, int ldy, const float* g,
+hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const float* g,
                               const float* b, float eps, int rows, int C, hipStream_t s) {
   if (C != 768 || (ld & 3) || (ldy & 3)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(add_ln_hilo_kernel<3>, dim3((rows + 3) / 4), dim3(256), 0, s, hi, lo, ld, y, ldy, g, b, eps, rows);
   return hipGetLastError();
 }
 
-hipError_t launch_hilo_rows(const bf16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
+hipError_t launch_hilo_rows(const f16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
                             hipStream_t s) {
   if ((C & 3) || (row_stride & 3)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(hilo_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, s, hi, lo, row_stride, out, B, C);

@@ -1,17 +1,17 @@
 // HBM-bound 1x1 convolutions of EfficientNet-B0 (expand: K = cin <= 192, project: N = cout <= 320
 // with K = cexp <= 256) as a streaming MFMA kernel:
-//     C[M][N] = act((A[M][K] * s[b][K]) . W[N][K]^T + bias) (+ res16), bf16 in / bf16 out.
+//     C[M][N] = act((A[M][K] * s[b][K]) . W[N][K]^T + bias) (+ res16), fp16 in / fp16 out.
 // M = B*H*W pixels is huge and N, K are small, so these launches are bounded by streaming A in
 // and C out: a GEMM tiling (K loop, double-buffered LDS tiles, 128x128 tiles
 // padded to K = 64) spends most of its time in per-tile latency instead.  Here instead:
-//  * a workgroup stages its W column block (<= 128 x KP bf16) and bias in LDS once, then walks
+//  * a workgroup stages its W column block (<= 128 x KP fp16) and bias in LDS once, then walks
 //    row blocks persistently;
 //  * each wave loads its A fragments straight from HBM into registers (16 rows x 16 B per lane,
 //    the MFMA B-operand layout), with the next row block's loads issued before the current
 //    block's MFMAs and epilogue (software pipelining across the persistent loop);
 //  * the epilogue (bias, SiLU, SE scale on A, residual) goes through a per-wave fp32 LDS stage so
 //    that every output byte leaves in a 16-B-per-lane, row-contiguous store (coalesced), with a
-//    single bf16 rounding, matching the tiled GEMM's numerics exactly.
+//    single fp16 rounding, matching the tiled GEMM's numerics exactly.
 #include "common.h"
 #include "kernels.h"
 
@@ -19,7 +19,7 @@ namespace {
 
 constexpr int PW_THREADS = 256;  // 4 waves
 
-// LDS image of W: [BN][KP] bf16, 16-B chunks XOR-swizzled per row so the 16-lane groups of the
+// LDS image of W: [BN][KP] fp16, 16-B chunks XOR-swizzled per row so the 16-lane groups of the
 // fragment ds_read_b128 are conflict-free (brute-forced against the gfx950 lane groups).
 template <int KS>
 MMF_DEV int pw_swz(int r) {
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
   constexpr int ROWS = 4 * RPW * 16;  // rows per row block (4 waves)
   constexpr int SLD = BN + 4;         // stage row stride (floats): conflict-free float4 writes
   constexpr int CPR = BN / 8;         // 16-B output chunks per stage row
-  __shared__ __attribute__((aligned(16))) bf16_t sW[BN * KP];
+  __shared__ __attribute__((aligned(16))) f16_t sW[BN * KP];
   __shared__ __attribute__((aligned(16))) float sBias[BN];
   __shared__ __attribute__((aligned(16))) float sStage[4][16 * SLD];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
 #pragma unroll
     for (int f = 0; f < RPW; ++f) {
       const uint32_t mrow0 = (uint32_t)rb * ROWS + (wave * RPW + f) * 16;
-      if (has_scale) {  // SE excitation: A *= s[image][k] (rounded to bf16 like the tiled GEMM)
+      if (has_scale) {  // SE excitation: A *= s[image][k] (rounded to fp16 like the tiled GEMM)
         const uint32_t bimg = min(mrow0 + fr, (uint32_t)(M - 1)) / (uint32_t)g.rows_per_batch;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -91,10 +91,10 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
           const uint32_t off = k < K ? (bimg * (uint32_t)K + k) * 4u : kOOB;
           const float4 s0 = buf_load_f4(rs, off), s1 = buf_load_f4(rs, off + 16u);
           u32x4& v = acur[f * KS + s];
-          v.x = pack2bf(lo_bf(v.x) * s0.x, hi_bf(v.x) * s0.y);
-          v.y = pack2bf(lo_bf(v.y) * s0.z, hi_bf(v.y) * s0.w);
-          v.z = pack2bf(lo_bf(v.z) * s1.x, hi_bf(v.z) * s1.y);
-          v.w = pack2bf(lo_bf(v.w) * s1.z, hi_bf(v.w) * s1.w);
+          v.x = pack2h(lo_h(v.x) * s0.x, hi_h(v.x) * s0.y);
+          v.y = pack2h(lo_h(v.y) * s0.z, hi_h(v.y) * s0.w);
+          v.z = pack2h(lo_h(v.z) * s1.x, hi_h(v.z) * s1.y);
+          v.w = pack2h(lo_h(v.w) * s1.z, hi_h(v.w) * s1.w);
         }
       }
       f32x4 acc[CF];
@@ -102,12 +102,12 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
       for (int c = 0; c < CF; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const bf16x8 xb = __builtin_bit_cast(bf16x8, acur[f * KS + s]);
+        const f16x8 xb = __builtin_bit_cast(f16x8, acur[f * KS + s]);
 #pragma unroll
         for (int c = 0; c < CF; ++c) {
           const int r = c * 16 + fr;
-          const bf16x8 wb =
-              as_bf16x8(*reinterpret_cast<const uint4*>(sW + r * KP + (((s * 4 + fg) ^ pw_swz<KS>(r)) << 3)));
+          const f16x8 wb =
+              as_f16x8(*reinterpret_cast<const uint4*>(sW + r * KP + (((s * 4 + fg) ^ pw_swz<KS>(r)) << 3)));
           acc[c] = mfma16x16x32(wb, xb, acc[c]);
         }
       }
@@ -139,11 +139,11 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
           if (has_res) {
             const u32x4 r4 =
                 __builtin_amdgcn_raw_buffer_load_b128(rr, n < N ? (m * (uint32_t)g.ldr + n) * 2u : kOOB, 0, 0);
-            o[0] += lo_bf(r4.x); o[1] += hi_bf(r4.x); o[2] += lo_bf(r4.y); o[3] += hi_bf(r4.y);
-            o[4] += lo_bf(r4.z); o[5] += hi_bf(r4.z); o[6] += lo_bf(r4.w); o[7] += hi_bf(r4.w);
+            o[0] += lo_h(r4.x); o[1] += hi_h(r4.x); o[2] += lo_h(r4.y); o[3] += hi_h(r4.y);
+            o[4] += lo_h(r4.z); o[5] += hi_h(r4.z); o[6] += lo_h(r4.w); o[7] += hi_h(r4.w);
           }
           const uint4 pk =
-              make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+              make_uint4(pack2h(o[0], o[1]), pack2h(o[2], o[3]), pack2h(o[4], o[5]), pack2h(o[6], o[7]));
           buf_store_u4(rc, n < N ? (m * (uint32_t)g.ldc + n) * 2u : kOOB, pk);
         }
       }

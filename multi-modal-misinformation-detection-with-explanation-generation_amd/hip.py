@@ -42,9 +42,9 @@ SIGNATURES = {
     "mmf_set_option": (_I, [_P, ctypes.c_char_p, _I]),
     "mmf_get_option": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_I)]),
     "mmf_device_bytes": (ctypes.c_int64, [_P]),
-    "mmf_gemm_bf16": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
-    "mmf_gemm_bf16_ex": (_I, [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P]),
-    "mmf_attention_bf16": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
+    "mmf_gemm_f16": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "mmf_gemm_f16_ex": (_I, [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P]),
+    "mmf_attention_f16": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }
 
 _lib = None

@@ -1,6 +1,6 @@
 """Per-kernel roofline accounting from the library's event timing (mmf_profile_begin/end).
 
-Peaks (MI355X, /opt/skills/guides/MI355X_MICROARCH.md): dense bf16 MFMA 2.5 PFLOP/s; HBM3E
+Peaks (MI355X, /opt/skills/guides/MI355X_MICROARCH.md): dense fp16 MFMA 2.5 PFLOP/s; HBM3E
 8.0 TB/s.  `achieved` divides ALGORITHMIC work (flops of the contraction, or the minimum bytes
 the op must move) by measured device time, so it is a lower bound on utilisation.
 """
@@ -54,13 +54,13 @@ def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:
 
 def kind_symbol(kind: str) -> str:
     """Event-profile kind -> kernel symbol as rocprofv3 prints it (GEMM kinds only)."""
-    m = re.match(r"gemm_(glds|bf16)<([\d,]+)> act=(\d)", kind)
+    m = re.match(r"gemm_(glds|f16)<([\d,]+)> act=(\d)", kind)
     if not m:
         return kind
     dims = m.group(2).split(",")
     if m.group(1) == "glds":
         return f"gemm_glds_kernel<{', '.join(dims + [m.group(3)])}>"
-    return f"gemm_bf16_kernel<{', '.join(dims)}>"
+    return f"gemm_f16_kernel<{', '.join(dims)}>"
 
 
 def pmc_traffic(symbol: str, path: str | None = None) -> float | None:

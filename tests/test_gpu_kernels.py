@@ -1,5 +1,5 @@
 """Per-kernel numerics of libmmf_hip.so on a real MI355X against plain PyTorch fp32 references
-of the same op (computed on the CPU from the same bf16-rounded operands)."""
+of the same op (computed on the CPU from the same fp16-rounded operands)."""
 import numpy as np
 import pytest
 import torch
@@ -15,8 +15,8 @@ def lib():
     return hip.load()
 
 
-def _bf16(x):
-    return x.to(torch.bfloat16)
+def _f16(x):
+    return x.to(torch.float16)
 
 
 def _act(x, act):
@@ -40,8 +40,8 @@ def _act(x, act):
 def test_gemm_vs_torch_fp32(lib, M, N, K, act, res):
     import mmf_amd.hip as hip
     g = torch.Generator().manual_seed(M * 7 + N)
-    A = _bf16(torch.randn(M, K, generator=g))
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
+    A = _f16(torch.randn(M, K, generator=g))
+    W = _f16(torch.randn(N, K, generator=g) * 0.05)
     bias = torch.randn(N, generator=g)
     R = torch.randn(M, N, generator=g) if res else None
     ref = _act(A.float() @ W.float().T + bias, act)
@@ -51,8 +51,8 @@ def test_gemm_vs_torch_fp32(lib, M, N, K, act, res):
     Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
     Rd = R.to(dev) if res else None
     c32 = torch.empty(M, N, device=dev)
-    c16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    hip.check(lib.mmf_gemm_bf16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), c32.data_ptr(),
+    c16 = torch.empty(M, N, device=dev, dtype=torch.float16)
+    hip.check(lib.mmf_gemm_f16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), c32.data_ptr(),
                                 c16.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
     torch.cuda.synchronize()
     out = c32.cpu()
@@ -63,18 +63,18 @@ def test_gemm_vs_torch_fp32(lib, M, N, K, act, res):
 
 @pytest.mark.parametrize("M,N,K,act", [(1000, 200, 128, 1), (2048, 2304, 768, 0), (777, 392, 512, 2),
                                        (4096, 3072, 768, 1), (300, 136, 64, 0)])
-def test_gemm_bf16_only_output(lib, M, N, K, act):
-    """bf16-only epilogue (paired 16-B stores across lanes l, l^16), incl. column tails."""
+def test_gemm_f16_only_output(lib, M, N, K, act):
+    """fp16-only epilogue (paired 16-B stores across lanes l, l^16), incl. column tails."""
     import mmf_amd.hip as hip
     g = torch.Generator().manual_seed(M + 3 * N)
-    A = _bf16(torch.randn(M, K, generator=g))
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
+    A = _f16(torch.randn(M, K, generator=g))
+    W = _f16(torch.randn(N, K, generator=g) * 0.05)
     bias = torch.randn(N, generator=g)
     ref = _act(A.float() @ W.float().T + bias, act)
     dev = torch.device("cuda")
-    c16 = torch.full((M, N + 8), 7.0, device=dev, dtype=torch.bfloat16)  # ldc = N + 8: canary columns
+    c16 = torch.full((M, N + 8), 7.0, device=dev, dtype=torch.float16)  # ldc = N + 8: canary columns
     Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)  # keep the device buffers alive across the call
-    hip.check(lib.mmf_gemm_bf16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), None,
+    hip.check(lib.mmf_gemm_f16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), None,
                                 None, c16.data_ptr(), N + 8, M, N, K, act, hip.stream_ptr()))
     torch.cuda.synchronize()
     out = c16.cpu().float()
@@ -99,8 +99,8 @@ def test_gemm_forced_configs(lib, gemm_config, cfg, M, N, K, act, res):
     import mmf_amd.hip as hip
     gemm_config(cfg)
     g = torch.Generator().manual_seed(cfg * 1000 + M)
-    A = _bf16(torch.randn(M, K, generator=g))
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
+    A = _f16(torch.randn(M, K, generator=g))
+    W = _f16(torch.randn(N, K, generator=g) * 0.05)
     bias = torch.randn(N, generator=g)
     R = torch.randn(M, N, generator=g) if res else None
     ref = _act(A.float() @ W.float().T + bias, act)
@@ -109,9 +109,9 @@ def test_gemm_forced_configs(lib, gemm_config, cfg, M, N, K, act, res):
     dev = torch.device("cuda")
     Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
     Rd = torch.nn.functional.pad(R, (0, 8)).to(dev) if res else None  # residual shares ldc = N + 8
-    c16 = torch.full((M, N + 8), 7.0, device=dev, dtype=torch.bfloat16)
+    c16 = torch.full((M, N + 8), 7.0, device=dev, dtype=torch.float16)
     c32 = torch.empty(M, N + 8, device=dev) if res else None
-    hip.check(lib.mmf_gemm_bf16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), hip.ptr(c32),
+    hip.check(lib.mmf_gemm_f16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), hip.ptr(c32),
                                 c16.data_ptr(), N + 8, M, N, K, act, hip.stream_ptr()))
     torch.cuda.synchronize()
     scale = ref.abs().max().item()
@@ -146,7 +146,7 @@ def _attn_ref(qkv, mask, B, L, H, causal):
 def test_attention_vs_torch_fp32(lib, B, L, H, causal, masked):
     import mmf_amd.hip as hip
     g = torch.Generator().manual_seed(L * 13 + H)
-    qkv = _bf16(torch.randn(B * L, 3 * H * 64, generator=g))
+    qkv = _f16(torch.randn(B * L, 3 * H * 64, generator=g))
     mask = None
     if masked:
         lens = torch.randint(1, L + 1, (B,), generator=g)
@@ -154,23 +154,23 @@ def test_attention_vs_torch_fp32(lib, B, L, H, causal, masked):
         mask = (torch.arange(L)[None] < lens[:, None]).int()
     ref = _attn_ref(qkv, mask, B, L, H, causal)
     dev = torch.device("cuda")
-    out = torch.empty(B * L, H * 64, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(B * L, H * 64, device=dev, dtype=torch.float16)
     md = mask.to(dev, torch.int32) if mask is not None else None
     qkv_d = qkv.to(dev)
-    hip.check(lib.mmf_attention_bf16(qkv_d.data_ptr(), hip.ptr(md), out.data_ptr(), B, L, H, causal,
+    hip.check(lib.mmf_attention_f16(qkv_d.data_ptr(), hip.ptr(md), out.data_ptr(), B, L, H, causal,
                                      hip.stream_ptr()))
     torch.cuda.synchronize()
     got = out.cpu().float()
     if mask is not None:  # padded query rows are don't-care in every caller; compare real rows
         keep = mask.reshape(-1).bool()
         got, ref = got[keep], ref[keep]
-    # P is rounded to bf16 before P.V (fp32 accumulate): ~2^-8 relative per term
+    # P is rounded to fp16 before P.V (fp32 accumulate): ~2^-8 relative per term
     assert (got - ref).abs().max().item() < 2e-2
     assert (got - ref).abs().mean().item() < 2e-3
 
 
 # EfficientNet 1x1 convolutions (M = B*H*W pixels): expand (SiLU) and project (SE scale on A,
-# optional bf16 residual); shapes of the real blocks at small batch, plus ragged M / N tails.
+# optional fp16 residual); shapes of the real blocks at small batch, plus ragged M / N tails.
 @pytest.mark.parametrize("M,N,K,act,scale,res", [
     (8 * 3136, 96, 16, 3, False, False), (4 * 3136, 144, 24, 3, False, False), (2 * 784, 240, 40, 3, False, False),
     (3 * 196, 480, 80, 3, False, False), (3 * 196, 672, 112, 3, False, False), (2 * 12544, 16, 32, 0, True, False),
@@ -183,14 +183,14 @@ def test_gemm_effnet_convs(lib, M, N, K, act, scale, res):
     g = torch.Generator().manual_seed(M + N + K)
     rpb = {8 * 3136: 3136, 4 * 3136: 3136, 3 * 3136: 3136, 2 * 784: 784, 3 * 196: 196, 2 * 12544: 12544,
            5 * 49: 49, 2 * 49: 49}.get(M, 1000)
-    A = _bf16(torch.randn(M, K, generator=g))
-    W = _bf16(torch.randn(N, K, generator=g) * (2.0 / K) ** 0.5)
+    A = _f16(torch.randn(M, K, generator=g))
+    W = _f16(torch.randn(N, K, generator=g) * (2.0 / K) ** 0.5)
     bias = torch.randn(N, generator=g) * 0.1
     S = torch.rand((M + rpb - 1) // rpb, K, generator=g) if scale else None
-    R = _bf16(torch.randn(M, N, generator=g)) if res else None
+    R = _f16(torch.randn(M, N, generator=g)) if res else None
     Af = A.float()
     if scale:
-        Af = (Af * S.repeat_interleave(rpb, 0)[:M]).to(torch.bfloat16).float()  # A*s rounded to bf16
+        Af = (Af * S.repeat_interleave(rpb, 0)[:M]).to(torch.float16).float()  # A*s rounded to fp16
     ref = _act(Af @ W.float().T + bias, act)
     if res:
         ref = ref + R.float()
@@ -198,8 +198,8 @@ def test_gemm_effnet_convs(lib, M, N, K, act, scale, res):
     Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
     Sd = S.to(dev) if scale else None
     Rd = R.to(dev) if res else None
-    out = torch.full((M, N), 7.0, device=dev, dtype=torch.bfloat16)
-    hip.check(lib.mmf_gemm_bf16_ex(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), hip.ptr(Sd), rpb,
+    out = torch.full((M, N), 7.0, device=dev, dtype=torch.float16)
+    hip.check(lib.mmf_gemm_f16_ex(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), hip.ptr(Sd), rpb,
                                    out.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
     torch.cuda.synchronize()
     got = out.cpu().float()

@@ -64,7 +64,7 @@ def test_analyze_batch_vs_golden(engine, golden, golden_inputs):
     np.testing.assert_array_equal(o["verdict"], (golden["fusion_probs"][:, 1] > 0.5).astype(np.int32))
     np.testing.assert_array_equal(o["top_idx"], golden["vault_top_idx"])
     np.testing.assert_allclose(o["top_sims"], golden["vault_top_sim"], atol=TOL)
-    # text_similarity (misinfo_forensics.py:467-484) is a cosine between two separately bf16-computed
+    # text_similarity (misinfo_forensics.py:467-484) is a cosine between two separately fp16-computed
     # CLIP text embeddings and is NOT one of the five fusion inputs (quirk Q7): 2e-3 bound.
     np.testing.assert_allclose(o["text_similarity"], golden["text_similarity"], atol=2e-3)
 
@@ -99,7 +99,7 @@ def test_batch_invariance_full_size(engine, det_sd):
 def test_fused_expand_dwconv_bit_identical(engine):
     """The fused MBConv front (1x1 expand computed per tile into the depthwise conv's LDS tile)
     produces bit-identical EfficientNet outputs to the separate expand GEMM + depthwise launches
-    (same MFMA operand order over K, same bias / SiLU / bf16 rounding), on a full 256 batch."""
+    (same MFMA operand order over K, same bias / SiLU / fp16 rounding), on a full 256 batch."""
     import mmf_amd.synthetic as syn
     imgs = syn.images(256, 17)
     engine.set_option("fuse_expand", 0)
@@ -112,8 +112,8 @@ def test_fused_expand_dwconv_bit_identical(engine):
 
 def test_fused_stem_dwconv_matches_separate(engine):
     """Stem fused into the stage-1 depthwise conv (stem recomputed per halo tile on the MFMA with
-    hi/lo-split bf16 operands) vs the separate fp32-FMA stem kernel + depthwise launch.  The two
-    stems round differently in the last fp32 bits, which flips occasional bf16 roundings of the
+    hi/lo-split fp16 operands) vs the separate fp32-FMA stem kernel + depthwise launch.  The two
+    stems round differently in the last fp32 bits, which flips occasional fp16 roundings of the
     stem activation, so the comparison is at the north-star tolerance on deepfake_score and a
     tight bound on the logits; both entry points (uint8 pixels, normalised fp32 NCHW)."""
     import mmf_amd.synthetic as syn
@@ -140,7 +140,7 @@ def test_fused_stem_dwconv_matches_separate(engine):
 def test_compile_time_dwconv_matches_runtime_geometry(engine):
     """Depthwise kernels with compile-time tile geometry and output runs (dw_compute_ct, the
     default) vs the runtime-geometry kernels (option dw_ct = 0).  Conv outputs are computed in the same
-    order; the SE pool partial sums are grouped differently, and those 1-ulp differences flip bf16
+    order; the SE pool partial sums are grouped differently, and those 1-ulp differences flip fp16
     roundings downstream, so the comparison is at the north-star tolerance on deepfake_score (both
     paths are also checked against the fp32 oracle by test_effnet_signal for the default)."""
     import mmf_amd.synthetic as syn

@@ -29,21 +29,21 @@ def main():
               [(n, M, N, K, act, 0, 0, 1, out) for n, M, N, K, act, out in SHAPES + ROUND])
     variants = [{k: int(x) for k, x in (kv.split("=", 1) for kv in v.split(","))} for v in a.variants]
     for name, M, N, K, act, sc, rs, rpb, out in shapes:
-        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.float16)
+        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.float16)
         bias = torch.randn(N, device=dev)
         S = torch.rand((M + rpb - 1) // rpb, K, device=dev) if sc else None
-        R16 = torch.randn(M, N, device=dev).to(torch.bfloat16) if rs else None
+        R16 = torch.randn(M, N, device=dev).to(torch.float16) if rs else None
         c32 = torch.empty(M, N, device=dev) if "32" in out else None
-        c16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if "16" in out else None
+        c16 = torch.empty(M, N, device=dev, dtype=torch.float16) if "16" in out else None
         R32 = torch.randn(M, N, device=dev) if "r" in out else None
 
         def call():
             if a.effnet:
-                hip.check(lib.mmf_gemm_bf16_ex(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R16),
+                hip.check(lib.mmf_gemm_f16_ex(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R16),
                                                hip.ptr(S), rpb, c16.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
             else:
-                hip.check(lib.mmf_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R32),
+                hip.check(lib.mmf_gemm_f16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R32),
                                             hip.ptr(c32), hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
         times = [[] for _ in variants]
         for _ in range(a.rounds):

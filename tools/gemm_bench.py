@@ -1,4 +1,4 @@
-"""Micro-benchmark of libmmf_hip's bf16 GEMM on the encoder shapes of the hot path.
+"""Micro-benchmark of libmmf_hip's fp16 GEMM on the encoder shapes of the hot path.
 
     python tools/gemm_bench.py [--configs auto,4,6] [--iters 20] [--round] [--effnet]
 
@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import mmf_amd.hip as hip  # noqa: E402
 
 # (name, M, N, K, act, out) at B=256: RoBERTa L=128, ViT L=50, CLIP text L=77 (out-proj / FFN-2
-# write their bf16 branch output; the fp32 residual add happens in add+LN)
+# write their fp16 branch output; the fp32 residual add happens in add+LN)
 SHAPES = [
     ("rob_qkv", 32768, 2304, 768, 0, "16"), ("rob_o", 32768, 768, 768, 0, "16"),
     ("rob_fc1", 32768, 3072, 768, 1, "16"), ("rob_fc2", 32768, 768, 3072, 0, "16"),
@@ -30,7 +30,7 @@ SHAPES = [
 # one persistent round of 256x256 tiles (256 tiles) at growing K: per-K-step slope vs fixed cost
 ROUND = [("round_k%d" % k, 8192, 2048, k, 0, "16") for k in (256, 512, 768, 1536, 3072, 6144)]
 
-# EfficientNet-B0 1x1 convolutions at B=256: (name, M, N, K, act, SE scale, bf16 residual, rows/image)
+# EfficientNet-B0 1x1 convolutions at B=256: (name, M, N, K, act, SE scale, fp16 residual, rows/image)
 EFFNET = [
     ("e2.1", 256 * 12544, 96, 16, 3, 0, 0, 12544), ("e2.2", 256 * 3136, 144, 24, 3, 0, 0, 3136),
     ("e3.2", 256 * 784, 240, 40, 3, 0, 0, 784), ("e4.2", 256 * 196, 480, 80, 3, 0, 0, 196),
@@ -61,17 +61,17 @@ def force(cfg):
 
 def effnet(a, lib, dev):
     for name, M, N, K, act, sc, rs, rpb in EFFNET:
-        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.float16)
+        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.float16)
         bias = torch.randn(N, device=dev)
         S = torch.rand(M // rpb, K, device=dev) if sc else None
-        R = torch.randn(M, N, device=dev).to(torch.bfloat16) if rs else None
-        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        R = torch.randn(M, N, device=dev).to(torch.float16) if rs else None
+        C = torch.empty(M, N, device=dev, dtype=torch.float16)
         byts = 2.0 * M * (K + N + (N if rs else 0))
         row = {"shape": name, "M": M, "N": N, "K": K, "MB": round(byts / 1e6, 1)}
         for cfg in a.configs.split(","):
             force(cfg)
-            us = timed_us(lambda: hip.check(lib.mmf_gemm_bf16_ex(
+            us = timed_us(lambda: hip.check(lib.mmf_gemm_f16_ex(
                 A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R), hip.ptr(S), rpb, C.data_ptr(), N, M,
                 N, K, act, hip.stream_ptr())), a.iters)
             row[cfg] = f"{us:.1f}us {byts / us / 1e6:.2f}TB/s"
@@ -98,14 +98,14 @@ def main():
         shapes = [(f"{n}_k{m}", M, N, K * int(m), act, out) for n, M, N, K, act, out in shapes
                   for m in a.kscale.split(",")]
     for name, M, N, K, act, out in shapes:
-        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.float16)
+        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.float16)
         bias = torch.randn(N, device=dev)
         c32 = torch.empty(M, N, device=dev) if "32" in out else None
-        c16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if "16" in out else None
+        c16 = torch.empty(M, N, device=dev, dtype=torch.float16) if "16" in out else None
 
         def call():
-            hip.check(lib.mmf_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None, hip.ptr(c32),
+            hip.check(lib.mmf_gemm_f16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None, hip.ptr(c32),
                                         hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
         row = {"shape": name, "M": M, "N": N, "K": K}
         for gm in [""] + [g for g in a.group_m.split(",") if g]:

@@ -1,4 +1,4 @@
-"""Reference point: torch (hipBLASLt) bf16 linear on the encoder GEMM shapes, same timing method
+"""Reference point: torch (hipBLASLt) fp16 linear on the encoder GEMM shapes, same timing method
 as tools/gemm_bench.py.  Diagnostic only (the product path never calls hipBLASLt)."""
 import json
 import os
@@ -13,9 +13,9 @@ from gemm_bench import SHAPES  # noqa: E402
 def main():
     dev = torch.device("cuda")
     for name, M, N, K, act, out in SHAPES:
-        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
-        b = torch.randn(N, device=dev).to(torch.bfloat16)
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.float16)
+        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.float16)
+        b = torch.randn(N, device=dev).to(torch.float16)
         row = {"shape": name}
         for label, fn in (("linear", lambda: torch.nn.functional.linear(A, W, b)),
                           ("mm", lambda: A @ W.t()),
