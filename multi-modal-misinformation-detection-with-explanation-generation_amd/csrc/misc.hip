@@ -203,16 +203,14 @@ __global__ __launch_bounds__(256) void vault_sims_kernel(const float* q, const f
 
 // Ranking of the reference's np.argsort(sims)[-k:][::-1] (misinfo_forensics.py:449): value
 // descending; numpy sorts NaN (a zero-norm vault row: 0/0 in the renormalisation, :443-445) after
-// every number, so the reversed tail puts NaN rows FIRST.  Exact ties: numpy's default sort is not
-// stable (its tie order is data- and platform-dependent); ties are ordered here by
-// descending index = what a stable argsort would give.  Index -1 marks an empty slot (always worst).
-MMF_DEV bool better(float a, int ia, float b, int ib) {
-  if (ib < 0) return ia >= 0;
-  if (ia < 0) return false;
-  const bool na = a != a, nb = b != b;
-  if (na || nb) return na && (!nb || ia > ib);
-  return a > b || (a == b && ia > ib);
-}
+// every number, so the reversed tail puts NaN rows FIRST.  The scans rank by a key: the similarity,
+// with NaN mapped to +inf (a cosine of unit rows is never +inf) and mapped back on output; empty
+// slots hold -inf with index -1.  Exact ties: numpy's default sort is not stable (its tie order is
+// data- and platform-dependent); ties are ordered here by descending index = what a
+// stable argsort would give.
+MMF_DEV float rank_key(float v) { return v != v ? INFINITY : v; }
+MMF_DEV float unkey(float k) { return k == INFINITY ? NAN : k; }
+MMF_DEV bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia > ib); }
 
 template <int K>
 __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, int N, float thresh, float* sims,
@@ -231,7 +229,7 @@ __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, 
   for (int j0 = lane; j0 < N; j0 += 512) {
     float vv[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) vv[u] = (j0 + 64 * u < N) ? s[j0 + 64 * u] : -INFINITY;
+    for (int u = 0; u < 8; ++u) vv[u] = (j0 + 64 * u < N) ? rank_key(s[j0 + 64 * u]) : -INFINITY;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const float v = vv[u];
@@ -267,11 +265,11 @@ __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, 
       tv[K - 1] = -INFINITY; ti[K - 1] = -1;
     }
   }
-  const bool hit = outv[0] > thresh;
+  const bool hit = outv[0] > thresh && outv[0] != INFINITY;  // NaN > thresh is false
   if (lane == 0) {
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-      if (sims) sims[(size_t)row * K + t] = outv[t];
+      if (sims) sims[(size_t)row * K + t] = unkey(outv[t]);
       if (idx) idx[(size_t)row * K + t] = outi[t];
     }
     if (disc) disc[(size_t)row * disc_stride] = hit ? outv[0] : 0.f;
@@ -299,7 +297,7 @@ __global__ __launch_bounds__(1024) void vault_sort_topk_kernel(const float* S, i
   const int row = blockIdx.x, tid = threadIdx.x;
   const float* s = S + (size_t)row * N;
   for (int i = tid; i < P; i += 1024) {
-    key[i] = i < N ? s[i] : -INFINITY;
+    key[i] = i < N ? rank_key(s[i]) : -INFINITY;
     id[i] = i < N ? i : -1;
   }
   __syncthreads();
@@ -318,12 +316,12 @@ __global__ __launch_bounds__(1024) void vault_sort_topk_kernel(const float* S, i
       __syncthreads();
     }
   }
-  const bool hit = key[0] > thresh;
+  const bool hit = key[0] > thresh && key[0] != INFINITY;
   for (int t = tid; t < k; t += 1024) {
-    if (sims) sims[(size_t)row * k + t] = key[t];
+    if (sims) sims[(size_t)row * k + t] = unkey(key[t]);
     if (idx) idx[(size_t)row * k + t] = id[t];
   }
-  if (tid == 0 && disc) disc[(size_t)row * disc_stride] = hit ? key[0] : 0.f;
+  if (tid == 0 && disc) disc[(size_t)row * disc_stride] = hit ? key[0] : 0.f;  // (a hit is finite)
   if (tsim && tid < 64) {
     float d = 0.f;
     if (hit && temb && title) {

@@ -65,3 +65,54 @@ def test_gloo_world2_matches_single_process(tmp_path, n):
     ref = torch.softmax(P.fusion_logits(sd, torch.as_tensor(x)), 1)
     # row-independent math: the sharded result equals the single-process one bit for bit
     assert torch.equal(res["probs"], ref) or np.allclose(res["probs"].numpy(), ref.numpy(), atol=1e-7)
+
+
+def _bench_worker(rank, world, port, out_path):
+    """bench.py's rank plumbing (mmf_amd.benchrun) over gloo: the launcher's env, per-rank seeds,
+    barrier-bracketed timing and the max-over-ranks reduction."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from mmf_amd import benchrun
+    w, r, lr = benchrun.rank_env()
+    dist = benchrun.init_dist(w, "gloo")
+    calls = []
+    delay = 0.02 * (r + 1)  # rank 1 is the slow one: the whole-job time must be its time
+
+    def step():
+        calls.append(1)
+        time.sleep(delay)
+
+    dt = benchrun.timed_steps(step, steps=5, warmup=2, dist=dist)
+    rate = benchrun.whole_job_rate(w, 256, 5, dt)
+    import torch.distributed as tdist
+    rows = [None] * w
+    tdist.all_gather_object(rows, {"rank": r, "world": w, "local": lr, "seed": benchrun.input_seed(r),
+                                   "calls": len(calls), "dt": dt, "rate": rate})
+    if r == 0:
+        torch.save(rows, out_path)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_benchrun_gloo_world2(tmp_path):
+    out = str(tmp_path / "bench.pt")
+    mp.start_processes(_bench_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    rows = torch.load(out)
+    assert [x["rank"] for x in rows] == [0, 1] and all(x["world"] == 2 for x in rows)
+    assert [x["local"] for x in rows] == [0, 1]
+    assert len({x["seed"] for x in rows}) == 2  # each rank draws its own shard
+    assert all(x["calls"] == 7 for x in rows)  # warmup 2 + exactly 5 timed steps
+    # every rank reports the same (max) time, bounded below by the slow rank's 5 x 40 ms
+    assert rows[0]["dt"] == rows[1]["dt"] and rows[0]["dt"] >= 5 * 0.04
+    assert rows[0]["rate"] == pytest.approx(2 * 256 * 5 / rows[0]["dt"])
+
+
+def test_benchrun_single_process():
+    from mmf_amd import benchrun
+    assert benchrun.init_dist(1, "gloo") is None
+    assert benchrun.max_over_ranks(1.5) == 1.5
+    n = []
+    dt = benchrun.timed_steps(lambda: n.append(1), steps=3, warmup=1)
+    assert len(n) == 4 and dt >= 0
+    assert benchrun.usable_cpus() >= 1
