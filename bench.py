@@ -169,6 +169,15 @@ def config_lines(eng, t, steps, warmup, det):
         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / PEAK_GBS, 4),
                      "work": "4.35 MB/img block-fused activation floor + 8 MB weights (0.769 GFLOP/img)"}}
+    # the same workload on the fp32 tower (option effnet_fp32, the ill-conditioned-weights mode)
+    eng.set_option("effnet_fp32", 1)
+    try:
+        dt = benchrun.timed_steps(effnet, steps, warmup, None, sync)
+    finally:
+        eng.set_option("effnet_fp32", 0)
+    out["effnet_fp32_b512"] = {
+        "config": "configs[2] workload on the fp32-activation EfficientNet tower (option effnet_fp32)",
+        "value": round(Be * steps / dt, 1), "unit": "images/s", "ms_per_step": round(1000 * dt / steps, 3)}
     eng.reserve(B, 128, 77)
     return out
 

@@ -287,7 +287,9 @@ class MisinfoForensics:
                  device: str = "cuda",
                  *, roberta_tokenizer=None, clip_processor=None, detector_state=None, clip_state=None,
                  synthetic_seed: Optional[int] = None, max_batch: int = 256, max_text_len: int = 128,
-                 verbose: bool = True):
+                 effnet_precision: str = "fp16", verbose: bool = True):
+        if effnet_precision not in ("fp16", "fp32"):
+            raise ValueError(f"effnet_precision must be 'fp16' or 'fp32', got {effnet_precision!r}")
         self.device = _require_hip(device)
         self._verbose = verbose
         self._log(f"Using device: {self.device}")
@@ -337,6 +339,9 @@ class MisinfoForensics:
         self.clip_eos_token_id = int(os.environ.get("MMF_CLIP_EOS_TOKEN_ID", eos))
         self.engine = Engine(self.device.index or 0, None, clip_state, eos_token_id=self.clip_eos_token_id,
                              max_batch=max_batch, max_text_len=max_text_len)
+        # fp32 EfficientNet activations: for towers whose logits reach O(100), where
+        # fp16 storage rounding is amplified past the 1e-3 parity bar
+        self.engine.set_option("effnet_fp32", int(effnet_precision == "fp32"))
         self.detector.bind(self.engine)  # uploads RoBERTa + heads, EfficientNet, FusionJudge
         self.clip_state = clip_state
 

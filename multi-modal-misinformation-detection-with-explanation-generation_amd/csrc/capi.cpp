@@ -54,7 +54,12 @@ struct HostT {
   size_t numel() const { return f.size(); }
 };
 
-struct Lin16 { f16_t* w = nullptr; float* b = nullptr; int out = 0, in = 0; };
+struct Lin16 {
+  f16_t* w = nullptr;
+  float* b = nullptr;
+  int out = 0, in = 0;
+  float* w32 = nullptr;  // fp32 copy of w (EfficientNet 1x1 convs: the effnet_fp32 tower)
+};
 struct LNp { float* g = nullptr; float* b = nullptr; };
 struct EncLayer { Lin16 qkv, o, fc1, fc2; LNp ln1, ln2; };
 
@@ -62,6 +67,7 @@ struct EffBlock {
   int expand, k, stride, cin, cout, cexp, csq, residual;
   Lin16 e, p;            // expand / project 1x1 convs (BN folded)
   float* wd = nullptr;   // depthwise [cexp][k*k] (BN folded)
+  float* wd_t = nullptr; // the same, tap-major [k*k][cexp] (fp32 tower)
   float* bd = nullptr;
   float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;  // SE
 };
@@ -85,6 +91,9 @@ struct Workspace {
   // EfficientNet
   f16_t *e_a = nullptr, *e_b = nullptr, *e_exp = nullptr, *e_dw = nullptr;
   float *e_pool = nullptr, *e_scale = nullptr;
+  // fp32 EfficientNet activations (option effnet_fp32), allocated on first use for cap_b images
+  float *e32_a = nullptr, *e32_b = nullptr, *e32_exp = nullptr, *e32_dw = nullptr;
+  int e32_cap_b = 0;
   // split-K partials of the skinny-M GEMMs, one per tower (the towers run on concurrent streams)
   float *sk_text = nullptr, *sk_vit = nullptr, *sk_ctext = nullptr;
   size_t sk_elems = 0;
@@ -104,13 +113,14 @@ struct Options {
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
+  int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
     {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"}, {"dw_ct", &Options::dw_ct, "MMF_DW_CT"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
-    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"},
+    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -132,7 +142,7 @@ void apply_options(const Options& o, GemmArgs* g) {
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the
 // workspaces) frees exactly what it replaces.
-enum AllocGroup { AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_COUNT };
+enum AllocGroup { AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_EFF32, AG_COUNT };
 
 }  // namespace
 
@@ -225,11 +235,12 @@ int free_group(mmf_handle* h, int group) {
 constexpr int kGemmActs = 5;
 enum ProfKind {
   PK_GEMM0 = 0, PK_GEMM_LAST = 13 * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
-  PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_COUNT
+  PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_PW32, PK_COUNT
 };
 const char* prof_kind_name(int k) {
   static const char* names[PK_COUNT - PK_ATTN] = {"attention", "layernorm", "embed+ln", "clip_im2col", "effnet_stem",
-                                                  "dwconv", "se", "gap_classifier", "text_heads", "vault", "fusion"};
+                                                  "dwconv", "se", "gap_classifier", "text_heads", "vault", "fusion",
+                                                  "pw32"};
   static char gemm_names[PK_GEMM_LAST + 1][64];
   if (k >= 0 && k <= PK_GEMM_LAST) {
     if (!gemm_names[k][0])
@@ -408,6 +419,7 @@ int finalize_effnet(mmf_handle* h) {
       if (B.expand != 1) {
         CHK(fold_bn(h, bp + "0.0", bp + "0.1", B.cexp, B.cin, &w, &b));
         CHK(up_f16(h, &B.e.w, w));
+        CHK(up_f32(h, &B.e.w32, w));
         CHK(up_f32(h, &B.e.b, b));
         B.e.out = B.cexp;
         B.e.in = B.cin;
@@ -415,6 +427,13 @@ int finalize_effnet(mmf_handle* h) {
       }
       CHK(fold_bn(h, bp + std::to_string(i) + ".0", bp + std::to_string(i) + ".1", B.cexp, (size_t)B.k * B.k, &w, &b));
       CHK(up_f32(h, &B.wd, w));
+      {
+        std::vector<float> t(w.size());
+        const int kk = B.k * B.k;
+        for (int c = 0; c < B.cexp; ++c)
+          for (int q = 0; q < kk; ++q) t[(size_t)q * B.cexp + c] = w[(size_t)c * kk + q];
+        CHK(up_f32(h, &B.wd_t, t));
+      }
       CHK(up_f32(h, &B.bd, b));
       const std::string se = bp + std::to_string(i + 1) + ".";
       CHK(load_f32(h, &B.w1, se + "fc1.weight", (size_t)B.csq * B.cexp));
@@ -426,6 +445,7 @@ int finalize_effnet(mmf_handle* h) {
       CHK(load_f32(h, &B.b2, se + "fc2.bias", B.cexp));
       CHK(fold_bn(h, bp + std::to_string(i + 2) + ".0", bp + std::to_string(i + 2) + ".1", B.cout, B.cexp, &w, &b));
       CHK(up_f16(h, &B.p.w, w));
+      CHK(up_f32(h, &B.p.w32, w));
       CHK(up_f32(h, &B.p.b, b));
       B.p.out = B.cout;
       B.p.in = B.cexp;
@@ -434,6 +454,7 @@ int finalize_effnet(mmf_handle* h) {
   }
   CHK(fold_bn(h, p + "8.0", p + "8.1", 1280, 320, &w, &b));
   CHK(up_f16(h, &h->e_head.w, w));
+  CHK(up_f32(h, &h->e_head.w32, w));
   CHK(up_f32(h, &h->e_head.b, b));
   h->e_head.out = 1280;
   h->e_head.in = 320;
@@ -728,8 +749,92 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
   return 0;
 }
 
+// EfficientNet-B0 activation elements per image: block input/output, expanded, depthwise output,
+// SE pool partials (nchunks x channels) maxima over the network
+struct EffSizes { size_t io, exp, dw, pool; };
+EffSizes eff_sizes() {
+  EffSizes z{(size_t)112 * 112 * 32, 0, 0, 0};
+  int H = 112;
+  for (int si = 0; si < 7; ++si)
+    for (int j = 0; j < kStages[si][5]; ++j) {
+      const int e = kStages[si][0], st = j == 0 ? kStages[si][2] : 1;
+      const int cin = j == 0 ? kStages[si][3] : kStages[si][4], cout = kStages[si][4], cexp = cin * e;
+      const int Ho = (H - 1) / st + 1;
+      z.exp = std::max(z.exp, (size_t)H * H * cexp);
+      z.dw = std::max(z.dw, (size_t)Ho * Ho * cexp);
+      z.io = std::max(z.io, (size_t)Ho * Ho * cout);
+      z.pool = std::max(z.pool, (size_t)dwconv_nchunks(H, H, cexp, st) * cexp);
+      H = Ho;
+    }
+  z.exp = std::max(z.exp, (size_t)7 * 7 * 1280);
+  return z;
+}
+
+// The fp32 tower (option effnet_fp32): same network, same folded weights (fp32 copies of the 1x1
+// convs), activations fp32 throughout -- no fusion, one launch per layer.
+int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score,
+                 int score_stride, hipStream_t s) {
+  Workspace& w = h->ws;
+  if (w.e32_cap_b < h->cap_b) {
+    CHK(free_group(h, AG_EFF32));
+    const EffSizes es = eff_sizes();
+    const size_t nb = (size_t)h->cap_b * 4;
+    void* p;
+    CHK(dev_alloc(h, &p, nb * es.io, AG_EFF32)); w.e32_a = (float*)p;
+    CHK(dev_alloc(h, &p, nb * es.io, AG_EFF32)); w.e32_b = (float*)p;
+    CHK(dev_alloc(h, &p, nb * es.exp, AG_EFF32)); w.e32_exp = (float*)p;
+    CHK(dev_alloc(h, &p, nb * es.dw, AG_EFF32)); w.e32_dw = (float*)p;
+    w.e32_cap_b = h->cap_b;
+  }
+  float* cur = w.e32_a;
+  float* nxt = w.e32_b;
+  {
+    ProfScope ps(h, s, PK_STEM, 2.0 * B * 112 * 112 * 32 * 27, (double)B * (224 * 224 * 3 + 112 * 112 * 32 * 4));
+    HIPCHK(launch_effnet_stem32(img, xf32, h->e_stem_w, h->e_stem_b, cur, B, s));
+  }
+  int H = 112, W = 112;
+  for (const EffBlock& b : h->e_blocks) {
+    const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
+    const float* src = cur;
+    if (b.expand != 1) {
+      ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * b.cin * b.cexp, 4.0 * B * H * W * (b.cin + b.cexp));
+      HIPCHK(launch_pw32(cur, b.e.w32, b.e.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, b.cexp, b.cin, 3 /* SiLU */, s));
+      src = w.e32_exp;
+    }
+    {
+      ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k, 4.0 * B * b.cexp * ((double)H * W + Ho * Wo));
+      HIPCHK(launch_dw32(src, b.wd_t, b.bd, w.e32_dw, B, H, W, b.cexp, b.k, b.stride, s));
+    }
+    {
+      ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, 4.0 * B * b.cexp * ((double)Ho * Wo + 2));
+      // as many pool chunks as the fp16 tower uses for this layer (fits e_pool by construction)
+      const int nch = std::min(dwconv_nchunks(H, W, b.cexp, b.stride), Ho * Wo);
+      HIPCHK(launch_sum32(w.e32_dw, B, Ho * Wo, b.cexp, nch, w.e_pool, s));
+      HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s,
+                       true));
+    }
+    {
+      ProfScope ps(h, s, PK_PW32, 2.0 * B * Ho * Wo * b.cexp * b.cout,
+                   4.0 * B * Ho * Wo * (b.cexp + b.cout * (b.residual ? 2 : 1)));
+      HIPCHK(launch_pw32(w.e32_dw, b.p.w32, b.p.b, w.e_scale, Ho * Wo, b.residual ? cur : nullptr, nxt, B * Ho * Wo,
+                         b.cout, b.cexp, 0, s));
+    }
+    std::swap(cur, nxt);
+    H = Ho;
+    W = Wo;
+  }
+  {
+    ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * 320 * 1280, 4.0 * B * H * W * (320 + 1280));
+    HIPCHK(launch_pw32(cur, h->e_head.w32, h->e_head.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, 1280, 320, 3, s));
+  }
+  ProfScope ps(h, s, PK_GAP, (double)B * H * W * 1280 + 4.0 * B * 1280, (double)B * H * W * 1280 * 4);
+  HIPCHK(launch_gap32(w.e32_exp, H * W, 1280, h->e_cls_w, h->e_cls_b, logits, score, score_stride, B, s));
+  return 0;
+}
+
 int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score, int score_stride,
                hipStream_t s) {
+  if (h->opt.effnet_fp32) return run_effnet32(h, img, xf32, B, logits, score, score_stride, s);
   Workspace& w = h->ws;
   f16_t* cur = w.e_a;
   f16_t* nxt = w.e_b;
@@ -899,6 +1004,7 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   HIPCHK(hipSetDevice(h->device));
   CHK(free_group(h, AG_WS));
   CHK(free_group(h, AG_SIMS));
+  CHK(free_group(h, AG_EFF32));
   h->ws = Workspace();
   h->cap_b = h->cap_lr = h->cap_lc = 0;
   Workspace& w = h->ws;
@@ -937,22 +1043,8 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   CHK(A((void**)&w.sk_vit, w.sk_elems * 4));
   CHK(A((void**)&w.sk_ctext, w.sk_elems * 4));
   // EfficientNet activation sizes per image
-  size_t max_io = 112 * 112 * 32, max_exp = 0, max_dw = 0, max_pool = 0, max_c = 1280;
-  {
-    int H = 112;
-    for (int si = 0; si < 7; ++si)
-      for (int j = 0; j < kStages[si][5]; ++j) {
-        const int e = kStages[si][0], st = j == 0 ? kStages[si][2] : 1;
-        const int cin = j == 0 ? kStages[si][3] : kStages[si][4], cout = kStages[si][4], cexp = cin * e;
-        const int Ho = (H - 1) / st + 1;
-        max_exp = std::max(max_exp, (size_t)H * H * cexp);
-        max_dw = std::max(max_dw, (size_t)Ho * Ho * cexp);
-        max_io = std::max(max_io, (size_t)Ho * Ho * cout);
-        max_pool = std::max(max_pool, (size_t)dwconv_nchunks(H, H, cexp, st) * cexp);
-        H = Ho;
-      }
-    max_exp = std::max(max_exp, (size_t)7 * 7 * 1280);
-  }
+  const EffSizes es = eff_sizes();
+  const size_t max_io = es.io, max_exp = es.exp, max_dw = es.dw, max_pool = es.pool, max_c = 1280;
   CHK(A((void**)&w.e_a, (size_t)B * max_io * 2));
   CHK(A((void**)&w.e_b, (size_t)B * max_io * 2));
   CHK(A((void**)&w.e_exp, (size_t)B * max_exp * 2));

@@ -57,6 +57,11 @@ MMF_DEV float gelu_erf(float x) {
   return fmaf(-fabsf(x), p * e, fmaxf(x, 0.0f));
 }
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QUICK_GELU = 2, ACT_SILU = 3, ACT_RELU = 4 };
+// SiLU as torch's CPU kernel evaluates it (x / (1 + exp(-x)), IEEE division, ~1-ulp exp): the fp32
+// EfficientNet tower (effnet_f32.hip), where approximate transcendentals would be amplified
+MMF_DEV float silu_precise(float x) { return x / (1.0f + expf(-x)); }
+MMF_DEV float act_precise(float x, int act) { return act == ACT_SILU ? silu_precise(x) : x; }
+
 MMF_DEV float act_apply(float x, int act) {
   switch (act) {
     case ACT_GELU: return gelu_erf(x);

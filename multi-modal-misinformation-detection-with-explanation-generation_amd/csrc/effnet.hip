@@ -16,9 +16,13 @@ namespace {
 // One thread per output pixel, all 32 channels; weights transposed in LDS to [tap][channel] so
 // every tap is 8 broadcast float4 reads.  ToTensor + Normalize folded into one FMA per input.
 // F32 = true: input is an already-normalised fp32 NCHW tensor (detector.forward_image signature,
-// misinfo_forensics.py:102-104) instead of uint8 HWC pixels.
-template <bool F32>
-__global__ __launch_bounds__(256) void stem_kernel(const void* src, const float* w, const float* bias, f16_t* out,
+// misinfo_forensics.py:102-104) instead of uint8 HWC pixels.  OT = float: fp32 output for the
+// fp32 tower (option effnet_fp32, effnet_f32.hip).
+__constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
+__constant__ float kStd[3] = {0.229f, 0.224f, 0.225f};
+
+template <bool F32, typename OT = f16_t>
+__global__ __launch_bounds__(256) void stem_kernel(const void* src, const float* w, const float* bias, OT* out,
                                                    int B) {
   const uint8_t* img = (const uint8_t*)src;
   const float* xf = (const float*)src;
@@ -46,7 +50,10 @@ __global__ __launch_bounds__(256) void stem_kernel(const void* src, const float*
       const uint8_t* p = img + (((size_t)bi * 224 + iy) * 224 + ix) * 3;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float v = F32 ? xf[(((size_t)bi * 3 + c) * 224 + iy) * 224 + ix] : fmaf((float)p[c], sc[c], of[c]);
+        // fp32 tower: ToTensor / Normalize evaluated as torchvision does ((u / 255 - mean) / std)
+        const float v = F32 ? xf[(((size_t)bi * 3 + c) * 224 + iy) * 224 + ix]
+                        : sizeof(OT) == 4 ? ((float)p[c] / 255.0f - kMean[c]) / kStd[c]
+                                          : fmaf((float)p[c], sc[c], of[c]);
         const float4* wr = reinterpret_cast<const float4*>(sw + (c * 9 + ky * 3 + kx) * 32);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -58,6 +65,14 @@ __global__ __launch_bounds__(256) void stem_kernel(const void* src, const float*
         }
       }
     }
+  }
+  if constexpr (sizeof(OT) == 4) {
+    float4* dst = reinterpret_cast<float4*>(out + pix * 32);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      dst[q] = make_float4(silu_precise(acc[q * 4]), silu_precise(acc[q * 4 + 1]), silu_precise(acc[q * 4 + 2]),
+                           silu_precise(acc[q * 4 + 3]));
+    return;
   }
   uint4* dst = reinterpret_cast<uint4*>(out + pix * 32);
 #pragma unroll
@@ -538,6 +553,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
 //          so consecutive threads read consecutive addresses)
 constexpr int SE_THREADS = 1024;
 
+template <bool PRECISE>
 __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, int nchunks, float inv_hw,
                                                         const float* w1, const float* b1, const float* w2t,
                                                         const float* b2, float* scale, int C, int Csq) {
@@ -581,7 +597,7 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
     for (int t = 0; t < OPW; ++t) {
       const int o = wave + 16 * t;
       const float a = wave_sum(acc[t]);
-      if (o < Csq && lane == 0) s1[o] = act_apply(a + b1[o], ACT_SILU);
+      if (o < Csq && lane == 0) s1[o] = PRECISE ? silu_precise(a + b1[o]) : act_apply(a + b1[o], ACT_SILU);
     }
   }
   __syncthreads();
@@ -690,6 +706,14 @@ hipError_t launch_effnet_stem_f32(const float* x, const float* w, const float* b
   return hipGetLastError();
 }
 
+hipError_t launch_effnet_stem32(const uint8_t* img, const float* x, const float* w, const float* bias, float* out,
+                                int B, hipStream_t s) {
+  const dim3 grid((unsigned)(((size_t)B * 112 * 112 + 255) / 256)), blk(256);
+  if (x) hipLaunchKernelGGL((stem_kernel<true, float>), grid, blk, 0, s, (const void*)x, w, bias, out, B);
+  else hipLaunchKernelGGL((stem_kernel<false, float>), grid, blk, 0, s, (const void*)img, w, bias, out, B);
+  return hipGetLastError();
+}
+
 // tile edge: the largest divisor of the output edge up to 16 (stride 1) / 8 (stride 2)
 static void dw_geometry(int H, int W, int C, int stride, int* T_, int* CW_, int* tiles_x_, int* ntiles_) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
@@ -794,9 +818,15 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
 }
 
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
-                     const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s) {
+                     const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s,
+                     bool precise) {
   if (C > 1280 || Csq > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(se_kernel, dim3(B), dim3(SE_THREADS), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2, b2, scale, C, Csq);
+  if (precise)
+    hipLaunchKernelGGL(se_kernel<true>, dim3(B), dim3(SE_THREADS), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2, b2,
+                       scale, C, Csq);
+  else
+    hipLaunchKernelGGL(se_kernel<false>, dim3(B), dim3(SE_THREADS), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2, b2,
+                       scale, C, Csq);
   return hipGetLastError();
 }
 

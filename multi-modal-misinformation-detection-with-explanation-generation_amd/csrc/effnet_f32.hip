@@ -1,0 +1,204 @@
+// EfficientNet-B0 tower in fp32 end to end (process/handle option "effnet_fp32"): activations NHWC
+// fp32, 1x1 convolutions as fp32-FMA GEMMs, depthwise convs and pooling in fp32.  The default
+// tower (effnet.hip + the fp16 MFMA GEMM) stores activations in fp16; that is within the north-star
+// 1e-3 for a trained / BN-conditioned network, but a tower whose logits reach O(100) (random He
+// fan_in convolutions with unit running statistics) amplifies fp16 storage rounding
+// past it.  This path trades ~3x the tower time for fp32 rounding throughout (the torch fp32 eval
+// forward of torchvision's EfficientNet-B0 that misinfo_forensics.py:95-104 runs).
+//   pw32     C = act((A * scale[image]) W^T + bias) (+ residual): the expand / project / head convs
+//   dw32     depthwise kxk + BN + SiLU, one thread per (output pixel, 4 channels); weights
+//            tap-major [k*k][C] so a thread's 4 channels are one float4
+//   sum32    per-(image, pixel chunk, channel) sums in a fixed order -> the SE pool partials
+//   gap32    global average pool + Linear(1280, 2) + softmax[:, 1]
+// The stem is effnet.hip's stem kernel with fp32 output; the SE is effnet.hip's se kernel.  Every
+// SiLU / sigmoid here is the IEEE-division, full-precision-exp form torch's CPU kernels use
+// (silu_precise): the towers this mode exists for amplify ~1e-7 relative perturbations to ~1e-4.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// 64 x 64 output tile, K in steps of 16 staged through LDS ([k][m] / [k][n], so each thread's 4
+// rows and 4 columns are one float4 read each); thread (ty, tx) owns rows ty*4.. and cols tx*4..
+constexpr int PB = 64, PK = 16;
+
+__global__ __launch_bounds__(256) void pw32_kernel(const float* __restrict__ A, const float* __restrict__ Wt,
+                                                   const float* __restrict__ bias, const float* __restrict__ ascale,
+                                                   int rows_per_image, const float* __restrict__ res,
+                                                   float* __restrict__ C, int M, int N, int K, int act) {
+  __shared__ __attribute__((aligned(16))) float As[PK][PB + 4];
+  __shared__ __attribute__((aligned(16))) float Ws[PK][PB + 4];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.x * PB, n0 = blockIdx.y * PB;
+  // loader: thread -> (row lr, k quad lq) of the 64 x 16 slab
+  const int lr = tid >> 2, lq = (tid & 3) * 4;
+  const int am = m0 + lr, wn = n0 + lr;
+  const float* sc = (ascale && am < M) ? ascale + (size_t)(am / rows_per_image) * K : nullptr;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += PK) {
+    const int k = k0 + lq;  // K % 4 == 0 (checked by the launcher): a quad is in or out whole
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), w = a;
+    if (am < M && k < K) {
+      a = *reinterpret_cast<const float4*>(A + (size_t)am * K + k);
+      if (sc) {
+        const float4 s = *reinterpret_cast<const float4*>(sc + k);
+        a.x *= s.x; a.y *= s.y; a.z *= s.z; a.w *= s.w;
+      }
+    }
+    if (wn < N && k < K) w = *reinterpret_cast<const float4*>(Wt + (size_t)wn * K + k);
+    __syncthreads();
+    As[lq][lr] = a.x; As[lq + 1][lr] = a.y; As[lq + 2][lr] = a.z; As[lq + 3][lr] = a.w;
+    Ws[lq][lr] = w.x; Ws[lq + 1][lr] = w.y; Ws[lq + 2][lr] = w.z; Ws[lq + 3][lr] = w.w;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < PK; ++kk) {
+      const float4 av = *reinterpret_cast<const float4*>(&As[kk][ty * 4]);
+      const float4 wv = *reinterpret_cast<const float4*>(&Ws[kk][tx * 4]);
+      const float ar[4] = {av.x, av.y, av.z, av.w}, wr[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(ar[i], wr[j], acc[i][j]);
+    }
+  }
+  const int n = n0 + tx * 4;
+  if (n >= N) return;  // N % 4 == 0
+  const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) break;
+    float o[4] = {acc[i][0] + bv.x, acc[i][1] + bv.y, acc[i][2] + bv.z, acc[i][3] + bv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = act_precise(o[j], act);
+    if (res) {
+      const float4 r = *reinterpret_cast<const float4*>(res + (size_t)m * N + n);
+      o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
+    }
+    *reinterpret_cast<float4*>(C + (size_t)m * N + n) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// torchvision pads (k - 1) / 2 on every side; output edge (H - 1) / S + 1
+template <int K, int S>
+__global__ __launch_bounds__(256) void dw32_kernel(const float* __restrict__ in, const float* __restrict__ w,
+                                                   const float* __restrict__ bias, float* __restrict__ out, int H,
+                                                   int W, int C, int Ho, int Wo, size_t total4) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int C4 = C / 4, c4 = (int)(i % C4);
+  const size_t pix = i / C4;
+  const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho), bi = (int)(pix / ((size_t)Wo * Ho));
+  const int c = c4 * 4;
+  float acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = bias[c + j];
+  constexpr int P = (K - 1) / 2;
+#pragma unroll
+  for (int ky = 0; ky < K; ++ky) {
+    const int iy = oy * S - P + ky;
+    if (iy < 0 || iy >= H) continue;
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) {
+      const int ix = ox * S - P + kx;
+      if (ix < 0 || ix >= W) continue;
+      const float4 v = *reinterpret_cast<const float4*>(in + (((size_t)bi * H + iy) * W + ix) * C + c);
+      const float4 wt = *reinterpret_cast<const float4*>(w + (size_t)(ky * K + kx) * C + c);
+      acc[0] = fmaf(v.x, wt.x, acc[0]);
+      acc[1] = fmaf(v.y, wt.y, acc[1]);
+      acc[2] = fmaf(v.z, wt.z, acc[2]);
+      acc[3] = fmaf(v.w, wt.w, acc[3]);
+    }
+  }
+  *reinterpret_cast<float4*>(out + pix * C + c) =
+      make_float4(silu_precise(acc[0]), silu_precise(acc[1]), silu_precise(acc[2]), silu_precise(acc[3]));
+}
+
+// grid (ceil(C / 64), nchunks, B): chunk j covers pixels [j HW / nchunks, (j + 1) HW / nchunks);
+// 4 pixel lanes x 64 channels, each lane sums its pixels in order, then the 4 lane sums are added
+// in a fixed order (deterministic) -> part[b][j][c]
+__global__ __launch_bounds__(256) void sum32_kernel(const float* __restrict__ x, int HW, int C,
+                                                    float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int bi = blockIdx.z, j = blockIdx.y, nch = gridDim.y;
+  const int cl = threadIdx.x & 63, r = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  const int p0 = (int)((long)j * HW / nch), p1 = (int)((long)(j + 1) * HW / nch);
+  float s = 0.f;
+  if (c < C)
+    for (int p = p0 + r; p < p1; p += 4) s += x[((size_t)bi * HW + p) * C + c];
+  red[r][cl] = s;
+  __syncthreads();
+  if (r == 0 && c < C)
+    part[((size_t)bi * nch + j) * C + c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
+__global__ __launch_bounds__(256) void gap32_kernel(const float* __restrict__ x, int HW, int C,
+                                                    const float* __restrict__ w, const float* __restrict__ b,
+                                                    float* logits, float* score, int score_stride) {
+  __shared__ float red[2][4];
+  const int bi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float inv = 1.0f / (float)HW;
+  float l0 = 0.f, l1 = 0.f;
+  for (int c = tid; c < C; c += 256) {
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += x[((size_t)bi * HW + p) * C + c];
+    l0 = fmaf(w[c], s * inv, l0);
+    l1 = fmaf(w[C + c], s * inv, l1);
+  }
+  l0 = wave_sum(l0);
+  l1 = wave_sum(l1);
+  if (lane == 0) { red[0][wave] = l0; red[1][wave] = l1; }
+  __syncthreads();
+  if (tid == 0) {
+    const float a = red[0][0] + red[0][1] + red[0][2] + red[0][3] + b[0];
+    const float c1 = red[1][0] + red[1][1] + red[1][2] + red[1][3] + b[1];
+    if (logits) { logits[bi * 2] = a; logits[bi * 2 + 1] = c1; }
+    if (score) {
+      const float m = fmaxf(a, c1), e0 = expf(a - m), e1 = expf(c1 - m);
+      score[(size_t)bi * score_stride] = e1 / (e0 + e1);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_pw32(const float* A, const float* W, const float* bias, const float* ascale, int rows_per_image,
+                       const float* res, float* C, int M, int N, int K, int act, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || (N % 4) || (K % 4) || (ascale && rows_per_image <= 0) ||
+      (act != ACT_NONE && act != ACT_SILU))
+    return hipErrorInvalidValue;
+  const dim3 grid((M + PB - 1) / PB, (N + PB - 1) / PB);
+  hipLaunchKernelGGL(pw32_kernel, grid, dim3(256), 0, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act);
+  return hipGetLastError();
+}
+
+hipError_t launch_dw32(const float* in, const float* w, const float* bias, float* out, int B, int H, int W, int C,
+                       int k, int stride, hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const size_t total4 = (size_t)B * Ho * Wo * (C / 4);
+  const dim3 grid((unsigned)((total4 + 255) / 256)), blk(256);
+#define MMF_DW32(KK, SS)                                                                                     \
+  if (k == KK && stride == SS) {                                                                             \
+    hipLaunchKernelGGL((dw32_kernel<KK, SS>), grid, blk, 0, s, in, w, bias, out, H, W, C, Ho, Wo, total4);   \
+    return hipGetLastError();                                                                                \
+  }
+  MMF_DW32(3, 1)
+  MMF_DW32(3, 2)
+  MMF_DW32(5, 1)
+  MMF_DW32(5, 2)
+#undef MMF_DW32
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_sum32(const float* x, int B, int HW, int C, int nchunks, float* part, hipStream_t s) {
+  if (nchunks < 1 || nchunks > HW) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sum32_kernel, dim3((C + 63) / 64, nchunks, B), dim3(256), 0, s, x, HW, C, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_gap32(const float* x, int HW, int C, const float* w, const float* b, float* logits, float* score,
+                        int score_stride, int B, hipStream_t s) {
+  hipLaunchKernelGGL(gap32_kernel, dim3(B), dim3(256), 0, s, x, HW, C, w, b, logits, score, score_stride);
+  return hipGetLastError();
+}

@@ -113,7 +113,8 @@ hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const fl
 hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16_t* out, float* pool_part,
                          int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
-                     const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s);
+                     const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s,
+                     bool precise = false);  // precise: the fc1 SiLU in silu_precise form (fp32 tower)
 hipError_t launch_gap_classifier(const f16_t* x, int HW, int C, const float* w, const float* b, float* logits,
                                  float* score, int score_stride, int B, hipStream_t s);
 hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);
@@ -125,3 +126,17 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
                             int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 // number of pool-partial chunks launch_dwconv uses for an output of Ho x Wo with C channels
 int dwconv_nchunks(int H, int W, int C, int stride);
+
+// fp32 EfficientNet tower (option effnet_fp32, effnet_f32.hip): NHWC fp32 activations
+hipError_t launch_effnet_stem32(const uint8_t* img, const float* x_nchw, const float* w, const float* bias,
+                                float* out, int B, hipStream_t s);
+// C[M][N] = act((A .* ascale[m / rows_per_image]) W^T + bias) (+ res); W fp32 [N][K]; N, K % 4 == 0
+hipError_t launch_pw32(const float* A, const float* W, const float* bias, const float* ascale, int rows_per_image,
+                       const float* res, float* C, int M, int N, int K, int act, hipStream_t s);
+// w tap-major [k*k][C]
+hipError_t launch_dw32(const float* in, const float* w, const float* bias, float* out, int B, int H, int W, int C,
+                       int k, int stride, hipStream_t s);
+// part[b][j][c] = sum over pixel chunk j of nchunks (the SE's pool partials)
+hipError_t launch_sum32(const float* x, int B, int HW, int C, int nchunks, float* part, hipStream_t s);
+hipError_t launch_gap32(const float* x, int HW, int C, const float* w, const float* b, float* logits, float* score,
+                        int score_stride, int B, hipStream_t s);

@@ -45,6 +45,24 @@ def test_effnet_signal(engine, golden, golden_inputs):
     np.testing.assert_allclose(sc.cpu().numpy(), _sm1(golden["effnet_logits"]), atol=TOL)
 
 
+def test_effnet_fp32_tower_vs_golden(engine, golden, golden_inputs):
+    """The fp32 tower (option effnet_fp32) against the reference-generated logits: fp32 rounding
+    throughout, so the logits themselves agree to ~1e-4 (the fp16 tower is checked on its scores)."""
+    engine.set_option("effnet_fp32", 1)
+    try:
+        lg, sc = engine.effnet_forward(golden_inputs["imgs"])
+        x = torch.as_tensor(golden_inputs["imgs"]).permute(0, 3, 1, 2).float().div(255.0)
+        mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+        std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+        lgf, _ = engine.effnet_forward_f32(((x - mean) / std).contiguous())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_option("effnet_fp32", 0)
+    np.testing.assert_allclose(lg.cpu().numpy(), golden["effnet_logits"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(lgf.cpu().numpy(), golden["effnet_logits"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(sc.cpu().numpy(), _sm1(golden["effnet_logits"]), atol=1e-5)
+
+
 def test_clip_embeddings(engine, golden, golden_inputs):
     ie = engine.clip_image(golden_inputs["imgs"]).cpu().numpy()
     te = engine.clip_text(golden["clip_ids"], golden["clip_mask"]).cpu().numpy()
