@@ -254,7 +254,7 @@ MMF_DEV void tile_coords(int t, int tilesM, int tilesN, int gm, int& tm, int& tn
   tn = r / gsz;
 }
 
-template <int BM, int BN, int WGM, int WGN, int ACT>
+template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false>
 __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
                                                                      int gm) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
@@ -319,7 +319,39 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
       else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
       const f16_t* Xs = lds + cur * STAGE;
       const f16_t* Ws = Xs + BM * BK;
-      if constexpr (BN == 192) {
+      if constexpr (PIPE2) {
+        // half-step pipeline: the second K-half's fragment reads are issued between the first
+        // half's MFMAs (1 read per 2 MFMAs), so only the first half's reads are exposed after the
+        // barrier
+        f16x8 w0[NI], x0[MI], w1[NI], x1[MI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) w0[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, fg)));
+#pragma unroll
+        for (int j = 0; j < MI; ++j) x0[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, fg)));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          w1[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, 4 + fg)));
+#pragma unroll
+        for (int j = 0; j < MI; ++j)
+          x1[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, 4 + fg)));
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(w0[i], x0[j], acc[i][j]);
+#pragma unroll
+        for (int q = 0; q < NI + MI; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NI * MI - 2 * (NI + MI), 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(w1[i], x1[j], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (BN == 192) {
         // 256x192 (wave tile 64x96): all 20 fragment reads of the K-step first, then its 48 MFMAs,
         // then the barrier -- pinned with sched_barriers (hipcc otherwise interleaves 2 reads +
         // lgkmcnt(0) per 8 MFMAs and sinks MFMAs below the barrier's vmcnt(0)).  Measured: these
@@ -444,7 +476,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   }
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false>
 hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
@@ -454,7 +486,7 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int gm = a.group_m;  // tile-order option (handle option "gemm_group_m"; 0 = row-major)
 #define MMF_GLDS_CASE(ACT)                                                                                  \
   case ACT:                                                                                                 \
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT>), dim3(grid), blk, 0, s, a, tilesN, tiles, tilesM, \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2>), dim3(grid), blk, 0, s, a, tilesN, tiles, tilesM, \
                        gm);                                                                                      \
     break;
   switch (a.act) {
@@ -549,9 +581,9 @@ static int forced_config(const GemmArgs& a) {
   // handle option "gemm_config" (benchmarking override, tools/gemm_bench.py); ignored if inapplicable
   if (a.force_cfg <= 0) return -1;
   const int c = a.force_cfg - 1;
-  if (c >= 4 && c <= 8 && !glds_ok(a)) return -1;
+  if (((c >= 4 && c <= 8) || c >= 10) && !glds_ok(a)) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
-  return (c >= 0 && c <= 9) ? c : -1;
+  return (c >= 0 && c <= 11) ? c : -1;
 }
 
 int gemm_config(const GemmArgs& a) {
@@ -564,10 +596,11 @@ int gemm_config(const GemmArgs& a) {
   if (glds_ok(a) && a.N >= 128) {
     // persistent 256-row LDS-DMA tiles: pick the column tile that minimises whole "rounds" of
     // 256 CUs x per-tile time (wider tiles are more efficient per flop)
+    // (the 256- and 192-column tiles run the half-step-pipelined K loop, configs 11 / 10)
     const long tm = (a.M + 255) / 256;
-    const int bns[3] = {256, 192, 128}, cfg[3] = {4, 6, 5};
-    const double eff[3] = {1.0, 0.97, 0.80};  // measured per-flop efficiency (tools/gemm_bench.py)
-    int best = 4;
+    const int bns[3] = {256, 192, 128}, cfg[3] = {11, 10, 5};
+    const double eff[3] = {1.0, 0.88, 0.80};  // measured per-flop efficiency (tools/gemm_bench.py)
+    int best = 11;
     double bc = 1e30;
     for (int i = 0; i < 3; ++i) {
       const long tiles = tm * ((a.N + bns[i] - 1) / bns[i]);
@@ -594,8 +627,8 @@ const char* gemm_config_name(int c) {
   static const char* names[] = {"gemm_f16<256,32,4,1>",  "gemm_f16<256,64,4,1>",  "gemm_f16<64,128,1,4>",
                                 "gemm_f16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
                                 "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
-                                "pw_conv"};
-  return (c >= 0 && c < 10) ? names[c] : "gemm_f16<?>";
+                                "pw_conv", "gemm_glds_pipe2<256,192,4,2>", "gemm_glds_pipe2<256,256,2,4>"};
+  return (c >= 0 && c < 12) ? names[c] : "gemm_f16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
@@ -616,6 +649,8 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
     case 7: return run_glds<128, 192, 2, 2>(a, s);
     case 8: return run_glds<128, 128, 2, 2>(a, s);
     case 9: return launch_pw(a, s);
+    case 10: return run_glds<256, 192, 4, 2, true>(a, s);
+    case 11: return run_glds<256, 256, 2, 4, true>(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

@@ -54,12 +54,14 @@ def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:
 
 def kind_symbol(kind: str) -> str:
     """Event-profile kind -> kernel symbol as rocprofv3 prints it (GEMM kinds only)."""
-    m = re.match(r"gemm_(glds|f16)<([\d,]+)> act=(\d)", kind)
+    m = re.match(r"gemm_(glds|glds_pipe2|f16)<([\d,]+)> act=(\d)", kind)
     if not m:
         return kind
     dims = m.group(2).split(",")
     if m.group(1) == "glds":
         return f"gemm_glds_kernel<{', '.join(dims + [m.group(3)])}>"
+    if m.group(1) == "glds_pipe2":
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true'])}>"
     return f"gemm_f16_kernel<{', '.join(dims)}>"
 
 
