@@ -29,10 +29,11 @@ MMF_DEV int kv_swz(int key, int kc) { return key * 64 + ((kc ^ (key & 7)) << 3);
 // LK = keys padded to the 32-deep PV k-step, a compile-time constant (32 / 64 / 96 / 128) so the
 // key-tile loops carry no runtime bounds: the K-fragment reads of a query tile batch up ahead of
 // its MFMAs instead of sitting in one basic block per key tile.
-template <int LK>
+// CAUSAL (CLIP text) is compile-time too: the bidirectional encoders carry no per-score compare.
+template <int LK, bool CAUSAL>
 __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restrict__ qkv, int ld,
                                                         const int32_t* __restrict__ mask, f16_t* __restrict__ out,
-                                                        int ldo, int L, int H, int causal) {
+                                                        int ldo, int L, int H) {
   __shared__ __attribute__((aligned(16))) f16_t Ks[LK * 64];
   __shared__ __attribute__((aligned(16))) f16_t Vs[LK * 64];
   __shared__ __attribute__((aligned(16))) float kbias[LK];
@@ -100,7 +101,10 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restri
         s[j] = mfma16x16x32(kf, qf[ks], s[j]);
       }
     }
-    // masked softmax over keys (fp32), scale 1/sqrt(64)
+    // masked softmax over keys (fp32), scale 1/sqrt(64), in the exp2 domain: one FMA per score
+    // (scale * log2 e and the mask bias) and one v_exp_f32 per exponential.  P stays unnormalised
+    // (<= 1, rounded to fp16 for the PV MFMA) and O is divided by the row sum at the store.
+    constexpr float kScaleLog2e = 0.125f * 1.44269504088896341f;
     const int qq = qt * 16 + fr;
     float mx = -INFINITY;
 #pragma unroll
@@ -109,20 +113,21 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restri
       const float kbr[4] = {kb.x, kb.y, kb.z, kb.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = s[j][r] * 0.125f + kbr[r];
-        if (causal && j * 16 + fg * 4 + r > qq) v = -INFINITY;
+        float v = fmaf(s[j][r], kScaleLog2e, kbr[r]);
+        if (CAUSAL && j * 16 + fg * 4 + r > qq) v = -INFINITY;
         s[j][r] = v;
         mx = fmaxf(mx, v);
       }
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (mx == -INFINITY) mx = 0.f;  // every key masked: all exponentials 0, sum 0, output 0
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < NKT; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = (mx == -INFINITY) ? 0.f : __expf(s[j][r] - mx);
+        const float e = __builtin_amdgcn_exp2f(s[j][r] - mx);
         s[j][r] = e;
         sum += e;
       }
@@ -138,10 +143,9 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restri
 #pragma unroll
     for (int kb = 0; kb < LK / 32; ++kb) {
       {
-        const uint4 pk = make_uint4(pack2h(s[2 * kb][0] * inv, s[2 * kb][1] * inv),
-                                    pack2h(s[2 * kb][2] * inv, s[2 * kb][3] * inv),
-                                    pack2h(s[2 * kb + 1][0] * inv, s[2 * kb + 1][1] * inv),
-                                    pack2h(s[2 * kb + 1][2] * inv, s[2 * kb + 1][3] * inv));
+        const uint4 pk = make_uint4(pack2h(s[2 * kb][0], s[2 * kb][1]), pack2h(s[2 * kb][2], s[2 * kb][3]),
+                                    pack2h(s[2 * kb + 1][0], s[2 * kb + 1][1]),
+                                    pack2h(s[2 * kb + 1][2], s[2 * kb + 1][3]));
         const f16x8 pf = as_f16x8(pk);
         // A operand V^T[d = dt*16 + fr][keys 32kb + 4fg + 0..3 | 32kb + 16 + 4fg + 0..3]: lane
         // 4q + p of each 16-lane group addresses key row (.. + q), dims dt*16 + 4p .. +3
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restri
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         *reinterpret_cast<uint2*>(dst + dt * 16) =
-            make_uint2(pack2h(o[dt][0], o[dt][1]), pack2h(o[dt][2], o[dt][3]));
+            make_uint2(pack2h(o[dt][0] * inv, o[dt][1] * inv), pack2h(o[dt][2] * inv, o[dt][3] * inv));
     }
     qf[0] = qfa[1][0];
     qf[1] = qfa[1][1];
@@ -328,8 +332,9 @@ hipError_t launch_attention(const f16_t* qkv, int ldqkv, const int32_t* mask, f1
                        causal);
     return hipGetLastError();
   }
-#define MMF_ATTN(LK) \
-  hipLaunchKernelGGL(attention_kernel<LK>, dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H, causal)
+#define MMF_ATTN(LK)                                                                                              \
+  if (causal) hipLaunchKernelGGL((attention_kernel<LK, true>), dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H); \
+  else hipLaunchKernelGGL((attention_kernel<LK, false>), dim3(B * H), dim3(256), 0, s, qkv, ldqkv, mask, out, ldo, L, H)
   switch ((L + 31) >> 5) {  // keys padded to 32
     case 1: MMF_ATTN(32); break;
     case 2: MMF_ATTN(64); break;
