@@ -113,6 +113,7 @@ struct Options {
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
+  int gemm_prio = 2;    // s_setprio 1 for waves 0-3 of the persistent GEMM (+0.4 % step; A/B)
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
@@ -120,7 +121,7 @@ const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
     {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"}, {"dw_ct", &Options::dw_ct, "MMF_DW_CT"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
-    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
+    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -138,6 +139,7 @@ void apply_options(const Options& o, GemmArgs* g) {
   g->force_cfg = o.gemm_config >= 0 ? o.gemm_config + 1 : 0;
   g->no_splitk = o.gemm_splitk ? 0 : 1;
   g->group_m = o.gemm_group_m;
+  g->prio = o.gemm_prio;
 }
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the

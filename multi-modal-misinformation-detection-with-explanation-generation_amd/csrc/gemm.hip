@@ -291,6 +291,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
 
   int t = wgid;
   if (t >= tiles) return;
+  if ((g.prio == 1 && wave >= NW / 2) || (g.prio == 2 && wave < NW / 2)) __builtin_amdgcn_s_setprio(1);
   auto stage = [&](int buf, int tile, int kt) {
     int tm_, tn_;
     tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);

@@ -22,6 +22,7 @@ struct GemmArgs {
   int force_cfg;                 // 0 = automatic tile choice, c + 1 = instantiation c (A/B option)
   int no_splitk;                 // 1 = never split K on the skinny-M path (A/B option)
   int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
+  int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
 };

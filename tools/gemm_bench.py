@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
     ap.add_argument("--round", action="store_true", help="one 256-tile round at K = 256 .. 6144")
     ap.add_argument("--group-m", default="", help="extra timed pass per config per gemm_group_m value (comma list)")
+    ap.add_argument("--opt", default="gemm_group_m", help="process option swept by --vals (default gemm_group_m)")
+    ap.add_argument("--vals", default="", help="extra timed pass per config per value of --opt (comma list)")
     a = ap.parse_args()
     lib = hip.load()
     dev = torch.device("cuda")
@@ -108,13 +110,15 @@ def main():
             hip.check(lib.mmf_gemm_f16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None, hip.ptr(c32),
                                         hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
         row = {"shape": name, "M": M, "N": N, "K": K}
-        for gm in [""] + [g for g in a.group_m.split(",") if g]:
-            hip.set_process_option("gemm_group_m", int(gm or 0))
+        opt = "gemm_group_m" if a.group_m else a.opt
+        vals = a.group_m or a.vals
+        for v in [""] + [x for x in vals.split(",") if x]:
+            hip.set_process_option(opt, int(v or 0))
             for cfg in a.configs.split(","):
                 force(cfg)
                 us = timed_us(call, a.iters)
-                row[(f"gm{gm}:" if gm else "") + cfg] = round(2.0 * M * N * K / (us / 1e6) / 1e12, 1)
-        hip.set_process_option("gemm_group_m", 0)
+                row[(f"{opt}={v}:" if v else "") + cfg] = round(2.0 * M * N * K / (us / 1e6) / 1e12, 1)
+        hip.set_process_option(opt, 0)
         force("auto")
         print(json.dumps(row), flush=True)
 
