@@ -611,9 +611,7 @@ class MisinfoForensics:
         rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
         self._fit_text(rid.shape[1])
         cid, cm = self._clip_ids(list(texts))
-        pils = [io_utils.to_pil(i) for i in images]
-        eff = np.stack([io_utils.effnet_pixels(p) for p in pils])
-        clp = np.stack([io_utils.clip_pixels(p) for p in pils])
+        eff, clp = io_utils.decode_batch(images)  # one decode per image, both geometries, threaded
         same = bool(np.array_equal(eff, clp))
         out = self.analyze_batch(rid, rm, cid, cm, eff, None if same else clp)
         return self.batch_to_dicts(out)

@@ -46,6 +46,34 @@ def clip_pixels(img) -> np.ndarray:
     return np.asarray(img, dtype=np.uint8)
 
 
+def _decode_one(args):
+    i, item, eff, clp = args
+    pil = to_pil(Image.open(io.BytesIO(item)) if isinstance(item, (bytes, bytearray)) else item)
+    eff[i] = effnet_pixels(pil)
+    clp[i] = clip_pixels(pil)
+
+
+def decode_batch(images, workers: Optional[int] = None, out: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+    """Host input stage of a batch: each image (path, PIL image or encoded bytes) is
+    decoded once and resampled to both towers' geometries -- EfficientNet's squash-resize and CLIP's
+    shortest-edge resize + centre crop -- straight into uint8 [B,224,224,3] arrays (e.g. pinned
+    staging buffers passed as `out`).  Pillow's decoders and resamplers release the GIL, so a thread
+    pool scales over the host cores; results equal the serial per-image path bit for bit."""
+    n = len(images)
+    eff, clp = out if out is not None else (np.empty((n, 224, 224, 3), np.uint8), np.empty((n, 224, 224, 3), np.uint8))
+    if workers is None:
+        workers = min(n, len(os.sched_getaffinity(0)), 16)
+    jobs = [(i, im, eff, clp) for i, im in enumerate(images)]
+    if workers <= 1 or n <= 1:
+        for j in jobs:
+            _decode_one(j)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=workers) as ex:
+            list(ex.map(_decode_one, jobs))
+    return eff, clp
+
+
 def pad_ids(seqs: List[List[int]], pad_id: int, length: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
     L = length or max(len(s) for s in seqs)
     ids = np.full((len(seqs), L), pad_id, dtype=np.int32)
