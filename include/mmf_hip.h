@@ -100,6 +100,17 @@ int mmf_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
 int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, const int32_t* mask, int B, int L,
                          float* img_emb, float* txt_emb, float* sim, void* stream);
 
+/* Host-input geometry on the device (misinfo_forensics.py:249-253 and the
+ * CLIPImageProcessor the reference calls at :386-401): B decoded uint8 images (HWC, pixel_bytes =
+ * 3 for RGB or 4 for RGBX -- Pillow's in-memory layout --, any size up to a 47x downscale)
+ * concatenated in device memory at byte offsets[i] with sizes wh[2i] = width, wh[2i+1] = height
+ * (host arrays) -> out_effnet uint8 [B,224,224,3] =
+ * Image.resize((224,224), BILINEAR) and out_clip uint8 [B,224,224,3] = shortest edge -> 224 BICUBIC
+ * + centre crop, both bit-exact with Pillow's resampler (either output may be NULL).  Returns after
+ * the work on `stream` has completed. */
+int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, const int32_t* wh, int B,
+                   int pixel_bytes, uint8_t* out_effnet, uint8_t* out_clip, void* stream);
+
 /* Truth-Vault (misinfo_forensics.py:214-246, 443-445): host fp32 [N, D=512] raw embeddings; rows
  * are L2-normalised once here instead of on every search call. */
 int mmf_set_vault(mmf_handle* h, const float* host_vault, int N, int D);

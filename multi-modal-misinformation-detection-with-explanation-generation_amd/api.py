@@ -25,6 +25,7 @@ import torch.nn as nn
 
 from . import explain, io_utils, weights as W
 from .engine import Engine, SCORE_KEYS
+from .hip import MMFError
 
 _DEFAULT_CLIP_DIR = r"C:\Users\Lenovo\OneDrive\Desktop\hack\models\clip-vit-b32"
 
@@ -607,13 +608,18 @@ class MisinfoForensics:
             for i in range(0, len(texts), cap):
                 res.extend(self.analyze_pairs(texts[i:i + cap], images[i:i + cap]))
             return res
-        rob = [io_utils.tokenize_roberta(self.roberta_tokenizer, t) for t in texts]
+        rob = io_utils.tokenize_roberta_batch(self.roberta_tokenizer, texts)
         rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
         self._fit_text(rid.shape[1])
         cid, cm = self._clip_ids(list(texts))
-        eff, clp = io_utils.decode_batch(images)  # one decode per image, both geometries, threaded
-        same = bool(np.array_equal(eff, clp))
-        out = self.analyze_batch(rid, rm, cid, cm, eff, None if same else clp)
+        # decode on the host (threaded), resample to both towers' windows on the device
+        # (Pillow-exact); images past the device resampler's 47x downscale take the host path
+        rgb = io_utils.decode_rgb(images)
+        try:
+            eff, clp = self.engine.resize_images(rgb)
+        except MMFError:
+            eff, clp = io_utils.decode_batch([io_utils.Image.fromarray(a) for a in rgb])
+        out = self.analyze_batch(rid, rm, cid, cm, eff, clp)
         return self.batch_to_dicts(out)
 
     def analyze_batch(self, rob_ids, rob_mask, clip_ids, clip_mask, images_u8, clip_images_u8=None,

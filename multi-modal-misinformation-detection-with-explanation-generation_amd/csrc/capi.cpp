@@ -144,7 +144,7 @@ void apply_options(const Options& o, GemmArgs* g) {
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the
 // workspaces) frees exactly what it replaces.
-enum AllocGroup { AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_EFF32, AG_COUNT };
+enum AllocGroup { AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_EFF32, AG_RESIZE, AG_COUNT };
 
 }  // namespace
 
@@ -197,6 +197,14 @@ struct mmf_handle {
   // fork/join streams of mmf_analyze_batch (text, effnet, clip-text towers beside the caller's)
   hipStream_t tower[3] = {nullptr, nullptr, nullptr};
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
+  // mmf_resize_pil workspaces (grow-only, group AG_RESIZE)
+  struct ResizeWs {
+    ResizeJob* jobs = nullptr;
+    uint8_t** outs = nullptr;
+    int32_t *coef = nullptr, *bounds = nullptr;
+    uint8_t* tmp = nullptr;
+    size_t cap_jobs = 0, cap_coef = 0, cap_tmp = 0;
+  } rs;
 
   ~mmf_handle() {
     for (auto& g : groups)
@@ -1316,6 +1324,118 @@ int mmf_get_option(mmf_handle* h, const char* name, int* value) {
       return 0;
     }
   return fail(MMF_EINVAL, "unknown option '%s'", name);
+}
+
+namespace {
+// Pillow's support / taps / bounds on the host (the same double arithmetic as Resample.c) for the
+// window bookkeeping; the coefficients themselves are computed on the device (resize.hip)
+struct AxisPlan { double scale, support; int ks; };
+AxisPlan axis_plan(int in_size, int out_size, int filt) {
+  AxisPlan a;
+  a.scale = (double)(float)in_size / out_size;
+  const double fs = a.scale < 1.0 ? 1.0 : a.scale;
+  a.support = (filt ? 2.0 : 1.0) * fs;
+  a.ks = (int)std::ceil(a.support) * 2 + 1;
+  return a;
+}
+void tap_range(const AxisPlan& a, int in_size, int xx, int* lo, int* hi) {
+  const double center = (xx + 0.5) * a.scale;
+  int xmin = (int)(center - a.support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + a.support + 0.5);
+  if (xmax > in_size) xmax = in_size;
+  *lo = xmin;
+  *hi = xmax;
+}
+// one job = one image in one geometry: geom 0 = EfficientNet squash (bilinear), 1 = CLIP
+// shortest-edge + centre crop (bicubic); returns false when a pass needs more than kResizeKMax taps
+bool plan_job(int w, int h, int geom, ResizeJob* J) {
+  *J = ResizeJob{};
+  J->w = w;
+  J->h = h;
+  J->filt = geom;
+  if (w == 224 && h == 224) {
+    J->ow = J->oh = 224;
+  } else if (geom == 0) {
+    J->ow = J->oh = 224;
+  } else {
+    const int shrt = w <= h ? w : h, lng = w <= h ? h : w;
+    const int new_long = (int)(224.0 * lng / shrt);
+    J->ow = w <= h ? 224 : new_long;
+    J->oh = w <= h ? new_long : 224;
+    J->cx = (J->ow - 224) / 2;
+    J->cy = (J->oh - 224) / 2;
+  }
+  J->need_h = J->ow != w;
+  J->need_v = J->oh != h;
+  J->ksh = J->need_h ? axis_plan(w, J->ow, J->filt).ks : 1;
+  J->ksv = J->need_v ? axis_plan(h, J->oh, J->filt).ks : 1;
+  if (J->ksh > kResizeKMax || J->ksv > kResizeKMax) return false;
+  if (J->need_v) {
+    const AxisPlan a = axis_plan(h, J->oh, J->filt);
+    int lo, hi;
+    tap_range(a, h, J->cy, &lo, &hi);
+    J->y0 = lo;
+    tap_range(a, h, J->cy + 223, &lo, &hi);
+    J->y1 = hi;
+  } else {
+    J->y0 = J->cy;
+    J->y1 = J->cy + 224;
+  }
+  return true;
+}
+}  // namespace
+
+int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, const int32_t* wh, int B,
+                   int pixel_bytes, uint8_t* out_effnet, uint8_t* out_clip, void* stream) {
+  if (!h || !src || !offsets || !wh || B < 0) return fail(MMF_EINVAL, "null argument");
+  if (pixel_bytes != 3 && pixel_bytes != 4) return fail(MMF_EINVAL, "pixel_bytes must be 3 (RGB) or 4 (RGBX)");
+  if (!out_effnet && !out_clip) return 0;
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<ResizeJob> jobs;
+  std::vector<uint8_t*> outs;
+  long long tmp = 0;
+  int coef = 0, max_rows = 0;
+  for (int i = 0; i < B; ++i) {
+    const int w = wh[2 * i], ht = wh[2 * i + 1];
+    if (w <= 0 || ht <= 0) return fail(MMF_EINVAL, "image %d has size %dx%d", i, w, ht);
+    for (int geom = 0; geom < 2; ++geom) {
+      uint8_t* o = geom ? out_clip : out_effnet;
+      if (!o) continue;
+      ResizeJob J;
+      if (!plan_job(w, ht, geom, &J))
+        return fail(MMF_EINVAL, "image %d (%dx%d): downscale beyond %d taps per output pixel", i, w, ht, kResizeKMax);
+      J.src_off = offsets[i];
+      J.ps = pixel_bytes;
+      J.tmp_off = tmp;
+      J.coef_off = coef;
+      tmp += (long long)(J.y1 - J.y0) * 224 * 3;
+      coef += 224 * (J.ksh + J.ksv);
+      max_rows = std::max(max_rows, J.y1 - J.y0);
+      jobs.push_back(J);
+      outs.push_back(o + (size_t)i * 224 * 224 * 3);
+    }
+  }
+  auto& R = h->rs;
+  const size_t nj = jobs.size();
+  if (nj > R.cap_jobs || (size_t)coef > R.cap_coef || (size_t)tmp > R.cap_tmp) {
+    CHK(free_group(h, AG_RESIZE));
+    R.cap_jobs = std::max(nj, R.cap_jobs);
+    R.cap_coef = std::max((size_t)coef, R.cap_coef);
+    R.cap_tmp = std::max((size_t)tmp, R.cap_tmp);
+    void* p;
+    CHK(dev_alloc(h, &p, R.cap_jobs * sizeof(ResizeJob), AG_RESIZE)); R.jobs = (ResizeJob*)p;
+    CHK(dev_alloc(h, &p, R.cap_jobs * sizeof(uint8_t*), AG_RESIZE)); R.outs = (uint8_t**)p;
+    CHK(dev_alloc(h, &p, R.cap_jobs * 2 * 224 * 2 * sizeof(int32_t), AG_RESIZE)); R.bounds = (int32_t*)p;
+    CHK(dev_alloc(h, &p, R.cap_coef * sizeof(int32_t), AG_RESIZE)); R.coef = (int32_t*)p;
+    CHK(dev_alloc(h, &p, R.cap_tmp, AG_RESIZE)); R.tmp = (uint8_t*)p;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(R.jobs, jobs.data(), nj * sizeof(ResizeJob), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(R.outs, outs.data(), nj * sizeof(uint8_t*), hipMemcpyHostToDevice, s));
+  HIPCHK(launch_resize_pil(src, R.jobs, (int)nj, max_rows, R.coef, R.bounds, R.tmp, R.outs, s));
+  HIPCHK(hipStreamSynchronize(s));  // the host job tables above are released on return
+  return 0;
 }
 
 int64_t mmf_device_bytes(mmf_handle* h) {

@@ -128,6 +128,24 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
 // number of pool-partial chunks launch_dwconv uses for an output of Ho x Wo with C channels
 int dwconv_nchunks(int H, int W, int C, int stride);
 
+// Pillow-exact resampling of decoded images to the towers' 224 x 224 windows (resize.hip)
+constexpr int kResizeKMax = 96;  // taps per output coordinate (bicubic support 2 x scale <= 47)
+struct ResizeJob {
+  long long src_off;  // byte offset of the source image (uint8 HWC RGB) in the source buffer
+  int w, h;           // source size
+  int ow, oh;         // Pillow resize output size (before the crop)
+  int cx, cy;         // window offset in the resize output (centre crop; 0 for the squash)
+  int filt;           // 0 bilinear, 1 bicubic
+  int need_h, need_v; // Pillow runs the pass (size changes on that axis)
+  int y0, y1;         // source rows the window's vertical taps read
+  int ksh, ksv;       // taps per coordinate, horizontal / vertical
+  long long tmp_off;  // byte offset of this job's [y1 - y0][224][3] horizontal-pass rows
+  int coef_off;       // int32 offset of [224][ksh] then [224][ksv] coefficients
+  int ps;             // source bytes per pixel: 3 (RGB) or 4 (RGBX, Pillow's in-memory layout)
+};
+hipError_t launch_resize_pil(const uint8_t* src, const ResizeJob* jobs, int njobs, int max_rows, int32_t* coef,
+                             int32_t* bounds, uint8_t* tmp, uint8_t* const* outs, hipStream_t s);
+
 // fp32 EfficientNet tower (option effnet_fp32, effnet_f32.hip): NHWC fp32 activations
 hipError_t launch_effnet_stem32(const uint8_t* img, const float* x_nchw, const float* w, const float* bias,
                                 float* out, int B, hipStream_t s);

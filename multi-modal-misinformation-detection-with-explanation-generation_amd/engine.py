@@ -95,6 +95,44 @@ class Engine:
             check(self.lib.mmf_set_vault_titles(self.h, ptr(ids), ptr(mask), ids.shape[0], ids.shape[1],
                                                 stream_ptr()), "mmf_set_vault_titles")
 
+    # ------------------------------------------------------------------ host-input geometry
+    def resize_images(self, images, effnet: bool = True, clip: bool = True):
+        """Decoded uint8 images (HxWx3 RGB or HxWx4 RGBX numpy arrays -- all of one kind --, any
+        sizes) -> device uint8 [B,224,224,3] EfficientNet squash-resize and CLIP shortest-edge +
+        centre-crop windows, bit-exact with Pillow (mmf_resize_pil).  The images cross PCIe once,
+        packed (threaded copies) into a pinned staging buffer."""
+        arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+        ps = arrs[0].shape[2] if arrs else 3
+        for a in arrs:
+            assert a.ndim == 3 and a.shape[2] == ps and ps in (3, 4), f"expected HxWx{ps} uint8, got {a.shape}"
+        sizes = [a.nbytes for a in arrs]
+        offs = np.zeros(len(arrs), np.int64)
+        if arrs:
+            offs[1:] = np.cumsum(sizes)[:-1]
+        total = int(sum(sizes)) or 1
+        if getattr(self, "_rs_host", None) is None or self._rs_host.numel() < total:
+            self._rs_host = torch.empty(total, dtype=torch.uint8).pin_memory()
+        host = self._rs_host.numpy()
+
+        def pack(i):
+            np.copyto(host[offs[i]:offs[i] + sizes[i]], arrs[i].reshape(-1))
+        if total > (8 << 20) and len(arrs) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=min(16, len(arrs))) as ex:
+                list(ex.map(pack, range(len(arrs))))
+        else:
+            for i in range(len(arrs)):
+                pack(i)
+        src = self._rs_host[:total].to(self.device, non_blocking=True)
+        wh = np.array([[a.shape[1], a.shape[0]] for a in arrs], np.int32).reshape(-1)
+        B = len(arrs)
+        eff = torch.empty((B, 224, 224, 3), dtype=torch.uint8, device=self.device) if effnet else None
+        clp = torch.empty((B, 224, 224, 3), dtype=torch.uint8, device=self.device) if clip else None
+        check(self.lib.mmf_resize_pil(self.h, ptr(src), offs.ctypes.data_as(ctypes.c_void_p),
+                                      wh.ctypes.data_as(ctypes.c_void_p), B, ps, ptr(eff), ptr(clp), stream_ptr()),
+              "mmf_resize_pil")
+        return eff, clp
+
     # ------------------------------------------------------------------ helpers
     def _i32(self, x) -> torch.Tensor:
         t = torch.as_tensor(x)

@@ -46,11 +46,52 @@ def clip_pixels(img) -> np.ndarray:
     return np.asarray(img, dtype=np.uint8)
 
 
+def _open(item):
+    return to_pil(Image.open(io.BytesIO(item)) if isinstance(item, (bytes, bytearray)) else item)
+
+
 def _decode_one(args):
     i, item, eff, clp = args
-    pil = to_pil(Image.open(io.BytesIO(item)) if isinstance(item, (bytes, bytearray)) else item)
+    pil = _open(item)
     eff[i] = effnet_pixels(pil)
     clp[i] = clip_pixels(pil)
+
+
+def _rgbx_view(pil):
+    """Pillow keeps RGB pixels as 4 bytes (RGBX); its Arrow export (Pillow >= 11.2) hands that
+    memory over without a copy, which np.asarray (a GIL-held tobytes copy) does not."""
+    try:
+        import pyarrow as pa
+        buf = pa.array(pil).buffers()[-1]
+        w, h = pil.size
+        if buf is not None and buf.size == w * h * 4:
+            return np.frombuffer(buf, np.uint8).reshape(h, w, 4)
+    except Exception:  # noqa: BLE001 - no pyarrow / no Arrow export: the copying path below
+        pass
+    return None
+
+
+def decode_rgb(images, workers: Optional[int] = None) -> List[np.ndarray]:
+    """Decode only (threaded) -> uint8 HxWx4 RGBX views of Pillow's own pixel memory when the
+    Arrow export is available (else HxWx3 RGB copies); the resampling to both towers' windows then
+    runs on the device (Engine.resize_images, Pillow-exact).  All arrays returned are of one kind."""
+    if workers is None:
+        workers = min(len(images), len(os.sched_getaffinity(0)), 16)
+
+    def one(item):
+        pil = _open(item)
+        pil.load()
+        v = _rgbx_view(pil)
+        return (v, pil) if v is not None else (np.asarray(pil, dtype=np.uint8), pil)
+    if workers <= 1 or len(images) <= 1:
+        res = [one(x) for x in images]
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=workers) as ex:
+            res = list(ex.map(one, images))
+    if len({a.shape[2] for a, _ in res}) > 1:  # mixed kinds: fall back to RGB copies for all
+        return [np.asarray(p, dtype=np.uint8) for _, p in res]
+    return [a for a, _ in res]
 
 
 def decode_batch(images, workers: Optional[int] = None, out: Optional[Tuple[np.ndarray, np.ndarray]] = None):
@@ -98,6 +139,18 @@ def tokenize_roberta(tok, text: str) -> List[int]:
     if (hasattr(ids, "dim") and ids.dim() == 2) or (isinstance(ids, (list, tuple)) and isinstance(ids[0], (list, tuple))):
         ids = ids[0]
     return _to_list(ids)
+
+
+def tokenize_roberta_batch(tok, texts: List[str]) -> List[List[int]]:
+    """tokenize_roberta for many texts in one tokenizer call (fast tokenizers encode the batch in
+    parallel); each text is encoded independently and right padding only appends, so stripping
+    by the attention mask returns exactly the per-text ids."""
+    try:
+        enc = tok(list(texts), return_tensors="pt", max_length=512, truncation=True, padding=True)
+    except (TypeError, KeyError, ValueError):  # a tokenizer object that only takes single strings
+        return [tokenize_roberta(tok, t) for t in texts]
+    ids, mask = enc["input_ids"], enc["attention_mask"]
+    return [_to_list(ids[i])[:int(sum(_to_list(mask[i])))] for i in range(len(texts))]
 
 
 def tokenize_clip(proc, texts: List[str], truncation: bool = False) -> List[List[int]]:

@@ -10,9 +10,15 @@ class TableRobertaTokenizer:
         self.table = table
 
     def __call__(self, text, return_tensors="pt", max_length=512, truncation=True, padding=True):
-        ids = list(self.table[text])[:max_length] if truncation else list(self.table[text])
-        t = torch.tensor([ids], dtype=torch.long)
-        return BatchEncoding({"input_ids": t, "attention_mask": torch.ones_like(t)})
+        texts = [text] if isinstance(text, str) else list(text)
+        seqs = [list(self.table[s])[:max_length] if truncation else list(self.table[s]) for s in texts]
+        L = max(len(s) for s in seqs)
+        ids = torch.full((len(seqs), L), 1, dtype=torch.long)  # RoBERTa pad id, right padding
+        mask = torch.zeros((len(seqs), L), dtype=torch.long)
+        for i, s in enumerate(seqs):
+            ids[i, :len(s)] = torch.tensor(s)
+            mask[i, :len(s)] = 1
+        return BatchEncoding({"input_ids": ids, "attention_mask": mask})
 
 
 class TableClipProcessor:

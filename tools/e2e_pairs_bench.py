@@ -1,0 +1,116 @@
+"""Text+JPEG -> verdict throughput through the drop-in API (`MisinfoForensics.analyze_pairs`), i.e.
+the reference's `analyze(text, image)` for a batch of real-format inputs, with the time split into
+its host and device stages.
+
+    python tools/e2e_pairs_bench.py [--n 256] [--reps 3] [--json out.json]
+
+Inputs: synthetic 640x480 JPEGs (tools/host_pipeline_bench.py) and ~40-word texts; tokenizers are
+byte-level BPEs trained on a synthetic corpus and wrapped with RoBERTa's / CLIP's special-token and
+padding conventions (the vocab files are absent), weights are synthetic.  Prints one JSON object.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from host_pipeline_bench import synth_jpegs, synth_texts  # noqa: E402
+
+
+class _BPE:
+    """A byte-level BPE with a tokenizer-call interface: `prefix + bpe[:cap] + suffix`, right padded."""
+
+    def __init__(self, bpe, prefix, suffix, pad, cap):
+        self.bpe, self.prefix, self.suffix, self.pad, self.cap = bpe, prefix, suffix, pad, cap
+
+    def _ids(self, encs, truncation, max_length):
+        seqs = [self.prefix + e.ids[:self.cap] + self.suffix for e in encs]
+        if truncation:
+            seqs = [s[:max_length] for s in seqs]
+        L = max(len(s) for s in seqs)
+        ids = torch.full((len(seqs), L), self.pad, dtype=torch.long)
+        mask = torch.zeros((len(seqs), L), dtype=torch.long)
+        for i, s in enumerate(seqs):
+            ids[i, :len(s)] = torch.tensor(s)
+            mask[i, :len(s)] = 1
+        return {"input_ids": ids, "attention_mask": mask}
+
+
+class RobertaLike(_BPE):
+    def __call__(self, text, return_tensors="pt", max_length=512, truncation=True, padding=True):
+        texts = [text] if isinstance(text, str) else list(text)
+        return self._ids(self.bpe.encode_batch(texts), truncation, max_length)
+
+
+class ClipLike(_BPE):
+    def __call__(self, text=None, images=None, return_tensors="pt", padding=False, truncation=False):
+        return self._ids(self.bpe.encode_batch(list(text)), truncation, 77)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    from tokenizers import ByteLevelBPETokenizer
+    from mmf_amd import io_utils
+    from mmf_amd.api import MisinfoForensics
+    bpe = ByteLevelBPETokenizer()
+    bpe.train_from_iterator(synth_texts(4000, seed=9)[0], vocab_size=8000, min_frequency=2, show_progress=False)
+    rob = RobertaLike(bpe, [0], [2], 1, 510)
+    clp = ClipLike(bpe, [49406], [49407], 49407, 75)
+    texts = synth_texts(a.n, seed=4, words=40)[0]
+    jpegs = synth_jpegs(a.n)
+    mf = MisinfoForensics(fusion_weights="", faiss_index_path="", synthetic_seed=0, roberta_tokenizer=rob,
+                          clip_processor=clp, max_batch=a.n, verbose=False)
+    g = np.random.default_rng(11)
+    emb = g.standard_normal((2170, 512)).astype(np.float32)
+    mf.set_vault(emb, [{"title": t, "url": "u", "date": "d"} for t in synth_texts(2170, seed=12, words=12)[0]])
+    mf.analyze_pairs(texts, jpegs)  # warm (workspace growth, first launches)
+    torch.cuda.synchronize()
+
+    stages = {"tokenize": [], "decode": [], "pack_h2d_device_resample": [], "device_analyze": [],
+              "result_dicts": [], "total": [], "host_resample_instead": []}
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        r = io_utils.tokenize_roberta_batch(rob, texts)
+        rid, rm = io_utils.pad_ids(r, 1)
+        cid, cm = mf._clip_ids(texts)
+        t1 = time.perf_counter()
+        rgb = io_utils.decode_rgb(jpegs)
+        t2 = time.perf_counter()
+        eff, cl = mf.engine.resize_images(rgb)
+        t3 = time.perf_counter()
+        out = mf.analyze_batch(rid, rm, cid, cm, eff, cl)
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        mf.batch_to_dicts(out)
+        t5 = time.perf_counter()
+        io_utils.decode_batch(jpegs)  # the all-host alternative (decode + both Pillow resamplings)
+        t6 = time.perf_counter()
+        for k, v in zip(stages, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t5 - t0, t6 - t5)):
+            stages[k].append(v)
+        t5 = time.perf_counter()
+        mf.analyze_pairs(texts, jpegs)
+        stages.setdefault("analyze_pairs_call", []).append(time.perf_counter() - t5)
+    best = {k: min(v) for k, v in stages.items()}
+    from mmf_amd import benchrun
+    res = {"n_pairs": a.n, "usable_cores": benchrun.usable_cpus(),
+           "pairs_per_s": round(a.n / best["analyze_pairs_call"], 1),
+           "stage_ms": {k: round(1e3 * v, 2) for k, v in best.items()},
+           "note": "synthetic 640x480 JPEGs, ~40-word texts, synthetic BPE tokenizers and weights; stages timed "
+                   "sequentially (analyze_pairs runs them in the same order)"}
+    print(json.dumps(res), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
