@@ -599,28 +599,39 @@ class MisinfoForensics:
 
     def analyze_pairs(self, texts: List[str], images: List) -> List[Dict]:
         """Batched analyze() for text+image pairs: one analyze_batch launch sequence per
-        `max_batch` pairs, then the reference's result dicts (one per pair, in order)."""
+        `max_batch` pairs, then the reference's result dicts (one per pair, in order).  The host
+        stage of chunk i + 1 (tokenisation, threaded image decode) runs on a helper thread while
+        chunk i is resampled, analysed on the device and turned into dicts."""
         if len(texts) != len(images):
             raise ValueError(f"{len(texts)} texts vs {len(images)} images")
         cap = self.engine.max_batch
-        if len(texts) > cap:
-            res = []
-            for i in range(0, len(texts), cap):
-                res.extend(self.analyze_pairs(texts[i:i + cap], images[i:i + cap]))
-            return res
-        rob = io_utils.tokenize_roberta_batch(self.roberta_tokenizer, texts)
-        rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
-        self._fit_text(rid.shape[1])
-        cid, cm = self._clip_ids(list(texts))
-        # decode on the host (threaded), resample to both towers' windows on the device
-        # (Pillow-exact); images past the device resampler's 47x downscale take the host path
-        rgb = io_utils.decode_rgb(images)
-        try:
-            eff, clp = self.engine.resize_images(rgb)
-        except MMFError:
-            eff, clp = io_utils.decode_batch([io_utils.Image.fromarray(a) for a in rgb])
-        out = self.analyze_batch(rid, rm, cid, cm, eff, clp)
-        return self.batch_to_dicts(out)
+        chunks = [(i, min(i + cap, len(texts))) for i in range(0, len(texts), cap)]
+        if not chunks:
+            return []
+
+        def host_stage(a, b):
+            rob = io_utils.tokenize_roberta_batch(self.roberta_tokenizer, texts[a:b])
+            rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
+            cid, cm = self._clip_ids(list(texts[a:b]))
+            # decoded pixels; the resampling to both towers' windows runs on the device
+            return rid, rm, cid, cm, io_utils.decode_rgb(images[a:b])
+
+        from concurrent.futures import ThreadPoolExecutor
+        res: List[Dict] = []
+        with ThreadPoolExecutor(max_workers=1) as ex:
+            fut = ex.submit(host_stage, *chunks[0])
+            for k in range(len(chunks)):
+                rid, rm, cid, cm, rgb = fut.result()
+                if k + 1 < len(chunks):
+                    fut = ex.submit(host_stage, *chunks[k + 1])
+                self._fit_text(rid.shape[1])
+                try:  # Pillow-exact device resampling; past its 47x downscale, Pillow on the host
+                    eff, clp = self.engine.resize_images(rgb)
+                except MMFError:
+                    eff, clp = io_utils.decode_batch([io_utils.Image.fromarray(np.ascontiguousarray(a[..., :3]))
+                                                      for a in rgb])
+                res.extend(self.batch_to_dicts(self.analyze_batch(rid, rm, cid, cm, eff, clp)))
+        return res
 
     def analyze_batch(self, rob_ids, rob_mask, clip_ids, clip_mask, images_u8, clip_images_u8=None,
                       out: Optional[dict] = None) -> Dict[str, torch.Tensor]:
