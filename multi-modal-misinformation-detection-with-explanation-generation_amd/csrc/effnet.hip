@@ -8,10 +8,19 @@
 //   se        mean -> fc1 + SiLU -> fc2 + sigmoid -> per-(image, channel) scale (applied inside
 //             the project GEMM's A load)
 //   gap_cls   global average pool of the head conv + Linear(1280, 2) + softmax[:, 1]
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace {
+
+// per-image base pointer (workgroup-uniform -> SGPRs) + 32-bit byte offset: global loads / stores
+// use the saddr + 32-bit voffset form instead of per-lane 64-bit address arithmetic
+template <typename T>
+MMF_DEV T* at_bytes(T* base, uint32_t byte_off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(const_cast<typename std::remove_const<T>::type*>(base)) + byte_off);
+}
 
 // One thread per output pixel, all 32 channels; weights transposed in LDS to [tap][channel] so
 // every tap is 8 broadcast float4 reads.  ToTensor + Normalize folded into one FMA per input.
@@ -121,7 +130,8 @@ MMF_DEV void dw_compute(const f16_t* tile, const float* sw, const float* sb, flo
         acc[j] = act_apply(acc[j], ACT_SILU);
         psum[j] += acc[j];
       }
-      *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox) * C + c0 + g * 8) =
+      *reinterpret_cast<uint4*>(at_bytes(out + (size_t)bi * Ho * Wo * C,
+                                         (uint32_t)(((oy0 + oy) * Wo + ox0 + ox) * C + c0 + g * 8) * 2u)) =
           make_uint4(pack2h(acc[0], acc[1]), pack2h(acc[2], acc[3]), pack2h(acc[4], acc[5]),
                      pack2h(acc[6], acc[7]));
     }
@@ -134,7 +144,7 @@ MMF_DEV void dw_compute(const f16_t* tile, const float* sw, const float* sb, flo
   for (int c = tid; c < CW; c += 256) {
     float sum = 0.f;
     for (int q = 0; q < PX; ++q) sum += red[q * CW + c];
-    pool_part[((size_t)bi * ntiles + blockIdx.x) * C + c0 + c] = sum;
+    *at_bytes(pool_part + (size_t)bi * ntiles * C, (uint32_t)(blockIdx.x * C + c0 + c) * 4u) = sum;
   }
 }
 
@@ -197,7 +207,8 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
           act4<ACT_SILU>(acc[o] + 4);
 #pragma unroll
           for (int j = 0; j < 8; ++j) psum[j] += acc[o][j];
-          *reinterpret_cast<uint4*>(out + (((size_t)bi * Ho + oy0 + oy) * Wo + ox0 + ox + o) * C + c0 + g * 8) =
+          *reinterpret_cast<uint4*>(at_bytes(out + (size_t)bi * Ho * Wo * C,
+                                             (uint32_t)(((oy0 + oy) * Wo + ox0 + ox + o) * C + c0 + g * 8) * 2u)) =
               make_uint4(pack2h(acc[o][0], acc[o][1]), pack2h(acc[o][2], acc[o][3]), pack2h(acc[o][4], acc[o][5]),
                          pack2h(acc[o][6], acc[o][7]));
         }
@@ -215,7 +226,7 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
   for (int c = tid; c < CW; c += 256) {
     float sum = 0.f;
     for (int q = 0; q < NRED; ++q) sum += red[q * CW + c];
-    pool_part[((size_t)bi * ntiles + blockIdx.x) * C + c0 + c] = sum;
+    *at_bytes(pool_part + (size_t)bi * ntiles * C, (uint32_t)(blockIdx.x * C + c0 + c) * 4u) = sum;
   }
 }
 
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
     const int iy = iy0 + ty, ix = ix0 + tx;
     v = make_uint4(0, 0, 0, 0);
     if (idx < IT * IT * NG && iy >= 0 && iy < H && ix >= 0 && ix < W)
-      v = *reinterpret_cast<const uint4*>(in + (((size_t)bi * H + iy) * W + ix) * C + c0 + g * 8);
+      v = *reinterpret_cast<const uint4*>(at_bytes(in + (size_t)bi * H * W * C, (uint32_t)((iy * W + ix) * C + c0 + g * 8) * 2u));
   };
   if constexpr (TT > 0) {
     // compile-time tile: every thread's loads are issued before its first LDS store, so the
@@ -353,7 +364,8 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = ks * 32 + fg * 8;
-      xr[it][ks] = (inimg && k < Cin) ? *reinterpret_cast<const uint4*>(x + (((size_t)bi * H + iy) * W + ix) * Cin + k)
+      xr[it][ks] = (inimg && k < Cin) ? *reinterpret_cast<const uint4*>(at_bytes(x + (size_t)bi * H * W * Cin,
+                                                                                 (uint32_t)((iy * W + ix) * Cin + k) * 2u))
                                       : make_uint4(0, 0, 0, 0);
     }
   }
@@ -489,7 +501,8 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
     const int iyc = min(max(iy, 0), 223), ixc = min(max(ix, 0), 223);
     chan[i] = ok ? c : -1;
     if constexpr (F32) raw[i] = xf[(((size_t)bi * 3 + c) * 224 + iyc) * 224 + ixc];
-    else raw[i] = __builtin_bit_cast(float, (uint32_t)img[(((size_t)bi * 224 + iyc) * 224 + ixc) * 3 + c]);
+    else raw[i] = __builtin_bit_cast(float, (uint32_t)*at_bytes(img + (size_t)bi * 224 * 224 * 3,
+                                                                (uint32_t)((iyc * 224 + ixc) * 3 + c)));
   }
 #pragma unroll
   for (int i = 0; i < NL; ++i) {  // (the array is padded to NL * 256: no branch around the stores)
