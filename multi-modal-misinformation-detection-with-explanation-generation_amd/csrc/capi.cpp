@@ -113,6 +113,7 @@ struct Options {
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
+  int text_hilo = 0;    // RoBERTa residual stream as fp16 hi + fp16 lo (1) or fp16 alone (0, default: DESIGN §4)
   int gemm_prio = 2;    // s_setprio 1 for waves 0-3 of the persistent GEMM (+0.4 % step; A/B)
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
 };
@@ -121,7 +122,8 @@ const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
     {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"}, {"dw_ct", &Options::dw_ct, "MMF_DW_CT"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
-    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
+    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"},
+    {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -593,10 +595,11 @@ int check_cap(mmf_handle* h, int B, int Lr, int Lc) {
 int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
              float* scores, int score_stride, hipStream_t s) {
   Workspace& w = h->ws;
+  uint16_t* rlo = h->opt.text_hilo ? w.r_lo : nullptr;
   const int M = B * L;
   {
     ProfScope ps(h, s, PK_EMBED, 10.0 * M * 768, (double)M * 768 * (4 + 4 + 2 + 2));
-    HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, w.r_lo,
+    HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, rlo,
                                 w.r_xb, B, L, 768, 1, s));
   }
   for (int i = 0; i < 12; ++i) {
@@ -615,7 +618,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       g = gemm_args(w.r_ctx, 768, Ly.o, M);
       g.c16 = y;
       CHK(gemm(h, g, s));
-      CHK(add_ln_hilo(h, w.r_xb, w.r_lo, 768, y, 768, Ly.ln1, M, s));
+      CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln1, M, s));
       g = gemm_args(w.r_xb, 768, Ly.fc1, M);
       g.act = 1;  // GELU-erf
       g.c16 = w.r_h;
@@ -624,13 +627,13 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       g = gemm_args(w.r_h, 3072, Ly.fc2, M);
       g.c16 = y;
       CHK(gemm(h, g, s));
-      CHK(add_ln_hilo(h, w.r_xb, w.r_lo, 768, y, 768, Ly.ln2, M, s));
+      CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln2, M, s));
       continue;
     }
     const int Mr = last ? B : M;            // rows after the attention
     const int rs = last ? L * 768 : 768;    // row stride of ctx at this point
     // the B CLS rows of the split residual stream, as fp32 (r_y, compact)
-    HIPCHK(launch_hilo_rows(w.r_xb, w.r_lo, rs, w.r_y, B, 768, s));
+    HIPCHK(launch_hilo_rows(w.r_xb, rlo, rs, w.r_y, B, 768, s));
     g = with_ws(gemm_args(w.r_ctx, rs, Ly.o, Mr), w.sk_text, w.sk_elems);
     g.res32 = w.r_y;
     g.ldr = 768;

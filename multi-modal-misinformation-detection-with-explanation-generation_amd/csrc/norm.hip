@@ -109,13 +109,15 @@ MMF_DEV void store_row_hilo(const float4 (&v)[NV], f16_t* hi, uint16_t* lo, int 
     const int c = (i * 64 + lane) * 4;
     const uint2 h = make_uint2(pack2h(v[i].x, v[i].y), pack2h(v[i].z, v[i].w));
     *reinterpret_cast<uint2*>(hi + c) = h;
-    *reinterpret_cast<uint2*>(lo + c) = make_uint2(pack2h(v[i].x - lo_h(h.x), v[i].y - hi_h(h.x)),
+    if (lo)  // lo = null: fp16-only stream (option text_hilo = 0)
+      *reinterpret_cast<uint2*>(lo + c) = make_uint2(pack2h(v[i].x - lo_h(h.x), v[i].y - hi_h(h.x)),
                                                    pack2h(v[i].z - lo_h(h.y), v[i].w - hi_h(h.y)));
   }
 }
 
 // post-LN add+LayerNorm on the split stream: s = (hi + lo) + y; (hi, lo) = split(LN(s)), in place
-template <int NV>
+// HILO = false: the stream is hi alone (fp16; option text_hilo = 0)
+template <int NV, bool HILO>
 __global__ __launch_bounds__(256) void add_ln_hilo_kernel(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy,
                                                           const float* g, const float* b, float eps, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(256) void add_ln_hilo_kernel(f16_t* hi, uint16_t* l
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
     xh[i] = *reinterpret_cast<const uint2*>(hr + c);
-    xl[i] = *reinterpret_cast<const uint2*>(lr + c);
+    xl[i] = HILO ? *reinterpret_cast<const uint2*>(lr + c) : make_uint2(0, 0);
     a[i] = *reinterpret_cast<const uint2*>(yr + c);
   }
 #pragma unroll
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(256) void add_ln_hilo_kernel(f16_t* hi, uint16_t* l
     v[i].w = (hi_h(xh[i].y) + hi_h(xl[i].y)) + hi_h(a[i].y);
   }
   ln_row<NV>(v, g, b, eps, NV * 256, lane);
-  store_row_hilo<NV>(v, hr, lr, lane);
+  store_row_hilo<NV>(v, hr, HILO ? lr : nullptr, lane);
 }
 
 // fp32 rows (hi + lo) of the split stream, gathered with a row stride (the last layer's CLS rows)
@@ -149,9 +151,10 @@ __global__ __launch_bounds__(256) void hilo_rows_kernel(const f16_t* hi, const u
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
   const f16_t* hr = hi + (size_t)row * row_stride;
-  const uint16_t* lr = lo + (size_t)row * row_stride;
+  const uint16_t* lr = lo ? lo + (size_t)row * row_stride : nullptr;
   for (int c = lane * 4; c < C; c += 256) {
-    const uint2 h = *reinterpret_cast<const uint2*>(hr + c), l = *reinterpret_cast<const uint2*>(lr + c);
+    const uint2 h = *reinterpret_cast<const uint2*>(hr + c);
+    const uint2 l = lr ? *reinterpret_cast<const uint2*>(lr + c) : make_uint2(0, 0);
     *reinterpret_cast<float4*>(out + (size_t)row * C + c) =
         make_float4(lo_h(h.x) + lo_h(l.x), hi_h(h.x) + hi_h(l.x), lo_h(h.y) + lo_h(l.y), hi_h(h.y) + hi_h(l.y));
   }
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
     add_row<NV>(v, pos + (size_t)s_pos[t] * C, lane);
     ln_row<NV>(v, g, b, eps, C, lane);
     const size_t r = (size_t)bi * L + t;
-    store_row_hilo<NV>(v, xb + r * C, xlo + r * C, lane);
+    store_row_hilo<NV>(v, xb + r * C, xlo ? xlo + r * C : nullptr, lane);
   }
 }
 
@@ -422,7 +425,12 @@ hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s) {
 hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const float* g,
                               const float* b, float eps, int rows, int C, hipStream_t s) {
   if (C != 768 || (ld & 3) || (ldy & 3)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(add_ln_hilo_kernel<3>, dim3((rows + 3) / 4), dim3(256), 0, s, hi, lo, ld, y, ldy, g, b, eps, rows);
+  if (lo)
+    hipLaunchKernelGGL((add_ln_hilo_kernel<3, true>), dim3((rows + 3) / 4), dim3(256), 0, s, hi, lo, ld, y, ldy, g, b, eps,
+                       rows);
+  else
+    hipLaunchKernelGGL((add_ln_hilo_kernel<3, false>), dim3((rows + 3) / 4), dim3(256), 0, s, hi, lo, ld, y, ldy, g, b,
+                       eps, rows);
   return hipGetLastError();
 }
 
