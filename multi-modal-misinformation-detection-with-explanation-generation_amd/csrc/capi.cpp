@@ -116,6 +116,7 @@ struct Options {
   int text_hilo = 0;    // RoBERTa residual stream as fp16 hi + fp16 lo (1) or fp16 alone (0, default: DESIGN §4)
   int gemm_prio = 2;    // s_setprio 1 for waves 0-3 of the persistent GEMM (+0.4 % step; A/B)
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
+  int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -124,6 +125,7 @@ const OptName kOptNames[] = {
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
     {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
+    {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -577,6 +579,13 @@ int add_ln(mmf_handle* h, float* x, int ldx, const f16_t* y, int ldy, const LNp&
   return 0;
 }
 
+int add_ln(mmf_handle* h, f16_t* x, int ldx, const f16_t* y, int ldy, const LNp& p, f16_t* o16, int ldo, int rows,
+           int C, hipStream_t s) {
+  ProfScope ps(h, s, PK_LN, 9.0 * rows * C, (double)rows * C * (2 + 2 + 2 + 2));
+  HIPCHK(launch_add_ln(x, ldx, y, ldy, p.g, p.b, 1e-5f, x, o16, ldo, rows, C, s));
+  return 0;
+}
+
 int add_ln_hilo(mmf_handle* h, f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const LNp& p, int rows,
                 hipStream_t s) {
   ProfScope ps(h, s, PK_LN, 9.0 * rows * 768, (double)rows * 768 * (2 + 2 + 2 + 2 + 2));
@@ -657,7 +666,8 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   return 0;
 }
 
-// pre-LN CLIP encoder over x (fp32 residual, in place) with xb = LN1_0(x) already computed
+// pre-LN CLIP encoder over x (residual stream, in place: fp32, or fp16 when opt.clip_res16) with
+// xb = LN1_0(x) already computed
 // Only one row per sequence is consumed after the last layer (CLS for the ViT, EOS for the text
 // tower: TF clip:561-582, 650-651): the last layer's out-proj / MLP run on those B rows, gathered
 // into compact buffers (xc fp32, ctxc fp16); on return xc holds them (before the final LN).
@@ -666,6 +676,7 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
                      const int32_t* last_rows, float* xc, f16_t* ctxc, float* skws, size_t sk_elems,
                      hipStream_t s) {
   const int M = B * L;
+  f16_t* x16 = h->opt.clip_res16 ? reinterpret_cast<f16_t*>(x) : nullptr;
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = layers[i];
     GemmArgs g = gemm_args(xb, H, Ly.qkv, M);
@@ -673,7 +684,7 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
     CHK(gemm(h, g, s));
     CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
     if (i == 11) {
-      HIPCHK(launch_gather_rows2(ctx, x, last_rows, L, H, ctxc, xc, B, s));
+      HIPCHK(launch_gather_rows2(ctx, x16 ? nullptr : x, x16, last_rows, L, H, ctxc, xc, B, s));
       g = with_ws(gemm_args(ctxc, H, Ly.o, B), skws, sk_elems);
       g.res32 = xc;
       g.c32 = xc;
@@ -694,7 +705,8 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
     g = gemm_args(ctx, H, Ly.o, M);
     g.c16 = hid;
     CHK(gemm(h, g, s));
-    CHK(add_ln(h, x, H, hid, H, Ly.ln2, x, nullptr, xb, H, M, H, s));
+    CHK(x16 ? add_ln(h, x16, H, hid, H, Ly.ln2, xb, H, M, H, s)
+            : add_ln(h, x, H, hid, H, Ly.ln2, x, nullptr, xb, H, M, H, s));
     g = gemm_args(xb, H, Ly.fc1, M);
     g.act = 2;  // quick_gelu
     g.c16 = hid;
@@ -703,7 +715,8 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
     g.c16 = ctx;
     CHK(gemm(h, g, s));
     // layer i + 1 < 12 always holds here (layer 11 takes the compact branch above)
-    CHK(add_ln(h, x, H, ctx, H, layers[i + 1].ln1, x, nullptr, xb, H, M, H, s));
+    CHK(x16 ? add_ln(h, x16, H, ctx, H, layers[i + 1].ln1, xb, H, M, H, s)
+            : add_ln(h, x, H, ctx, H, layers[i + 1].ln1, x, nullptr, xb, H, M, H, s));
   }
   return 0;
 }
@@ -724,7 +737,8 @@ int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStre
   {
     ProfScope ps(h, s, PK_EMBED, 16.0 * B * 50 * 768, (double)B * 50 * 768 * (4 + 4 + 2));
     HIPCHK(launch_clip_vision_assemble(w.v_patch, h->v_cls, h->v_pos, h->v_pre.g, h->v_pre.b, h->v_layers[0].ln1.g,
-                                       h->v_layers[0].ln1.b, 1e-5f, w.v_x, w.v_xb, B, s));
+                                       h->v_layers[0].ln1.b, 1e-5f, h->opt.clip_res16 ? nullptr : w.v_x,
+                                       h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.v_x) : nullptr, w.v_xb, B, s));
   }
   CHK(run_clip_encoder(h, h->v_layers, 768, 3072, 12, w.v_x, w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50,
                        nullptr, w.v_xc, w.v_ctxc, w.sk_vit, w.sk_elems, s));
@@ -744,8 +758,9 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
   Workspace& w = h->ws;
   {
     ProfScope ps(h, s, PK_EMBED, 10.0 * B * L * 512, (double)B * L * 512 * (4 + 4 + 4 + 2));
-    HIPCHK(launch_clip_text_embed(ids, h->t_tok, h->t_pos, h->t_layers[0].ln1.g, h->t_layers[0].ln1.b, 1e-5f, w.t_x,
-                                  w.t_xb, B, L, 512, s));
+    HIPCHK(launch_clip_text_embed(ids, h->t_tok, h->t_pos, h->t_layers[0].ln1.g, h->t_layers[0].ln1.b, 1e-5f,
+                                  h->opt.clip_res16 ? nullptr : w.t_x,
+                                  h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.t_x) : nullptr, w.t_xb, B, L, 512, s));
   }
   HIPCHK(launch_eos_index(ids, w.t_eos, B, L, h->eos_id, s));
   CHK(run_clip_encoder(h, h->t_layers, 512, 2048, 8, w.t_x, w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, w.t_eos,

@@ -46,6 +46,9 @@ hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd
 // s32 = s, o32 = LN(s) (both with stride ldx; may alias x); o16 = LN(s) fp16 (ldo).  C in {512, 768}.
 hipError_t launch_add_ln(const float* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps,
                          float* s32, float* o32, f16_t* o16, int ldo, int rows, int C, hipStream_t s);
+// the same with an fp16 residual stream (pre-LN CLIP, option clip_res16): s16 = s (may alias x)
+hipError_t launch_add_ln(const f16_t* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps,
+                         f16_t* s16, f16_t* o16, int ldo, int rows, int C, hipStream_t s);
 
 // Fused multi-head attention, head_dim 64, L <= 128: qkv fp16 [B*L][ldqkv] with q at col h*64,
 // k at D + h*64, v at 2D + h*64 (D = H*64); mask int32 [B][L] (1 keep) or null; out fp16 [B*L][ldo].
@@ -61,25 +64,28 @@ hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, i
                               const float* b, float eps, int rows, int C, hipStream_t s);
 hipError_t launch_hilo_rows(const f16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
                             hipStream_t s);
-// CLIP text embeddings (tok + pos) -> x fp32, then LN1 of layer 0 -> xb fp16
+// CLIP text embeddings (tok + pos) -> x fp32 (or x16 fp16: exactly one non-null), then LN1 of layer 0
+// -> xb fp16
 hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
-                                  const float* b, float eps, float* x, f16_t* xb, int B, int L, int H,
+                                  const float* b, float eps, float* x, f16_t* x16, f16_t* xb, int B, int L, int H,
                                   hipStream_t s);
 // CLIP patch im2col with normalisation: img uint8 [B,224,224,3] -> A fp16 [B*49][3072]
 hipError_t launch_clip_im2col(const uint8_t* img, f16_t* A, int B, hipStream_t s);
-// CLIP vision: x = preLN(cat(cls, patches) + pos) -> x fp32 [B*50][768], xb = LN1(x) fp16
+// CLIP vision: x = preLN(cat(cls, patches) + pos) -> x fp32 [B*50][768] (or x16 fp16: exactly one
+// non-null), xb = LN1(x) fp16
 hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
                                        const float* pre_g, const float* pre_b, const float* ln1_g,
-                                       const float* ln1_b, float eps, float* x, f16_t* xb, int B,
+                                       const float* ln1_b, float eps, float* x, f16_t* x16, f16_t* xb, int B,
                                        hipStream_t s);
 // EOS index per row (first == eos_id, or argmax when eos_id == 2)
 hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int eos_id, hipStream_t s);
 // gather rows: out fp16 [B][C] = LN(x[row_index(b)]) where row_index = b*L + (idx ? idx[b] : 0)
 hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const float* g, const float* b, float eps,
                             f16_t* out, float* out32, int B, int C, hipStream_t s);
-// compact copies of rows b*L + (idx ? idx[b] : 0) of a fp16 and an fp32 [.,C] buffer
-hipError_t launch_gather_rows2(const f16_t* a16, const float* a32, const int32_t* idx, int L, int C, f16_t* o16,
-                               float* o32, int B, hipStream_t s);
+// compact copies of rows b*L + (idx ? idx[b] : 0) of a fp16 and an fp32 (a32, or fp16 a32h: exactly
+// one non-null) [.,C] buffer; o32 is fp32 either way
+hipError_t launch_gather_rows2(const f16_t* a16, const float* a32, const f16_t* a32h, const int32_t* idx, int L,
+                               int C, f16_t* o16, float* o32, int B, hipStream_t s);
 // L2-normalise rows of fp32 [B][C] in place (C multiple of 64)
 hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s);
 // two 768->256->2 heads (fp32) from CLS rows x[b*L*768]; writes logits and softmax[:,1] scores

@@ -2,6 +2,8 @@
 // One 64-lane wave per row of width C in {512, 768}: every lane holds C/256 float4 in registers,
 // so a row is read once, reduced with DPP/shuffle trees and written once (fp32 residual stream
 // and/or fp16 GEMM operand).  Variance is the two-pass mean((x-mean)^2) in fp32 like torch.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -55,6 +57,36 @@ MMF_DEV void store_row(const float4 (&v)[NV], float* y32, f16_t* y16, int lane) 
   }
 }
 
+// CLIP residual-stream rows: fp32, or fp16 (option clip_res16)
+template <int NV, typename XT>
+MMF_DEV void load_x(float4 (&v)[NV], const XT* x, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if constexpr (std::is_same_v<XT, float>) {
+      v[i] = *reinterpret_cast<const float4*>(x + c);
+    } else {
+      const uint2 a = *reinterpret_cast<const uint2*>(x + c);
+      v[i] = make_float4(lo_h(a.x), hi_h(a.x), lo_h(a.y), hi_h(a.y));
+    }
+  }
+}
+// stores v as XT and leaves v holding the stored (rounded) values
+template <int NV, typename XT>
+MMF_DEV void store_x(float4 (&v)[NV], XT* x, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if constexpr (std::is_same_v<XT, float>) {
+      *reinterpret_cast<float4*>(x + c) = v[i];
+    } else {
+      const uint2 h = make_uint2(pack2h(v[i].x, v[i].y), pack2h(v[i].z, v[i].w));
+      *reinterpret_cast<uint2*>(x + c) = h;
+      v[i] = make_float4(lo_h(h.x), hi_h(h.x), lo_h(h.y), hi_h(h.y));
+    }
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx, const float* add, int ldadd,
                                                         const float* g, const float* b, float eps, float* y32,
@@ -73,26 +105,24 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx,
 //   pre-LN (CLIP, TF clip:357-385):   s32 = s (the new residual stream), o16 = LN(s)
 //   post-LN (RoBERTa, TF roberta:329-399): o32 = LN(s) (the new residual stream), o16 = LN(s)
 // s32 / o32 may alias x (each wave reads its whole row before writing it).
-template <int NV>
-__global__ __launch_bounds__(256) void add_ln_kernel(const float* x, int ldx, const f16_t* y, int ldy, const float* g,
-                                                     const float* b, float eps, float* s32, float* o32,
+// XT = f16_t: the CLIP residual stream held in fp16 (x and s32 fp16; o32 unused)
+template <int NV, typename XT>
+__global__ __launch_bounds__(256) void add_ln_kernel(const XT* x, int ldx, const f16_t* y, int ldy, const float* g,
+                                                     const float* b, float eps, XT* s32, float* o32,
                                                      f16_t* o16, int ldo, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   float4 v[NV];
   uint2 a[NV];
-  const float* xr = x + (size_t)row * ldx;
   const f16_t* yr = y + (size_t)row * ldy;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    v[i] = *reinterpret_cast<const float4*>(xr + (i * 64 + lane) * 4);
-    a[i] = *reinterpret_cast<const uint2*>(yr + (i * 64 + lane) * 4);
-  }
+  for (int i = 0; i < NV; ++i) a[i] = *reinterpret_cast<const uint2*>(yr + (i * 64 + lane) * 4);
+  load_x<NV>(v, x + (size_t)row * ldx, lane);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     v[i].x += lo_h(a[i].x); v[i].y += hi_h(a[i].x); v[i].z += lo_h(a[i].y); v[i].w += hi_h(a[i].y);
   }
-  if (s32) store_row<NV>(v, s32 + (size_t)row * ldx, nullptr, lane);
+  if (s32) store_x<NV>(v, s32 + (size_t)row * ldx, lane);
   ln_row<NV>(v, g, b, eps, NV * 256, lane);
   store_row<NV>(v, o32 ? o32 + (size_t)row * ldx : nullptr, o16 + (size_t)row * ldo, lane);
 }
@@ -201,10 +231,10 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
   }
 }
 
-// CLIP text: x = tok[id] + pos[t] (fp32 residual stream); xb = LN1_layer0(x) (fp16)
-template <int NV>
+// CLIP text: x = tok[id] + pos[t] (residual stream, fp32 or fp16); xb = LN1_layer0(x) (fp16)
+template <int NV, typename XT>
 __global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids, const float* tok, const float* pos,
-                                                              const float* g, const float* b, float eps, float* x,
+                                                              const float* g, const float* b, float eps, XT* x,
                                                               f16_t* xb, int rows, int L) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -213,7 +243,7 @@ __global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids
   float4 v[NV];
   load_row<NV>(v, tok + (size_t)ids[row] * C, lane);
   add_row<NV>(v, pos + (size_t)t * C, lane);
-  store_row<NV>(v, x + (size_t)row * C, nullptr, lane);
+  store_x<NV>(v, x + (size_t)row * C, lane);  // rounds v to XT: LN1 sees the stored stream
   ln_row<NV>(v, g, b, eps, C, lane);
   store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
 }
@@ -250,10 +280,11 @@ __global__ __launch_bounds__(256) void clip_im2col_kernel(const uint8_t* img, f1
 }
 
 // CLIP vision: e = (t==0 ? class_emb : patch[b*49+t-1]) + pos[t]; x = pre_LN(e); xb = LN1(x)
+template <typename XT>
 __global__ __launch_bounds__(256) void clip_vision_assemble_kernel(const float* patches, const float* cls,
                                                                    const float* pos, const float* pg,
                                                                    const float* pb, const float* g1,
-                                                                   const float* b1, float eps, float* x,
+                                                                   const float* b1, float eps, XT* x,
                                                                    f16_t* xb, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -264,7 +295,7 @@ __global__ __launch_bounds__(256) void clip_vision_assemble_kernel(const float* 
   else load_row<NV>(v, patches + ((size_t)bi * 49 + t - 1) * C, lane);
   add_row<NV>(v, pos + (size_t)t * C, lane);
   ln_row<NV>(v, pg, pb, eps, C, lane);
-  store_row<NV>(v, x + (size_t)row * C, nullptr, lane);
+  store_x<NV>(v, x + (size_t)row * C, lane);  // rounds v to XT: LN1 sees the stored stream
   ln_row<NV>(v, g1, b1, eps, C, lane);
   store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
 }
@@ -303,15 +334,22 @@ __global__ __launch_bounds__(256) void gather_ln_kernel(const float* x, const in
   store_row<NV>(v, out32 ? out32 + (size_t)bi * C : nullptr, out ? out + (size_t)bi * C : nullptr, lane);
 }
 
-// rows b*L + (idx ? idx[b] : 0) of a fp16 [.,C] and an fp32 [.,C] buffer -> compact [B,C] copies
-__global__ __launch_bounds__(256) void gather_rows2_kernel(const f16_t* a16, const float* a32, const int32_t* idx,
+// rows b*L + (idx ? idx[b] : 0) of a fp16 [.,C] and an fp32 (or fp16: XT) [.,C] buffer -> compact
+// [B,C] copies (o32 always fp32)
+template <typename XT>
+__global__ __launch_bounds__(256) void gather_rows2_kernel(const f16_t* a16, const XT* a32, const int32_t* idx,
                                                            int L, int C, f16_t* o16, float* o32, int B) {
   const int bi = blockIdx.x;
   if (bi >= B) return;
   const size_t row = (size_t)bi * L + (idx ? idx[bi] : 0);
   for (int c = threadIdx.x * 4; c < C; c += 256 * 4) {
     *reinterpret_cast<uint2*>(o16 + (size_t)bi * C + c) = *reinterpret_cast<const uint2*>(a16 + row * C + c);
-    *reinterpret_cast<float4*>(o32 + (size_t)bi * C + c) = *reinterpret_cast<const float4*>(a32 + row * C + c);
+    if constexpr (std::is_same_v<XT, float>) {
+      *reinterpret_cast<float4*>(o32 + (size_t)bi * C + c) = *reinterpret_cast<const float4*>(a32 + row * C + c);
+    } else {
+      const uint2 a = *reinterpret_cast<const uint2*>(a32 + row * C + c);
+      *reinterpret_cast<float4*>(o32 + (size_t)bi * C + c) = make_float4(lo_h(a.x), hi_h(a.x), lo_h(a.y), hi_h(a.y));
+    }
   }
 }
 
@@ -342,17 +380,32 @@ hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd
   return hipGetLastError();
 }
 
-hipError_t launch_add_ln(const float* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps,
-                         float* s32, float* o32, f16_t* o16, int ldo, int rows, int C, hipStream_t s) {
+namespace {
+template <typename XT>
+hipError_t add_ln_any(const XT* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps, XT* s32,
+                      float* o32, f16_t* o16, int ldo, int rows, int C, hipStream_t s) {
   const dim3 grid((rows + 3) / 4);
   if (!o16) return hipErrorInvalidValue;
   if (C == 768)
-    hipLaunchKernelGGL(add_ln_kernel<3>, grid, dim3(256), 0, s, x, ldx, y, ldy, g, b, eps, s32, o32, o16, ldo, rows);
+    hipLaunchKernelGGL((add_ln_kernel<3, XT>), grid, dim3(256), 0, s, x, ldx, y, ldy, g, b, eps, s32, o32, o16, ldo,
+                       rows);
   else if (C == 512)
-    hipLaunchKernelGGL(add_ln_kernel<2>, grid, dim3(256), 0, s, x, ldx, y, ldy, g, b, eps, s32, o32, o16, ldo, rows);
+    hipLaunchKernelGGL((add_ln_kernel<2, XT>), grid, dim3(256), 0, s, x, ldx, y, ldy, g, b, eps, s32, o32, o16, ldo,
+                       rows);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_add_ln(const float* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps,
+                         float* s32, float* o32, f16_t* o16, int ldo, int rows, int C, hipStream_t s) {
+  return add_ln_any(x, ldx, y, ldy, g, b, eps, s32, o32, o16, ldo, rows, C, s);
+}
+
+hipError_t launch_add_ln(const f16_t* x, int ldx, const f16_t* y, int ldy, const float* g, const float* b, float eps,
+                         f16_t* s16, f16_t* o16, int ldo, int rows, int C, hipStream_t s) {
+  return add_ln_any(x, ldx, y, ldy, g, b, eps, s16, nullptr, o16, ldo, rows, C, s);
 }
 
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
@@ -366,12 +419,16 @@ hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const flo
 }
 
 hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
-                                  const float* b, float eps, float* x, f16_t* xb, int B, int L, int H,
+                                  const float* b, float eps, float* x, f16_t* x16, f16_t* xb, int B, int L, int H,
                                   hipStream_t s) {
-  if (H != 512) return hipErrorInvalidValue;
+  if (H != 512 || !x == !x16) return hipErrorInvalidValue;
   const int rows = B * L;
-  hipLaunchKernelGGL(clip_text_embed_kernel<2>, dim3((rows + 3) / 4), dim3(256), 0, s, ids, tok, pos, g, b, eps, x,
-                     xb, rows, L);
+  if (x)
+    hipLaunchKernelGGL((clip_text_embed_kernel<2, float>), dim3((rows + 3) / 4), dim3(256), 0, s, ids, tok, pos, g, b,
+                       eps, x, xb, rows, L);
+  else
+    hipLaunchKernelGGL((clip_text_embed_kernel<2, f16_t>), dim3((rows + 3) / 4), dim3(256), 0, s, ids, tok, pos, g, b,
+                       eps, x16, xb, rows, L);
   return hipGetLastError();
 }
 
@@ -384,11 +441,16 @@ hipError_t launch_clip_im2col(const uint8_t* img, f16_t* A, int B, hipStream_t s
 
 hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
                                        const float* pre_g, const float* pre_b, const float* ln1_g,
-                                       const float* ln1_b, float eps, float* x, f16_t* xb, int B,
+                                       const float* ln1_b, float eps, float* x, f16_t* x16, f16_t* xb, int B,
                                        hipStream_t s) {
+  if (!x == !x16) return hipErrorInvalidValue;
   const int rows = B * 50;
-  hipLaunchKernelGGL(clip_vision_assemble_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, patches, cls, pos, pre_g,
-                     pre_b, ln1_g, ln1_b, eps, x, xb, rows);
+  if (x)
+    hipLaunchKernelGGL(clip_vision_assemble_kernel<float>, dim3((rows + 3) / 4), dim3(256), 0, s, patches, cls, pos,
+                       pre_g, pre_b, ln1_g, ln1_b, eps, x, xb, rows);
+  else
+    hipLaunchKernelGGL(clip_vision_assemble_kernel<f16_t>, dim3((rows + 3) / 4), dim3(256), 0, s, patches, cls, pos,
+                       pre_g, pre_b, ln1_g, ln1_b, eps, x16, xb, rows);
   return hipGetLastError();
 }
 
@@ -410,10 +472,13 @@ hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const flo
   return hipGetLastError();
 }
 
-hipError_t launch_gather_rows2(const f16_t* a16, const float* a32, const int32_t* idx, int L, int C, f16_t* o16,
-                               float* o32, int B, hipStream_t s) {
-  if (C & 3) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gather_rows2_kernel, dim3(B), dim3(256), 0, s, a16, a32, idx, L, C, o16, o32, B);
+hipError_t launch_gather_rows2(const f16_t* a16, const float* a32, const f16_t* a32h, const int32_t* idx, int L,
+                               int C, f16_t* o16, float* o32, int B, hipStream_t s) {
+  if ((C & 3) || !a32 == !a32h) return hipErrorInvalidValue;
+  if (a32)
+    hipLaunchKernelGGL(gather_rows2_kernel<float>, dim3(B), dim3(256), 0, s, a16, a32, idx, L, C, o16, o32, B);
+  else
+    hipLaunchKernelGGL(gather_rows2_kernel<f16_t>, dim3(B), dim3(256), 0, s, a16, a32h, idx, L, C, o16, o32, B);
   return hipGetLastError();
 }
 
