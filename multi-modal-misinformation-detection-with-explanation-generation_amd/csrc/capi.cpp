@@ -48,6 +48,12 @@ uint16_t f2h_host(float f) {
   return b;
 }
 
+float h2f_host(uint16_t b) {
+  _Float16 h;
+  std::memcpy(&h, &b, 2);
+  return (float)h;
+}
+
 struct HostT {
   std::vector<int64_t> shape;
   std::vector<float> f;
@@ -61,7 +67,9 @@ struct Lin16 {
   float* w32 = nullptr;  // fp32 copy of w (EfficientNet 1x1 convs: the effnet_fp32 tower)
 };
 struct LNp { float* g = nullptr; float* b = nullptr; };
-struct EncLayer { Lin16 qkv, o, fc1, fc2; LNp ln1, ln2; };
+// qkv_f / fc1_f (CLIP): the QKV and FFN-1 projections with their input LayerNorm folded in (lazy
+// LN, gemm.hip): w' = fp16(w diag(gamma)), bias c = b + w beta, u = rows of w' summed (fp16 values)
+struct EncLayer { Lin16 qkv, o, fc1, fc2; LNp ln1, ln2; Lin16 qkv_f, fc1_f; float *qkv_u = nullptr, *fc1_u = nullptr; };
 
 struct EffBlock {
   int expand, k, stride, cin, cout, cexp, csq, residual;
@@ -88,6 +96,9 @@ struct Workspace {
   f16_t *t_xb = nullptr, *t_qkv = nullptr, *t_ctx = nullptr, *t_h = nullptr, *t_pool = nullptr, *t_ctxc = nullptr;
   float *t_x = nullptr, *t_emb = nullptr, *t_xc = nullptr;
   int32_t* t_eos = nullptr;
+  // lazy-LN row partials of the CLIP streams (gemm.hip), two per tower (a producer writes the one
+  // its stream's previous partials are not in): [rows padded to 256][kLnP] float2
+  float2 *v_st[2] = {nullptr, nullptr}, *t_st[2] = {nullptr, nullptr};
   // EfficientNet
   f16_t *e_a = nullptr, *e_b = nullptr, *e_exp = nullptr, *e_dw = nullptr;
   float *e_pool = nullptr, *e_scale = nullptr;
@@ -117,6 +128,7 @@ struct Options {
   int gemm_prio = 2;    // s_setprio 1 for waves 0-3 of the persistent GEMM (+0.4 % step; A/B)
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
   int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
+  int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -125,7 +137,7 @@ const OptName kOptNames[] = {
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
     {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
-    {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"},
+    {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -323,20 +335,65 @@ int load_f32(mmf_handle* h, float** dst, const std::string& name, size_t n) {
   GET(t, name, n);
   return up_f32(h, dst, t->f);
 }
+// per-column vectors the lazy-LN epilogues DMA in 256-column blocks: zero-padded by 256
+constexpr int kColPad = 256;
+constexpr int kLnP = 8;  // lazy-LN partials per row a GEMM accepts (gemm.hip kLnPMax)
+int up_f32_padded(mmf_handle* h, float** dst, std::vector<float> v) {
+  v.resize(v.size() + kColPad, 0.f);
+  return up_f32(h, dst, v);
+}
+int load_f32_padded(mmf_handle* h, float** dst, const std::string& name, size_t n) {
+  GET(t, name, n);
+  return up_f32_padded(h, dst, t->f);
+}
 int load_ln(mmf_handle* h, LNp* ln, const std::string& p, int n) {
-  CHK(load_f32(h, &ln->g, p + ".weight", n));
-  return load_f32(h, &ln->b, p + ".bias", n);
+  CHK(load_f32_padded(h, &ln->g, p + ".weight", n));
+  return load_f32_padded(h, &ln->b, p + ".bias", n);
 }
 int load_lin(mmf_handle* h, Lin16* l, const std::string& p, int out, int in, bool bias) {
   GET(w, p + ".weight", (size_t)out * in);
   CHK(up_f16(h, &l->w, w->f));
-  if (bias) CHK(load_f32(h, &l->b, p + ".bias", out));
+  if (bias) CHK(load_f32_padded(h, &l->b, p + ".bias", out));
   l->out = out;
   l->in = in;
   return 0;
 }
-// fused QKV: rows [q; k; v] of [3*H][H] + bias
-int load_qkv(mmf_handle* h, Lin16* l, const std::string& q, const std::string& k, const std::string& v, int H) {
+// LN(x) W^T + b with LN = (gamma, beta) folded (gemm.hip lazy LN): w' = fp16(w diag(gamma)),
+// u = sum_k w'[n][k] over the fp16 values (so acc - mean u is exactly sum_k w'(s_k - mean)),
+// c = b + w beta, both in double
+int fold_ln_lin(mmf_handle* h, Lin16* dst, float** u, const std::vector<float>& w, const std::vector<float>& b,
+                int out, int in, const std::vector<float>& g, const std::vector<float>& beta) {
+  std::vector<float> wf((size_t)out * in), uv(out), c(out);
+  for (int n = 0; n < out; ++n) {
+    double su = 0.0, sc = b[n];
+    for (int k = 0; k < in; ++k) {
+      const float x = w[(size_t)n * in + k] * g[k];
+      wf[(size_t)n * in + k] = x;
+      su += (double)h2f_host(f2h_host(x));
+      sc += (double)w[(size_t)n * in + k] * beta[k];
+    }
+    uv[n] = (float)su;
+    c[n] = (float)sc;
+  }
+  CHK(up_f16(h, &dst->w, wf));
+  CHK(up_f32_padded(h, &dst->b, c));
+  CHK(up_f32_padded(h, u, uv));
+  dst->out = out;
+  dst->in = in;
+  return 0;
+}
+int fold_ln_named(mmf_handle* h, Lin16* dst, float** u, const std::string& lin, int out, int in,
+                  const std::string& ln) {
+  GET(w, lin + ".weight", (size_t)out * in);
+  GET(b, lin + ".bias", out);
+  GET(g, ln + ".weight", in);
+  GET(be, ln + ".bias", in);
+  return fold_ln_lin(h, dst, u, w->f, b->f, out, in, g->f, be->f);
+}
+// fused QKV: rows [q; k; v] of [3*H][H] + bias; with ln (non-empty) also the LN-folded copy
+int load_qkv(mmf_handle* h, EncLayer* L, const std::string& q, const std::string& k, const std::string& v, int H,
+             const std::string& ln) {
+  Lin16* l = &L->qkv;
   std::vector<float> w((size_t)3 * H * H), b((size_t)3 * H);
   const std::string names[3] = {q, k, v};
   for (int i = 0; i < 3; ++i) {
@@ -346,10 +403,13 @@ int load_qkv(mmf_handle* h, Lin16* l, const std::string& q, const std::string& k
     std::memcpy(b.data() + (size_t)i * H, tb->f.data(), sizeof(float) * H);
   }
   CHK(up_f16(h, &l->w, w));
-  CHK(up_f32(h, &l->b, b));
+  CHK(up_f32_padded(h, &l->b, b));
   l->out = 3 * H;
   l->in = H;
-  return 0;
+  if (ln.empty()) return 0;
+  GET(g, ln + ".weight", H);
+  GET(be, ln + ".bias", H);
+  return fold_ln_lin(h, &L->qkv_f, &L->qkv_u, w, b, 3 * H, H, g->f, be->f);
 }
 
 // BatchNorm (eval) folded into the preceding conv: w' = w * g/sqrt(v+eps), b' = beta - m*g/sqrt(v+eps)
@@ -390,7 +450,7 @@ int finalize_text(mmf_handle* h) {
   for (int i = 0; i < 12; ++i) {
     const std::string l = p + "encoder.layer." + std::to_string(i) + ".";
     EncLayer& L = h->r_layers[i];
-    CHK(load_qkv(h, &L.qkv, l + "attention.self.query", l + "attention.self.key", l + "attention.self.value", 768));
+    CHK(load_qkv(h, &L, l + "attention.self.query", l + "attention.self.key", l + "attention.self.value", 768, ""));
     CHK(load_lin(h, &L.o, l + "attention.output.dense", 768, 768, true));
     CHK(load_ln(h, &L.ln1, l + "attention.output.LayerNorm", 768));
     CHK(load_lin(h, &L.fc1, l + "intermediate.dense", 3072, 768, true));
@@ -481,10 +541,11 @@ int finalize_clip_layers(mmf_handle* h, EncLayer* layers, const std::string& bas
   for (int i = 0; i < 12; ++i) {
     const std::string l = base + std::to_string(i) + ".";
     EncLayer& L = layers[i];
-    CHK(load_qkv(h, &L.qkv, l + "self_attn.q_proj", l + "self_attn.k_proj", l + "self_attn.v_proj", H));
+    CHK(load_qkv(h, &L, l + "self_attn.q_proj", l + "self_attn.k_proj", l + "self_attn.v_proj", H, l + "layer_norm1"));
     CHK(load_lin(h, &L.o, l + "self_attn.out_proj", H, H, true));
     CHK(load_ln(h, &L.ln1, l + "layer_norm1", H));
     CHK(load_lin(h, &L.fc1, l + "mlp.fc1", I, H, true));
+    CHK(fold_ln_named(h, &L.fc1_f, &L.fc1_u, l + "mlp.fc1", I, H, l + "layer_norm2"));
     CHK(load_lin(h, &L.fc2, l + "mlp.fc2", H, I, true));
     CHK(load_ln(h, &L.ln2, l + "layer_norm2", H));
   }
@@ -556,6 +617,36 @@ int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   ProfScope ps(h, s, gemm_config(g) * kGemmActs + g.act, 2.0 * M * N * K, 2.0 * (M * K + N * K) + M * N * out_b);
   HIPCHK(launch_gemm(g, s));
   return 0;
+}
+
+// Lazy LayerNorm (option lazy_ln, gemm.hip): a row stream's statistics as partials
+struct LnStats {
+  float2* p = nullptr;  // [rows padded to 256][P]
+  int P = 0, tn = 0;
+};
+// consumer: LN(s) W^T + b with the LN folded into (w', u, c) -- s = raw rows with statistics st
+GemmArgs ln_consumer(const f16_t* s_rows, int ld, const Lin16& folded, const float* u, const LnStats& st, int M) {
+  GemmArgs g = gemm_args(s_rows, ld, folded, M);
+  g.epi = 1;
+  g.ln_in = st.p;
+  g.ln_in_P = st.P;
+  g.ln_in_tn = st.tn;
+  g.ln_u = u;
+  g.ln_eps = 1e-5f;
+  return g;
+}
+// producer: stream += A W^T + b in place; the new stream's statistics go to `out`
+GemmArgs ln_producer(const f16_t* A, int lda, const Lin16& l, f16_t* stream, int M, float2* out, LnStats* produced) {
+  GemmArgs g = gemm_args(A, lda, l, M);
+  g.res16 = stream;
+  g.c16 = stream;
+  g.ln_out = out;
+  g.ln_eps = 1e-5f;
+  g.epi = 2;
+  produced->p = out;
+  produced->tn = gemm_ln_tn(g);
+  produced->P = (l.out + produced->tn - 1) / produced->tn;
+  return g;
 }
 
 int attn(mmf_handle* h, const f16_t* qkv, int ld, const int32_t* mask, f16_t* out, int ldo, int B, int L, int H,
@@ -671,15 +762,24 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
 // Only one row per sequence is consumed after the last layer (CLS for the ViT, EOS for the text
 // tower: TF clip:561-582, 650-651): the last layer's out-proj / MLP run on those B rows, gathered
 // into compact buffers (xc fp32, ctxc fp16); on return xc holds them (before the final LN).
+// independent of the batch size: rows must not change with the batch they run in (the lazy and
+// materialised LayerNorms round differently), so sharding rows over GPUs keeps results bit-identical
+bool clip_lazy(mmf_handle* h, int /*M*/) { return h->opt.lazy_ln && h->opt.clip_res16; }
+
 int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, f16_t* xb, f16_t* qkv,
                      f16_t* ctx, f16_t* hid, const int32_t* mask, int causal, int B, int L,
                      const int32_t* last_rows, float* xc, f16_t* ctxc, float* skws, size_t sk_elems,
-                     hipStream_t s) {
+                     float2* const* st, hipStream_t s) {
   const int M = B * L;
   f16_t* x16 = h->opt.clip_res16 ? reinterpret_cast<f16_t*>(x) : nullptr;
+  // lazy LN (gemm.hip; the caller's embedding wrote st[0] with the stream's statistics): the QKV /
+  // FFN-1 GEMMs read the raw stream x16 with LN1 / LN2 folded, out-proj / FFN-2 add into it
+  const bool lazy = clip_lazy(h, M);
+  LnStats cur{st[0], 1, H};
+  int sti = 0;
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = layers[i];
-    GemmArgs g = gemm_args(xb, H, Ly.qkv, M);
+    GemmArgs g = lazy ? ln_consumer(x16, H, Ly.qkv_f, Ly.qkv_u, cur, M) : gemm_args(xb, H, Ly.qkv, M);
     g.c16 = qkv;
     CHK(gemm(h, g, s));
     CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
@@ -699,6 +799,20 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
       g.c32 = xc;
       CHK(gemm(h, g, s));
       break;
+    }
+    if (lazy) {
+      LnStats nxt;
+      sti ^= 1;
+      CHK(gemm(h, ln_producer(ctx, H, Ly.o, x16, M, st[sti], &nxt), s));
+      cur = nxt;
+      g = ln_consumer(x16, H, Ly.fc1_f, Ly.fc1_u, cur, M);
+      g.act = 2;  // quick_gelu
+      g.c16 = hid;
+      CHK(gemm(h, g, s));
+      sti ^= 1;
+      CHK(gemm(h, ln_producer(hid, I, Ly.fc2, x16, M, st[sti], &nxt), s));
+      cur = nxt;
+      continue;
     }
     // out-proj / FFN-2 write their fp16 branch output y (out-proj into `hid`, free until FFN-1;
     // FFN-2 into `ctx`, free after out-proj); add+LN adds it to the fp32 residual stream x in place
@@ -738,10 +852,11 @@ int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStre
     ProfScope ps(h, s, PK_EMBED, 16.0 * B * 50 * 768, (double)B * 50 * 768 * (4 + 4 + 2));
     HIPCHK(launch_clip_vision_assemble(w.v_patch, h->v_cls, h->v_pos, h->v_pre.g, h->v_pre.b, h->v_layers[0].ln1.g,
                                        h->v_layers[0].ln1.b, 1e-5f, h->opt.clip_res16 ? nullptr : w.v_x,
-                                       h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.v_x) : nullptr, w.v_xb, B, s));
+                                       h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.v_x) : nullptr, w.v_xb,
+                                       clip_lazy(h, B * 50) ? w.v_st[0] : nullptr, B, s));
   }
   CHK(run_clip_encoder(h, h->v_layers, 768, 3072, 12, w.v_x, w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50,
-                       nullptr, w.v_xc, w.v_ctxc, w.sk_vit, w.sk_elems, s));
+                       nullptr, w.v_xc, w.v_ctxc, w.sk_vit, w.sk_elems, w.v_st, s));
   HIPCHK(launch_gather_ln(w.v_xc, nullptr, 1, h->v_post.g, h->v_post.b, 1e-5f, w.v_cls, nullptr, B, 768, s));
   Lin16 pj;
   pj.w = h->v_proj;
@@ -760,11 +875,12 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
     ProfScope ps(h, s, PK_EMBED, 10.0 * B * L * 512, (double)B * L * 512 * (4 + 4 + 4 + 2));
     HIPCHK(launch_clip_text_embed(ids, h->t_tok, h->t_pos, h->t_layers[0].ln1.g, h->t_layers[0].ln1.b, 1e-5f,
                                   h->opt.clip_res16 ? nullptr : w.t_x,
-                                  h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.t_x) : nullptr, w.t_xb, B, L, 512, s));
+                                  h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.t_x) : nullptr, w.t_xb,
+                                  clip_lazy(h, B * L) ? w.t_st[0] : nullptr, B, L, 512, s));
   }
   HIPCHK(launch_eos_index(ids, w.t_eos, B, L, h->eos_id, s));
   CHK(run_clip_encoder(h, h->t_layers, 512, 2048, 8, w.t_x, w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, w.t_eos,
-                       w.t_xc, w.t_ctxc, w.sk_ctext, w.sk_elems, s));
+                       w.t_xc, w.t_ctxc, w.sk_ctext, w.sk_elems, w.t_st, s));
   HIPCHK(launch_gather_ln(w.t_xc, nullptr, 1, h->t_final.g, h->t_final.b, 1e-5f, w.t_pool, nullptr, B, 512, s));
   Lin16 pj;
   pj.w = h->t_proj;
@@ -1066,6 +1182,13 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   CHK(A((void**)&w.v_ctxc, (size_t)B * 768 * 2));
   CHK(A((void**)&w.t_xc, (size_t)B * 512 * 4));
   CHK(A((void**)&w.t_ctxc, (size_t)B * 512 * 2));
+  {
+    auto stats_rows = [](size_t rows) { return (rows + 255) / 256 * 256 * kLnP * sizeof(float2); };
+    for (int i = 0; i < 2; ++i) {
+      CHK(A((void**)&w.v_st[i], stats_rows(Mv)));
+      CHK(A((void**)&w.t_st[i], stats_rows(Mt)));
+    }
+  }
   w.sk_elems = (size_t)B * 9216;  // max over the compact layers of (K / 256) * N
   CHK(A((void**)&w.sk_text, w.sk_elems * 4));
   CHK(A((void**)&w.sk_vit, w.sk_elems * 4));

@@ -254,7 +254,19 @@ MMF_DEV void tile_coords(int t, int tilesM, int tilesN, int gm, int& tm, int& tn
   tn = r / gsz;
 }
 
-template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false>
+// Lazy LayerNorm (GemmArgs::epi, option lazy_ln) for the pre-LN CLIP encoders: no LayerNorm is
+// materialised.
+//  * a "producer" (out-projection / FFN-2, N = hidden width, 256x192 tiles, epi 2) adds the raw
+//    fp16 residual stream in its epilogue, stores the new stream in place and, per row and per
+//    wave, the partial statistics (mean, M2) of the STORED values over the wave's 96 columns;
+//  * a "consumer" (QKV / FFN-1, epi 1) reads the stream s itself as its A operand against
+//    W' = W diag(gamma) and finishes LN(s) W^T + b = r (s W'^T - mean u) + c with u = W' 1 and
+//    c = b + W beta (folded on the host), mean / r = rstd from the partials (Chan's combination).
+// The partials of a consumer tile's 256 rows and its column vectors (u, c) are LDS-DMA'd during
+// the second K-step and combined into (mean, rstd) per row at the top of the third.
+constexpr int kLnPMax = 8;  // partials per row a reader accepts
+
+template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
                                                                      int gm) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
@@ -268,6 +280,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   constexpr int STAGE = (BM + BN) * BK;
   static_assert(NW == 8 || NW == 4, "4 or 8 waves");
   __shared__ __attribute__((aligned(16))) f16_t lds[2 * STAGE];
+  constexpr bool ROWST = EPI == 1;  // reads row statistics
+  static_assert(EPI == 0 || BM == 256, "lazy-LN epilogues assume 256-row tiles");
+  __shared__ __attribute__((aligned(16))) float2 lds_rows[ROWST ? BM * kLnPMax : 2];
+  // column vectors of a consumer tile: u | bias (bias through LDS frees the 4*NI bias registers the
+  // plain path holds across the K loop)
+  constexpr int kBiasCol = 256;
+  __shared__ __attribute__((aligned(16))) float lds_cols[ROWST ? 512 : 4];
+  __shared__ __attribute__((aligned(16))) float2 lds_stat[ROWST ? BM : 2];  // (mean, rstd) per tile row
 
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -299,6 +319,27 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
     glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
     glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
   };
+  // lazy-LN epilogue operands of tile (m0_, n0_) -> LDS (issued in the second K-step: every wave
+  // has left the previous tile's epilogue by then; the K-step barriers' vmcnt(0) covers them)
+  auto epi_dma = [&](int m0_, int n0_) {
+    typedef __attribute__((address_space(3))) char lds_char_t;
+    if constexpr (ROWST) {  // the 256 rows' partials: 256 * P * 8 B, contiguous, whole KBs
+      const uint32_t bytes = (uint32_t)BM * g.ln_in_P * 8u;
+      const char* src = reinterpret_cast<const char*>(g.ln_in) + (size_t)m0_ * g.ln_in_P * 8;
+      for (uint32_t off = (uint32_t)wave * 1024u; off < bytes; off += NW * 1024u)
+        __builtin_amdgcn_global_load_lds((const void*)(src + off + lane * 16),
+                                         (lds_void_t*)((lds_char_t*)lds_rows + off), 16, 0, 0);
+    }
+    if constexpr (EPI == 1) {  // u[n0 .. n0 + 256)
+      if (wave == NW - 1)
+        __builtin_amdgcn_global_load_lds((const void*)(g.ln_u + n0_ + lane * 4), (lds_void_t*)lds_cols, 16, 0, 0);
+    }
+    if constexpr (ROWST) {  // bias[n0 .. n0 + 256) (buffers padded by 256)
+      if (wave == NW - 3)
+        __builtin_amdgcn_global_load_lds((const void*)(g.bias + n0_ + lane * 4),
+                                         (lds_void_t*)((lds_char_t*)lds_cols + kBiasCol * 4), 16, 0, 0);
+    }
+  };
   stage(0, t, 0);
   __syncthreads();
   int cur = 0;
@@ -311,11 +352,65 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
     for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 bias_r[NI];  // this lane's epilogue bias columns, fetched under the K loop
+    float4 bias_r[ROWST ? 1 : NI];  // this lane's epilogue bias columns, fetched under the K loop
+    if constexpr (!ROWST) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
+      for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
+    }
+    // bias of fragment column group i (ROWST: from LDS)
+    auto bias_of = [&](int i) -> float4 {
+      if constexpr (ROWST) return *reinterpret_cast<const float4*>(lds_cols + kBiasCol + wn * TN + i * 16 + fg * 4);
+      else return bias_r[i];
+    };
 
     for (int kt = 0; kt < nk; ++kt) {
+      if constexpr (ROWST) {
+        if (kt == 1) epi_dma(m0, n0);
+        if (kt == 2) {
+          // the DMA'd partials -> (mean, rstd) of the tile's 256 rows (threads 0-255, one row each,
+          // two passes over the LDS partials with a rolled loop: few live registers here, where the
+          // K loop's accumulators are live), before this K-step's fragment reads; the epilogue
+          // reads them after the K loop's later barriers
+          if (tid < BM && BN == 192) {
+            // 256x192 tiles have register room: all kLnPMax partial slots read at once, one LDS
+            // latency.  Slots p >= P belong to the next rows or lie past the DMA'd block (any bit
+            // pattern, NaN included), so they are SELECTED out, never weighted by 0.
+            const int P = g.ln_in_P, tnin = g.ln_in_tn, C = EPI == 1 ? g.K : N;
+            const float2* pr = lds_rows + tid * P;
+            float2 pv[kLnPMax];
+            float nv[kLnPMax];
+#pragma unroll
+            for (int pi = 0; pi < kLnPMax; ++pi) {
+              const float2 v = pr[pi];
+              pv[pi] = pi < P ? v : make_float2(0.f, 0.f);
+              nv[pi] = pi < P ? (float)min(C - pi * tnin, tnin) : 0.f;
+            }
+            float s1 = 0.f;
+#pragma unroll
+            for (int pi = 0; pi < kLnPMax; ++pi) s1 += nv[pi] * pv[pi].x;
+            const float mean = s1 / (float)C;
+            float s2 = 0.f;
+#pragma unroll
+            for (int pi = 0; pi < kLnPMax; ++pi) s2 += pv[pi].y + nv[pi] * (pv[pi].x - mean) * (pv[pi].x - mean);
+            lds_stat[tid] = make_float2(mean, rsqrtf(s2 / (float)C + g.ln_eps));
+          } else if (tid < BM) {
+            const int P = g.ln_in_P, tnin = g.ln_in_tn, C = EPI == 1 ? g.K : N;
+            const float2* pr = lds_rows + tid * P;
+            float s1 = 0.f;
+#pragma unroll 1
+            for (int pi = 0; pi < P; ++pi) s1 += (float)min(C - pi * tnin, tnin) * pr[pi].x;
+            const float mean = s1 / (float)C;
+            float s2 = 0.f;
+#pragma unroll 1
+            for (int pi = 0; pi < P; ++pi) {
+              const float2 v = pr[pi];
+              s2 += v.y + (float)min(C - pi * tnin, tnin) * (v.x - mean) * (v.x - mean);
+            }
+            lds_stat[tid] = make_float2(mean, rsqrtf(s2 / (float)C + g.ln_eps));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
       else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
       const f16_t* Xs = lds + cur * STAGE;
@@ -401,19 +496,82 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
     // branch and no load that has to wait on the stores issued before it -- bias columns were
     // fetched at tile start and residual rows are loaded one fragment row AHEAD of the stores (one
     // vmcnt counter covers loads and stores in issue order).
+    // lazy LN: (mean, rstd) of fragment row j -> lds_stat[wm * TM + j * 16 + fr] (computed at kt = 2)
+    if constexpr (EPI == 2) {
+      // producer: out = acc + bias + residual, stored fp16 (in place over the residual is allowed:
+      // each element is read before it is written, by one lane), then this wave's partial
+      // (mean, M2) of the STORED values over its TN columns of each row
+      const int Pout = (N + TN - 1) / TN, pidx = tn * WGN + wn;
+      const int nval = min(max(N - (n0 + wn * TN), 0), TN);
+      // every residual fragment of the tile requested up front: one HBM latency per tile instead
+      // of one per fragment row
+      uint2 rall[MI][NI];
+#pragma unroll
+      for (int j = 0; j < MI; ++j) {
+        const uint32_t m = m0 + wm * TM + j * 16 + fr;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          rall[j][i] = buf_load_u2(rres, (m * (uint32_t)g.ldr + (n0 + wn * TN + i * 16 + fg * 4)) * 2u);
+      }
+#pragma unroll
+      for (int j = 0; j < MI; ++j) {
+        const uint2* rcur = rall[j];
+        const uint32_t m = m0 + wm * TM + j * 16 + fr;
+        uint2 pk[NI];
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int nl = wn * TN + i * 16 + fg * 4, n = n0 + nl;
+          const float rv[4] = {lo_h(rcur[i].x), hi_h(rcur[i].x), lo_h(rcur[i].y), hi_h(rcur[i].y)};
+          const float4 bi = bias_of(i);
+          pk[i] = make_uint2(pack2h(acc[i][j][0] + bi.x + rv[0], acc[i][j][1] + bi.y + rv[1]),
+                             pack2h(acc[i][j][2] + bi.z + rv[2], acc[i][j][3] + bi.w + rv[3]));
+          const uint32_t e = n < N ? m * (uint32_t)g.ldc + n : (kOOB >> 2);
+          buf_store_u2(rc16, e * 2u, pk[i]);
+          if (n < N) sum += (lo_h(pk[i].x) + hi_h(pk[i].x)) + (lo_h(pk[i].y) + hi_h(pk[i].y));
+        }
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mean = sum / (float)(nval > 0 ? nval : 1);
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const float d0 = lo_h(pk[i].x) - mean, d1 = hi_h(pk[i].x) - mean;
+          const float d2 = lo_h(pk[i].y) - mean, d3 = hi_h(pk[i].y) - mean;
+          if (n0 + wn * TN + i * 16 + fg * 4 < N) q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+        }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (fg == 0 && (int)m < M && nval > 0) g.ln_out[(size_t)m * Pout + pidx] = make_float2(mean, q);
+      }
+      continue;
+    }
     if (!has_res && !g.c32) {
       // fp16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
       // fragment of each pair so every lane stores 16 contiguous bytes (half the store issues)
 #pragma unroll
       for (int j = 0; j < MI; ++j) {
         const uint32_t m = m0 + wm * TM + j * 16 + fr;
+        float2 st = make_float2(0.f, 1.f);
+        if constexpr (EPI == 1) st = lds_stat[wm * TM + j * 16 + fr];
 #pragma unroll
         for (int i = 0; i < NI; i += 2) {
           uint2 pk[2];
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2) {
-            float v[4] = {acc[i + h2][j][0] + bias_r[i + h2].x, acc[i + h2][j][1] + bias_r[i + h2].y,
-                          acc[i + h2][j][2] + bias_r[i + h2].z, acc[i + h2][j][3] + bias_r[i + h2].w};
+            float v[4] = {acc[i + h2][j][0], acc[i + h2][j][1], acc[i + h2][j][2], acc[i + h2][j][3]};
+            if constexpr (EPI == 1) {  // r (acc - mean u), then + c (the folded bias)
+              const float4 u = *reinterpret_cast<const float4*>(lds_cols + wn * TN + (i + h2) * 16 + fg * 4);
+              v[0] = st.y * (v[0] - st.x * u.x);
+              v[1] = st.y * (v[1] - st.x * u.y);
+              v[2] = st.y * (v[2] - st.x * u.z);
+              v[3] = st.y * (v[3] - st.x * u.w);
+            }
+            const float4 bi = bias_of(i + h2);
+            v[0] += bi.x;
+            v[1] += bi.y;
+            v[2] += bi.z;
+            v[3] += bi.w;
             if (ACT != ACT_NONE) act4<ACT>(v);
             pk[h2] = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
           }
@@ -458,8 +616,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           const int n = n0 + wn * TN + i * 16 + fg * 4;
-          float v[4] = {acc[i][j][0] + bias_r[i].x, acc[i][j][1] + bias_r[i].y, acc[i][j][2] + bias_r[i].z,
-                        acc[i][j][3] + bias_r[i].w};
+          const float4 bi = bias_of(i);
+          float v[4] = {acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w};
           if (ACT != ACT_NONE) {
             act4<ACT>(v);
           }
@@ -500,6 +658,35 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
       return hipErrorInvalidValue;
   }
 #undef MMF_GLDS_CASE
+  return hipGetLastError();
+}
+
+// lazy-LN epilogues (pipelined 256-row tiles only)
+template <int BM, int BN, int WGM, int WGN>
+hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
+  const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
+  const int tiles = tilesM * tilesN;
+  const int grid = tiles < 256 ? tiles : 256;
+  const dim3 blk(64 * WGM * WGN);
+  const int gm = a.group_m;
+#define MMF_EPI_CASE(EPI, ACT)                                                                                 \
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, true, EPI>), dim3(grid), blk, 0, s, a, tilesN, tiles, \
+                     tilesM, gm)
+  if (a.epi == 1) {
+    switch (a.act) {
+      case ACT_NONE: MMF_EPI_CASE(1, ACT_NONE); break;
+      case ACT_GELU: MMF_EPI_CASE(1, ACT_GELU); break;
+      case ACT_QUICK_GELU: MMF_EPI_CASE(1, ACT_QUICK_GELU); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (a.act != ACT_NONE) {
+    return hipErrorInvalidValue;
+  } else if (a.epi == 2) {
+    MMF_EPI_CASE(2, ACT_NONE);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef MMF_EPI_CASE
   return hipGetLastError();
 }
 
@@ -587,29 +774,33 @@ static int forced_config(const GemmArgs& a) {
   return (c >= 0 && c <= 11) ? c : -1;
 }
 
+// persistent 256-row LDS-DMA tiles: the column tile that minimises whole "rounds" of 256 CUs x
+// per-tile time (wider tiles are more efficient per flop); with_128 = also consider 256x128
+static int glds_pick(const GemmArgs& a, bool with_128) {
+  // (the 256- and 192-column tiles run the half-step-pipelined K loop, configs 11 / 10)
+  const long tm = (a.M + 255) / 256;
+  const int bns[3] = {256, 192, 128}, cfg[3] = {11, 10, 5};
+  const double eff[3] = {1.0, 0.88, 0.80};  // measured per-flop efficiency (tools/gemm_bench.py)
+  int best = 11;
+  double bc = 1e30;
+  for (int i = 0; i < (with_128 ? 3 : 2); ++i) {
+    const long tiles = tm * ((a.N + bns[i] - 1) / bns[i]);
+    const double c = (double)((tiles + 255) / 256) * bns[i] / eff[i];
+    if (c < bc) { bc = c; best = cfg[i]; }
+  }
+  return best;
+}
+
 int gemm_config(const GemmArgs& a) {
+  if (a.epi == 2) return 10;  // producers: 96-column partials (P = ceil(N / 96) <= kLnPMax)
   const int f = forced_config(a);
+  if (a.epi == 1) return (f == 10 || f == 11) ? f : glds_pick(a, false);
   if (f >= 0) return f;
   if (pw_applicable(a)) return 9;  // HBM-bound 1x1 convolutions (pointwise.hip)
   if (a.N <= 32) return 0;
   if (a.N <= 64) return 1;
   if (a.M <= 512) return 2;  // skinny-M (projections, M = batch)
-  if (glds_ok(a) && a.N >= 128) {
-    // persistent 256-row LDS-DMA tiles: pick the column tile that minimises whole "rounds" of
-    // 256 CUs x per-tile time (wider tiles are more efficient per flop)
-    // (the 256- and 192-column tiles run the half-step-pipelined K loop, configs 11 / 10)
-    const long tm = (a.M + 255) / 256;
-    const int bns[3] = {256, 192, 128}, cfg[3] = {11, 10, 5};
-    const double eff[3] = {1.0, 0.88, 0.80};  // measured per-flop efficiency (tools/gemm_bench.py)
-    int best = 11;
-    double bc = 1e30;
-    for (int i = 0; i < 3; ++i) {
-      const long tiles = tm * ((a.N + bns[i] - 1) / bns[i]);
-      const double c = (double)((tiles + 255) / 256) * bns[i] / eff[i];
-      if (c < bc) { bc = c; best = cfg[i]; }
-    }
-    return best;
-  }
+  if (glds_ok(a) && a.N >= 128) return glds_pick(a, true);
   // register-staged tiles (e.g. the SE-scaled EfficientNet projects): 64x128 tiles when 128x128
   // ones would leave the chip short of workgroups (late stages, M = B * 7^2, K = 1152)
   const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
@@ -624,6 +815,18 @@ int gemm_splitk_factor(const GemmArgs& a) {
   return a.K / 256;
 }
 
+int gemm_ln_tn(const GemmArgs& a) { return gemm_config(a) == 11 ? 64 : 96; }
+
+// what the lazy-LN epilogues need (the host mirrors it before choosing that path)
+static bool epi_ok(const GemmArgs& a) {
+  if (!glds_ok(a) || a.K < 3 * BK || a.M <= 0) return false;  // partials DMA'd at kt = 1, combined at kt = 2
+  if (a.epi == 1)
+    return a.ln_in && a.ln_u && a.bias && a.c16 && !a.c32 && !a.res16 && !a.res32 && a.ln_in_P >= 1 && a.ln_in_P <= kLnPMax &&
+           a.ln_in_tn > 0 && (long)a.ln_in_P * a.ln_in_tn >= a.K;
+  if (a.epi == 2) return a.c16 && !a.c32 && a.res16 && !a.res32 && a.ln_out && (a.N + 95) / 96 <= kLnPMax;
+  return false;
+}
+
 const char* gemm_config_name(int c) {
   static const char* names[] = {"gemm_f16<256,32,4,1>",  "gemm_f16<256,64,4,1>",  "gemm_f16<64,128,1,4>",
                                 "gemm_f16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
@@ -636,6 +839,10 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
   if (a0.M <= 0 || a0.N <= 0 || a0.K <= 0) return hipSuccess;
   if ((a0.K & 7) || (a0.N & 3) || (a0.lda & 7) || (a0.ldw & 7) || (a0.ldc & 3)) return hipErrorInvalidValue;
   const GemmArgs& a = a0;
+  if (a.epi != 0) {
+    if (!epi_ok(a)) return hipErrorInvalidValue;
+    return gemm_config(a) == 11 ? run_glds_epi<256, 256, 2, 4>(a, s) : run_glds_epi<256, 192, 4, 2>(a, s);
+  }
   switch (gemm_config(a)) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);

@@ -25,7 +25,20 @@ struct GemmArgs {
   int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
+  // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
+  // (mean_p, M2_p) over consecutive column blocks of tn columns ([rows][P] float2, buffers padded
+  // to whole 256-row blocks), combined with Chan's formula by the reader.
+  int epi;                       // 0 plain; 1 A = raw rows s: out = r (acc - mean u) + bias (LN folded
+                                 // into W, bias padded by 256); 2 out = acc + bias + res16 (in
+                                 // place allowed), partials of out written
+  const float2* ln_in;           // epi 1: partials of A's rows
+  int ln_in_P, ln_in_tn;         //   their count per row and column-block width
+  const float* ln_u;             // epi 1: [N] sum_k W[n][k] (padded to N + 256)
+  float2* ln_out;                // epi 2: partials of the output rows, [rows][ceil(N / tn_out)]
+  float ln_eps;
 };
+// epi 2: the column-block width (= P partials per row of ceil(N / tn)) launch_gemm will use
+int gemm_ln_tn(const GemmArgs& a);
 // split-K factor the skinny-M (M <= 512) GEMM path uses for this (K) -- independent of M, so
 // results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
 int gemm_splitk_factor(const GemmArgs& a);
@@ -67,16 +80,18 @@ hipError_t launch_hilo_rows(const f16_t* hi, const uint16_t* lo, int row_stride,
 // CLIP text embeddings (tok + pos) -> x fp32 (or x16 fp16: exactly one non-null), then LN1 of layer 0
 // -> xb fp16
 hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
-                                  const float* b, float eps, float* x, f16_t* x16, f16_t* xb, int B, int L, int H,
-                                  hipStream_t s);
+                                  const float* b, float eps, float* x, f16_t* x16, f16_t* xb, float2* st, int B, int L,
+                                  int H, hipStream_t s);
+// (lazy LN, st != null: st[row] = (mean, M2) of the stored stream instead of xb)
 // CLIP patch im2col with normalisation: img uint8 [B,224,224,3] -> A fp16 [B*49][3072]
 hipError_t launch_clip_im2col(const uint8_t* img, f16_t* A, int B, hipStream_t s);
 // CLIP vision: x = preLN(cat(cls, patches) + pos) -> x fp32 [B*50][768] (or x16 fp16: exactly one
 // non-null), xb = LN1(x) fp16
 hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
                                        const float* pre_g, const float* pre_b, const float* ln1_g,
-                                       const float* ln1_b, float eps, float* x, f16_t* x16, f16_t* xb, int B,
-                                       hipStream_t s);
+                                       const float* ln1_b, float eps, float* x, f16_t* x16, f16_t* xb, float2* st,
+                                       int B, hipStream_t s);
+
 // EOS index per row (first == eos_id, or argmax when eos_id == 2)
 hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int eos_id, hipStream_t s);
 // gather rows: out fp16 [B][C] = LN(x[row_index(b)]) where row_index = b*L + (idx ? idx[b] : 0)

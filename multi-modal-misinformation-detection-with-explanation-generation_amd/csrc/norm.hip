@@ -87,6 +87,23 @@ MMF_DEV void store_x(float4 (&v)[NV], XT* x, int lane) {
   }
 }
 
+// (mean, M2) of a row held by one wave -- the single lazy-LN partial (P = 1, tn = C) of a row
+// whose LayerNorm the next GEMM folds (gemm.hip)
+template <int NV>
+MMF_DEV float2 row_partial(const float4 (&v)[NV], int C) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+    q += (a * a + b * b) + (c * c + d * d);
+  }
+  return make_float2(mean, wave_sum(q));
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx, const float* add, int ldadd,
                                                         const float* g, const float* b, float eps, float* y32,
@@ -225,8 +242,8 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
     load_row<NV>(v, word + (size_t)s_ids[t] * C, lane);
     add_row<NV>(v, type0, lane);
     add_row<NV>(v, pos + (size_t)s_pos[t] * C, lane);
-    ln_row<NV>(v, g, b, eps, C, lane);
     const size_t r = (size_t)bi * L + t;
+    ln_row<NV>(v, g, b, eps, C, lane);
     store_row_hilo<NV>(v, xb + r * C, xlo ? xlo + r * C : nullptr, lane);
   }
 }
@@ -235,7 +252,7 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
 template <int NV, typename XT>
 __global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids, const float* tok, const float* pos,
                                                               const float* g, const float* b, float eps, XT* x,
-                                                              f16_t* xb, int rows, int L) {
+                                                              f16_t* xb, float2* st, int rows, int L) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   constexpr int C = NV * 256;
@@ -244,6 +261,11 @@ __global__ __launch_bounds__(256) void clip_text_embed_kernel(const int32_t* ids
   load_row<NV>(v, tok + (size_t)ids[row] * C, lane);
   add_row<NV>(v, pos + (size_t)t * C, lane);
   store_x<NV>(v, x + (size_t)row * C, lane);  // rounds v to XT: LN1 sees the stored stream
+  if (st) {  // lazy LN: statistics of the stored stream (layer 0's QKV folds LN1)
+    const float2 pm = row_partial<NV>(v, C);
+    if (lane == 0) st[row] = pm;
+    return;
+  }
   ln_row<NV>(v, g, b, eps, C, lane);
   store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
 }
@@ -285,7 +307,7 @@ __global__ __launch_bounds__(256) void clip_vision_assemble_kernel(const float* 
                                                                    const float* pos, const float* pg,
                                                                    const float* pb, const float* g1,
                                                                    const float* b1, float eps, XT* x,
-                                                                   f16_t* xb, int rows) {
+                                                                   f16_t* xb, float2* st, int rows) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   constexpr int NV = 3, C = 768;
@@ -296,6 +318,11 @@ __global__ __launch_bounds__(256) void clip_vision_assemble_kernel(const float* 
   add_row<NV>(v, pos + (size_t)t * C, lane);
   ln_row<NV>(v, pg, pb, eps, C, lane);
   store_x<NV>(v, x + (size_t)row * C, lane);  // rounds v to XT: LN1 sees the stored stream
+  if (st) {
+    const float2 pm = row_partial<NV>(v, C);
+    if (lane == 0) st[row] = pm;
+    return;
+  }
   ln_row<NV>(v, g1, b1, eps, C, lane);
   store_row<NV>(v, nullptr, xb + (size_t)row * C, lane);
 }
@@ -419,16 +446,16 @@ hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const flo
 }
 
 hipError_t launch_clip_text_embed(const int32_t* ids, const float* tok, const float* pos, const float* g,
-                                  const float* b, float eps, float* x, f16_t* x16, f16_t* xb, int B, int L, int H,
-                                  hipStream_t s) {
+                                  const float* b, float eps, float* x, f16_t* x16, f16_t* xb, float2* st, int B, int L,
+                                  int H, hipStream_t s) {
   if (H != 512 || !x == !x16) return hipErrorInvalidValue;
   const int rows = B * L;
   if (x)
     hipLaunchKernelGGL((clip_text_embed_kernel<2, float>), dim3((rows + 3) / 4), dim3(256), 0, s, ids, tok, pos, g, b,
-                       eps, x, xb, rows, L);
+                       eps, x, xb, st, rows, L);
   else
     hipLaunchKernelGGL((clip_text_embed_kernel<2, f16_t>), dim3((rows + 3) / 4), dim3(256), 0, s, ids, tok, pos, g, b,
-                       eps, x16, xb, rows, L);
+                       eps, x16, xb, st, rows, L);
   return hipGetLastError();
 }
 
@@ -441,16 +468,16 @@ hipError_t launch_clip_im2col(const uint8_t* img, f16_t* A, int B, hipStream_t s
 
 hipError_t launch_clip_vision_assemble(const float* patches, const float* cls, const float* pos,
                                        const float* pre_g, const float* pre_b, const float* ln1_g,
-                                       const float* ln1_b, float eps, float* x, f16_t* x16, f16_t* xb, int B,
-                                       hipStream_t s) {
+                                       const float* ln1_b, float eps, float* x, f16_t* x16, f16_t* xb, float2* st,
+                                       int B, hipStream_t s) {
   if (!x == !x16) return hipErrorInvalidValue;
   const int rows = B * 50;
   if (x)
     hipLaunchKernelGGL(clip_vision_assemble_kernel<float>, dim3((rows + 3) / 4), dim3(256), 0, s, patches, cls, pos,
-                       pre_g, pre_b, ln1_g, ln1_b, eps, x, xb, rows);
+                       pre_g, pre_b, ln1_g, ln1_b, eps, x, xb, st, rows);
   else
     hipLaunchKernelGGL(clip_vision_assemble_kernel<f16_t>, dim3((rows + 3) / 4), dim3(256), 0, s, patches, cls, pos,
-                       pre_g, pre_b, ln1_g, ln1_b, eps, x16, xb, rows);
+                       pre_g, pre_b, ln1_g, ln1_b, eps, x16, xb, st, rows);
   return hipGetLastError();
 }
 

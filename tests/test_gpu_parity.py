@@ -72,6 +72,34 @@ def test_clip_embeddings(engine, golden, golden_inputs):
     np.testing.assert_allclose((ie * te).sum(1), golden["clip_similarity"], atol=TOL)
 
 
+@pytest.mark.parametrize("B", [3, 37])
+def test_lazy_layernorm_clip_matches_materialised(engine, clip_sd, golden_inputs, B):
+    """CLIP towers with the LayerNorms folded into the GEMM epilogues (option lazy_ln, default)
+    against the materialised add+LN path and the fp32 oracle, at a few rows (B = 3: M = 150 / 231,
+    below the persistent GEMM's 256-row tile) and at ragged M (B = 37: 1850 / 2849 rows)."""
+    import mmf_amd.synthetic as syn
+    from oracle import models as M
+    cid, cm = syn.clip_ids(B, 77, 21)
+    imgs = syn.images(B, 21)
+    out = {}
+    try:
+        for v in (0, 1):
+            engine.set_option("lazy_ln", v)
+            out[v] = (engine.clip_image(imgs).cpu().numpy(), engine.clip_text(cid, cm).cpu().numpy())
+    finally:
+        engine.set_option("lazy_ln", 1)
+    csd = M.to_torch(clip_sd)
+    with torch.no_grad():
+        ie = M.l2n(M.clip_image_features(csd, M.clip_preprocess(torch.as_tensor(imgs)))).numpy()
+        te = M.l2n(M.clip_text_features(csd, torch.as_tensor(cid), torch.as_tensor(cm), golden_inputs["eos"])).numpy()
+    for v in (0, 1):
+        assert (out[v][0] * ie).sum(1).min() > 1 - 1e-4, v
+        assert (out[v][1] * te).sum(1).min() > 1 - 1e-4, v
+        np.testing.assert_allclose((out[v][0] * out[v][1]).sum(1), (ie * te).sum(1), atol=TOL)
+    assert (out[0][0] * out[1][0]).sum(1).min() > 1 - 1e-5
+    assert (out[0][1] * out[1][1]).sum(1).min() > 1 - 1e-5
+
+
 def test_analyze_batch_vs_golden(engine, golden, golden_inputs):
     out = engine.analyze_batch(golden["rob_ids"], golden["rob_mask"], golden["clip_ids"], golden["clip_mask"],
                                golden_inputs["imgs"])
