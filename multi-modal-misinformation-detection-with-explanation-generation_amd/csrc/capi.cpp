@@ -256,11 +256,11 @@ int free_group(mmf_handle* h, int group) {
 }
 
 // ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
-// GEMM launches are profiled per (tile instantiation, activation) -- one kernel symbol each, so
-// the numbers line up with a rocprofv3 kernel trace of the same run.
-constexpr int kGemmActs = 5;
+// GEMM launches are profiled per (tile instantiation, epilogue, activation) -- one kernel symbol
+// each, so the numbers line up with a rocprofv3 kernel trace of the same run.
+constexpr int kGemmActs = 5, kGemmEpis = 3;
 enum ProfKind {
-  PK_GEMM0 = 0, PK_GEMM_LAST = 13 * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
+  PK_GEMM0 = 0, PK_GEMM_LAST = 13 * kGemmEpis * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
   PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_PW32, PK_COUNT
 };
 const char* prof_kind_name(int k) {
@@ -269,8 +269,11 @@ const char* prof_kind_name(int k) {
                                                   "pw32"};
   static char gemm_names[PK_GEMM_LAST + 1][64];
   if (k >= 0 && k <= PK_GEMM_LAST) {
-    if (!gemm_names[k][0])
-      snprintf(gemm_names[k], sizeof(gemm_names[k]), "%s act=%d", gemm_config_name(k / kGemmActs), k % kGemmActs);
+    if (!gemm_names[k][0]) {
+      const int epi = (k / kGemmActs) % kGemmEpis;
+      snprintf(gemm_names[k], sizeof(gemm_names[k]), epi ? "%s act=%d epi=%d" : "%s act=%d",
+               gemm_config_name(k / (kGemmActs * kGemmEpis)), k % kGemmActs, epi);
+    }
     return gemm_names[k];
   }
   return (k >= PK_ATTN && k < PK_COUNT) ? names[k - PK_ATTN] : "?";
@@ -614,7 +617,8 @@ int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   apply_options(h->opt, &g);
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
-  ProfScope ps(h, s, gemm_config(g) * kGemmActs + g.act, 2.0 * M * N * K, 2.0 * (M * K + N * K) + M * N * out_b);
+  ProfScope ps(h, s, (gemm_config(g) * kGemmEpis + g.epi) * kGemmActs + g.act, 2.0 * M * N * K,
+               2.0 * (M * K + N * K) + M * N * out_b);
   HIPCHK(launch_gemm(g, s));
   return 0;
 }

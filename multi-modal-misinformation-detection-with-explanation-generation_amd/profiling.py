@@ -20,7 +20,7 @@ from .hip import check
 PROFILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0
-NK = 128
+NK = 256
 
 
 def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:
@@ -54,14 +54,15 @@ def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:
 
 def kind_symbol(kind: str) -> str:
     """Event-profile kind -> kernel symbol as rocprofv3 prints it (GEMM kinds only)."""
-    m = re.match(r"gemm_(glds|glds_pipe2|f16)<([\d,]+)> act=(\d)", kind)
+    m = re.match(r"gemm_(glds|glds_pipe2|f16)<([\d,]+)> act=(\d)(?: epi=(\d))?", kind)
     if not m:
         return kind
     dims = m.group(2).split(",")
+    epi = m.group(4) or "0"
     if m.group(1) == "glds":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3)])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi])}>"
     if m.group(1) == "glds_pipe2":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true'])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi])}>"
     return f"gemm_f16_kernel<{', '.join(dims)}>"
 
 
