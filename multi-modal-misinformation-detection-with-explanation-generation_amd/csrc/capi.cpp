@@ -129,6 +129,7 @@ struct Options {
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
   int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
+  int dw_v2 = 0;        // depthwise phases with one channel group per wave, weights in SGPRs (effnet.hip)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -138,6 +139,7 @@ const OptName kOptNames[] = {
     {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
+    {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -1005,7 +1007,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
       // stem output recomputed per 18x18 halo tile: 1.27x the stem MACs, image patch read once
       ProfScope ps(h, s, PK_DW, 2.0 * B * 112 * 112 * 32 * (9 + 27 * 1.27),
                    (double)B * (224 * 224 * 3 * 1.34 + 112 * 112 * 32 * 2));
-      HIPCHK(launch_effnet_stem_dw(img, xf32, h->e_stem_w, h->e_stem_b, b.wd, b.bd, w.e_dw, w.e_pool, B, &nch, s));
+      HIPCHK(launch_effnet_stem_dw(img, xf32, h->e_stem_w, h->e_stem_b, b.wd, h->opt.dw_v2 ? b.wd_t : nullptr, b.bd, w.e_dw, w.e_pool, B, &nch, s));
     } else if (fuse) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k + 2.0 * B * H * W * b.cin * b.cexp,
                    (double)B * 2 * ((double)H * W * b.cin * (b.cexp / 48) + (double)Ho * Wo * b.cexp));

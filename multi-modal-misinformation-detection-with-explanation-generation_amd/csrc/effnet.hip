@@ -433,16 +433,25 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
 // grid (49, 1, B); block 256
 constexpr int SD_T = 16, SD_IT = 18, SD_PR = 2 * SD_IT + 1, SD_PW = SD_PR * 3;
 
-template <bool F32>
+//
+// V2 (option dw_v2, default): each wave owns one 8-channel group of the 32 -- wave-uniform, so the
+// depthwise weights (tap-major copy) and bias arrive by scalar loads into SGPRs and no LDS cycle is
+// spent on weights; the stem tile is stored channel-group-planar [4][18][SD2_ITP][8] with a row
+// pitch of 21 pixels, so the 16 lanes of every ds_read_b128 lane group hit 16 distinct bank quads
+// (lane = (row, run of 4 outputs): 16 rows x 4 runs = the wave); the SE pool partial of the group
+// is a fixed-order butterfly over the wave's lanes (no LDS slots, no second barrier).
+constexpr int SD2_ITP = 21;
+
+template <bool F32, bool V2>
 __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const float* __restrict__ ws,
                                                       const float* __restrict__ bs, const float* __restrict__ wd,
                                                       const float* __restrict__ bd, f16_t* __restrict__ out,
                                                       float* __restrict__ pool_part) {
   constexpr int CW = 32, NPIX = SD_IT * SD_IT, NMT = (NPIX + 15) / 16;
   __shared__ __attribute__((aligned(16))) float patch[(SD_PR * SD_PW + 255) / 256 * 256];  // image patch, HWC
-  __shared__ __attribute__((aligned(16))) f16_t tile[NPIX * CW];      // stem output tile (+halo)
-  __shared__ __attribute__((aligned(16))) float sw[9 * CW];
-  __shared__ __attribute__((aligned(16))) float sb[CW];
+  __shared__ __attribute__((aligned(16))) f16_t tile[V2 ? 4 * SD_IT * SD2_ITP * 8 : NPIX * CW];  // stem tile (+halo)
+  __shared__ __attribute__((aligned(16))) float sw[V2 ? 4 : 9 * CW];  // (V2: 40,320 B in all -> 4 WGs/CU)
+  __shared__ __attribute__((aligned(16))) float sb[V2 ? 4 : CW];
   float* red = patch;  // pool-partial slots [64][32]: the patch is dead once the stem tile is built
   static_assert((SD_PR * SD_PW + 255) / 256 * 256 >= (256 / (CW / 8)) * CW, "red fits in the patch");
   const uint8_t* img = (const uint8_t*)src;
@@ -454,9 +463,10 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
   const int oy0 = ty0 * SD_T, ox0 = tx0 * SD_T;
   const int py0 = 2 * oy0 - 3, px0 = 2 * ox0 - 3;  // image coords of patch (0, 0)
 
-  const float wd0 = wd[(tid % CW) * 9 + tid / CW];
-  const float wd1 = tid + 256 < 9 * CW ? wd[((tid + 256) % CW) * 9 + (tid + 256) / CW] : 0.f;
-  const float bd0 = tid < CW ? bd[tid] : 0.f;
+  // (V1: depthwise weights [C][9] transposed into LDS; V2 reads `wd` as the tap-major [9][C] copy)
+  const float wd0 = V2 ? 0.f : wd[(tid % CW) * 9 + tid / CW];
+  const float wd1 = (!V2 && tid + 256 < 9 * CW) ? wd[((tid + 256) % CW) * 9 + (tid + 256) / CW] : 0.f;
+  const float bd0 = (!V2 && tid < CW) ? bd[tid] : 0.f;
   // stem weight fragments (A operand: row = output channel nt*16 + fr, k = fg*8 + e), split hi/lo
   int offk[8];
   f16x8 whi[2], wlo[2];
@@ -515,9 +525,11 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
     }
     patch[tid + i * 256] = c < 0 ? 0.f : v;
   }
-  sw[tid] = wd0;
-  if (tid + 256 < 9 * CW) sw[tid + 256] = wd1;
-  if (tid < CW) sb[tid] = bd0;
+  if constexpr (!V2) {
+    sw[tid] = wd0;
+    if (tid + 256 < 9 * CW) sw[tid + 256] = wd1;
+    if (tid < CW) sb[tid] = bd0;
+  }
   __syncthreads();
 
   // ---- stem: 16 tile pixels per MFMA column block ----
@@ -547,13 +559,65 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
       acc = mfma16x16x32(whi[nt], xhi, acc);
       float e4[4] = {acc[0] + sbias[nt].x, acc[1] + sbias[nt].y, acc[2] + sbias[nt].z, acc[3] + sbias[nt].w};
       act4<ACT_SILU>(e4);
+      const int ch = nt * 16 + fg * 4;
+      f16_t* dst = V2 ? tile + (((ch >> 3) * SD_IT + sy) * SD2_ITP + sx) * 8 + (ch & 7) : tile + p * CW + ch;
       if (p < NPIX)
-        *reinterpret_cast<uint2*>(tile + p * CW + nt * 16 + fg * 4) =
-            inimg ? make_uint2(pack2h(e4[0], e4[1]), pack2h(e4[2], e4[3])) : make_uint2(0, 0);
+        *reinterpret_cast<uint2*>(dst) = inimg ? make_uint2(pack2h(e4[0], e4[1]), pack2h(e4[2], e4[3])) : make_uint2(0, 0);
     }
   }
   __syncthreads();
-  dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW);
+  if constexpr (!V2) {
+    dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW);
+  } else {
+    const int g = __builtin_amdgcn_readfirstlane(wave);  // this wave's channel group
+    const int oy = lane >> 2, ox = (lane & 3) * 4;       // a run of 4 outputs of one tile row
+    float wk[9][8], acc[4][8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wk[t][j] = wd[t * CW + g * 8 + j];
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[o][j] = bd[g * 8 + j];
+    const f16_t* tp = tile + ((g * SD_IT + oy) * SD2_ITP + ox) * 8;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+      for (int col = 0; col < 6; ++col) {
+        const uint4 v = *reinterpret_cast<const uint4*>(tp + (ky * SD2_ITP + col) * 8);
+        const float f[8] = {lo_h(v.x), hi_h(v.x), lo_h(v.y), hi_h(v.y), lo_h(v.z), hi_h(v.z), lo_h(v.w), hi_h(v.w)};
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const int kx = col - o;
+          if (kx >= 0 && kx < 3) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[o][j] = fmaf(f[j], wk[ky * 3 + kx][j], acc[o][j]);
+          }
+        }
+      }
+    }
+    float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    f16_t* ob = out + (size_t)bi * 112 * 112 * CW;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      act4<ACT_SILU>(acc[o]);
+      act4<ACT_SILU>(acc[o] + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ps[j] += acc[o][j];
+      *reinterpret_cast<uint4*>(at_bytes(ob, (uint32_t)(((oy0 + oy) * 112 + ox0 + ox + o) * CW + g * 8) * 2u)) =
+          make_uint4(pack2h(acc[o][0], acc[o][1]), pack2h(acc[o][2], acc[o][3]), pack2h(acc[o][4], acc[o][5]),
+                     pack2h(acc[o][6], acc[o][7]));
+    }
+    // fixed-order butterfly: every lane ends with the wave's sum (deterministic, no atomics)
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ps[j] += __shfl_xor(ps[j], m, 64);
+    if (lane < 2)
+      *reinterpret_cast<float4*>(pool_part + ((size_t)bi * 49 + blockIdx.x) * CW + g * 8 + lane * 4) =
+          lane ? make_float4(ps[4], ps[5], ps[6], ps[7]) : make_float4(ps[0], ps[1], ps[2], ps[3]);
+  }
 }
 
 // Squeeze-excitation, one 1024-thread block per image.  The three phases are each a few dependent
@@ -702,12 +766,18 @@ hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* b
 }
 
 hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
-                                 const float* wd, const float* bd, f16_t* out, float* pool_part, int B,
+                                 const float* wd, const float* wd_t, const float* bd, f16_t* out, float* pool_part, int B,
                                  int* nchunks_out, hipStream_t s) {
   *nchunks_out = 49;  // = dwconv_nchunks(112, 112, 32, 1): the SE reads the same partial layout
   const dim3 grid(49, 1, B), blk(256);
-  if (xf32) hipLaunchKernelGGL(stem_dw_kernel<true>, grid, blk, 0, s, (const void*)xf32, ws, bs, wd, bd, out, pool_part);
-  else hipLaunchKernelGGL(stem_dw_kernel<false>, grid, blk, 0, s, (const void*)img, ws, bs, wd, bd, out, pool_part);
+  // wd_t (tap-major [9][32] copy) selects the V2 depthwise phase
+  if (wd_t) {
+    if (xf32) hipLaunchKernelGGL((stem_dw_kernel<true, true>), grid, blk, 0, s, (const void*)xf32, ws, bs, wd_t, bd, out, pool_part);
+    else hipLaunchKernelGGL((stem_dw_kernel<false, true>), grid, blk, 0, s, (const void*)img, ws, bs, wd_t, bd, out, pool_part);
+  } else {
+    if (xf32) hipLaunchKernelGGL((stem_dw_kernel<true, false>), grid, blk, 0, s, (const void*)xf32, ws, bs, wd, bd, out, pool_part);
+    else hipLaunchKernelGGL((stem_dw_kernel<false, false>), grid, blk, 0, s, (const void*)img, ws, bs, wd, bd, out, pool_part);
+  }
   return hipGetLastError();
 }
 

@@ -385,26 +385,33 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
               pv[pi] = pi < P ? v : make_float2(0.f, 0.f);
               nv[pi] = pi < P ? (float)min(C - pi * tnin, tnin) : 0.f;
             }
+            // explicit fmaf, the same operation sequence as the rolled loop below: a zero slot adds
+            // an exact 0, so both tile widths give bit-identical statistics (the consumer's tile
+            // width depends on M, and rows must not change with the batch they run in)
             float s1 = 0.f;
 #pragma unroll
-            for (int pi = 0; pi < kLnPMax; ++pi) s1 += nv[pi] * pv[pi].x;
+            for (int pi = 0; pi < kLnPMax; ++pi) s1 = fmaf(nv[pi], pv[pi].x, s1);
             const float mean = s1 / (float)C;
             float s2 = 0.f;
 #pragma unroll
-            for (int pi = 0; pi < kLnPMax; ++pi) s2 += pv[pi].y + nv[pi] * (pv[pi].x - mean) * (pv[pi].x - mean);
+            for (int pi = 0; pi < kLnPMax; ++pi) {
+              const float d = pv[pi].x - mean;
+              s2 += fmaf(nv[pi] * d, d, pv[pi].y);
+            }
             lds_stat[tid] = make_float2(mean, rsqrtf(s2 / (float)C + g.ln_eps));
           } else if (tid < BM) {
             const int P = g.ln_in_P, tnin = g.ln_in_tn, C = EPI == 1 ? g.K : N;
             const float2* pr = lds_rows + tid * P;
             float s1 = 0.f;
 #pragma unroll 1
-            for (int pi = 0; pi < P; ++pi) s1 += (float)min(C - pi * tnin, tnin) * pr[pi].x;
+            for (int pi = 0; pi < P; ++pi) s1 = fmaf((float)min(C - pi * tnin, tnin), pr[pi].x, s1);
             const float mean = s1 / (float)C;
             float s2 = 0.f;
 #pragma unroll 1
             for (int pi = 0; pi < P; ++pi) {
               const float2 v = pr[pi];
-              s2 += v.y + (float)min(C - pi * tnin, tnin) * (v.x - mean) * (v.x - mean);
+              const float d = v.x - mean;
+              s2 += fmaf((float)min(C - pi * tnin, tnin) * d, d, v.y);
             }
             lds_stat[tid] = make_float2(mean, rsqrtf(s2 / (float)C + g.ln_eps));
           }

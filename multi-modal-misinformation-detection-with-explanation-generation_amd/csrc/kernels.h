@@ -126,9 +126,10 @@ hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* b
 hipError_t launch_effnet_stem_f32(const float* x_nchw, const float* w, const float* bias, f16_t* out, int B,
                                   hipStream_t s);
 // stem fused into the stage-1 depthwise conv (3x3 s1, 32 channels at 112^2) + its SE pool partials;
-// exactly one of img (uint8 HWC) / xf32 (normalised fp32 NCHW) is non-null
+// exactly one of img (uint8 HWC) / xf32 (normalised fp32 NCHW) is non-null; wd_t (the tap-major
+// [9][32] weight copy) non-null selects the wave-per-channel-group depthwise phase (V2)
 hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
-                                 const float* wd, const float* bd, f16_t* out, float* pool_part, int B,
+                                 const float* wd, const float* wd_t, const float* bd, f16_t* out, float* pool_part, int B,
                                  int* nchunks_out, hipStream_t s);
 // ct = 0 forces the runtime-geometry kernels (A/B option "dw_ct"; the default uses the
 // compile-time tile geometries)

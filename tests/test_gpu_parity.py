@@ -199,6 +199,23 @@ def test_compile_time_dwconv_matches_runtime_geometry(engine):
     np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
 
 
+def test_dw_v2_matches_v1(engine):
+    """Depthwise phases with one channel group per wave and SGPR weights (option dw_v2) vs
+    the thread-per-(channel group, run) phases (dw_v2 = 0, default).  The conv taps accumulate in the same
+    order and round to fp16 the same way, so the stage outputs are bit-identical; only the SE pool
+    partial sums are grouped differently (cross-lane butterfly vs LDS slots), a last-bit effect that
+    can flip later fp16 roundings -- compared at the north-star tolerance on deepfake_score."""
+    import mmf_amd.synthetic as syn
+    imgs = syn.images(64, 29)
+    engine.set_option("dw_v2", 0)
+    lg0, s0 = engine.effnet_forward(imgs)
+    engine.set_option("dw_v2", 1)
+    lg1, s1 = engine.effnet_forward(imgs)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
+    np.testing.assert_allclose(lg1.cpu().numpy(), lg0.cpu().numpy(), atol=2e-2)
+
+
 def test_long_text_up_to_512(det_sd, clip_sd):
     """RoBERTa inputs past 128 tokens (the reference truncates at 512, misinfo_forensics.py:327-333):
     each padded row must score like the oracle's unpadded single-text analyze_text."""
