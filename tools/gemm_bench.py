@@ -89,6 +89,10 @@ def main():
     ap.add_argument("--group-m", default="", help="extra timed pass per config per gemm_group_m value (comma list)")
     ap.add_argument("--opt", default="gemm_group_m", help="process option swept by --vals (default gemm_group_m)")
     ap.add_argument("--vals", default="", help="extra timed pass per config per value of --opt (comma list)")
+    ap.add_argument("--no-store", action="store_true",
+                    help="also time each config with no output tensor (every store dropped by the buffer "
+                         "descriptor): the epilogue's write cost is the difference")
+    ap.add_argument("--shapes", default="", help="comma list of shape names to time (default all)")
     a = ap.parse_args()
     lib = hip.load()
     dev = torch.device("cuda")
@@ -96,6 +100,8 @@ def main():
         effnet(a, lib, dev)
         return
     shapes = ROUND if a.round else SHAPES
+    if a.shapes:
+        shapes = [x for x in shapes if x[0] in a.shapes.split(",")]
     if a.kscale:
         shapes = [(f"{n}_k{m}", M, N, K * int(m), act, out) for n, M, N, K, act, out in shapes
                   for m in a.kscale.split(",")]
@@ -106,9 +112,10 @@ def main():
         c32 = torch.empty(M, N, device=dev) if "32" in out else None
         c16 = torch.empty(M, N, device=dev, dtype=torch.float16) if "16" in out else None
 
-        def call():
-            hip.check(lib.mmf_gemm_f16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None, hip.ptr(c32),
-                                        hip.ptr(c16), N, M, N, K, act, hip.stream_ptr()))
+        def call(store=True):
+            hip.check(lib.mmf_gemm_f16(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), None,
+                                        hip.ptr(c32) if store else None, hip.ptr(c16) if store else None, N, M, N,
+                                        K, act, hip.stream_ptr()))
         row = {"shape": name, "M": M, "N": N, "K": K}
         opt = "gemm_group_m" if a.group_m else a.opt
         vals = a.group_m or a.vals
@@ -118,6 +125,9 @@ def main():
                 force(cfg)
                 us = timed_us(call, a.iters)
                 row[(f"{opt}={v}:" if v else "") + cfg] = round(2.0 * M * N * K / (us / 1e6) / 1e12, 1)
+                if a.no_store:
+                    us0 = timed_us(lambda: call(False), a.iters)
+                    row[(f"{opt}={v}:" if v else "") + cfg + ":us/us_nostore"] = f"{us:.1f}/{us0:.1f}"
         hip.set_process_option(opt, 0)
         force("auto")
         print(json.dumps(row), flush=True)
