@@ -148,6 +148,21 @@ MMF_DEV void dw_compute(const f16_t* tile, const float* sw, const float* sb, flo
   }
 }
 
+// acc + (float)half * w in one v_fma_mix_f32 (the half selected from a packed pair, converted exactly
+// in the multiplier: the same single-rounding fmaf as converting first, so outputs are bit-identical),
+// so the depthwise taps need no separate f16 -> f32 conversions.  Build with -DMMF_DW_MIX=0 for the
+// convert-once + packed-FMA form (measured: depthwise / fused-front kernels 1-11 % slower).
+#ifndef MMF_DW_MIX
+#define MMF_DW_MIX 1
+#endif
+template <bool HI>
+MMF_DEV float fma_mix(uint32_t h2, float w, float acc) {
+  float d;
+  if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(h2), "v"(w), "v"(acc));
+  else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(h2), "v"(w), "v"(acc));
+  return d;
+}
+
 // Compile-time-geometry variant of dw_compute: T x T output tile, CW channels, and each work item
 // (channel group g, output row oy, run of R consecutive outputs) walks the input row segment of a
 // kernel row once -- ((R-1)S + K) LDS reads / fp16 unpacks per kernel row instead of R*K -- and
@@ -188,14 +203,29 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
 #pragma unroll
         for (int col = 0; col < IC; ++col) {
           const uint4 v = *reinterpret_cast<const uint4*>(row + col * NG * 8);
-          const float f[8] = {lo_h(v.x), hi_h(v.x), lo_h(v.y), hi_h(v.y),
-                              lo_h(v.z), hi_h(v.z), lo_h(v.w), hi_h(v.w)};
+          if constexpr (MMF_DW_MIX) {
+            const uint32_t hv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int o = 0; o < R; ++o) {
-            const int kx = col - o * S;
-            if (kx >= 0 && kx < K) {
+            for (int o = 0; o < R; ++o) {
+              const int kx = col - o * S;
+              if (kx >= 0 && kx < K) {
 #pragma unroll
-              for (int j = 0; j < 8; ++j) acc[o][j] = fmaf(f[j], wk[kx][j], acc[o][j]);
+                for (int q = 0; q < 4; ++q) {
+                  acc[o][2 * q] = fma_mix<false>(hv[q], wk[kx][2 * q], acc[o][2 * q]);
+                  acc[o][2 * q + 1] = fma_mix<true>(hv[q], wk[kx][2 * q + 1], acc[o][2 * q + 1]);
+                }
+              }
+            }
+          } else {
+            const float f[8] = {lo_h(v.x), hi_h(v.x), lo_h(v.y), hi_h(v.y),
+                                lo_h(v.z), hi_h(v.z), lo_h(v.w), hi_h(v.w)};
+#pragma unroll
+            for (int o = 0; o < R; ++o) {
+              const int kx = col - o * S;
+              if (kx >= 0 && kx < K) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[o][j] = fmaf(f[j], wk[kx][j], acc[o][j]);
+              }
             }
           }
         }
