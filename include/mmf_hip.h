@@ -160,11 +160,13 @@ int mmf_profile_end(mmf_handle* h, int max_kinds, int* counts, double* ms, doubl
 const char* mmf_profile_kind_name(int kind);
 
 /* Run-time options (defaults read once per process from MMF_* environment variables):
- * "concurrent" (tower streams), "fuse_stem", "fuse_expand", "dw_ct", "gemm_splitk", "gemm_config",
- * "gemm_group_m" (A/B switches) and "effnet_fp32" (EfficientNet tower with fp32 activations,
- * fp32-FMA 1x1 convs and precise SiLU: the mode for checkpoints whose logits amplify fp16 storage
- * rounding past 1e-3; ~4x the tower time).  h = NULL reads/changes the process defaults used by
- * the handle-less ops below and by handles created afterwards. */
+ * "concurrent" (tower streams), "fuse_stem", "fuse_expand", "dw_ct", "dw_v2", "gemm_splitk",
+ * "gemm_config", "gemm_group_m", "gemm_prio", "text_hilo", "clip_res16", "lazy_ln" (A/B switches
+ * of layouts and fusions; the defaults are the measured best) and "effnet_fp32"
+ * (EfficientNet tower with fp32 activations, fp32-FMA 1x1 convs and precise SiLU: the mode for
+ * checkpoints whose logits amplify fp16 storage rounding past 1e-3; ~4x the tower time).  Every
+ * option keeps a row's results independent of the batch it runs in.  h = NULL reads/changes the
+ * process defaults used by the handle-less ops below and by handles created afterwards. */
 int mmf_set_option(mmf_handle* h, const char* name, int value);
 int mmf_get_option(mmf_handle* h, const char* name, int* value);
 /* Device bytes currently owned by the handle (weights, workspaces, vault). */
