@@ -164,9 +164,10 @@ const char* mmf_profile_kind_name(int kind);
  * "gemm_config", "gemm_group_m", "gemm_prio", "text_hilo", "clip_res16", "lazy_ln" (A/B switches
  * of layouts and fusions; the defaults are the measured best) and "effnet_fp32"
  * (EfficientNet tower with fp32 activations, fp32-FMA 1x1 convs and precise SiLU: the mode for
- * checkpoints whose logits amplify fp16 storage rounding past 1e-3; ~4x the tower time).  Every
- * option keeps a row's results independent of the batch it runs in.  h = NULL reads/changes the
- * process defaults used by the handle-less ops below and by handles created afterwards. */
+ * checkpoints whose logits amplify fp16 storage rounding past 1e-3; ~4x the tower time).  With the
+ * defaults a row's results do not depend on the batch it runs in (tests/test_gpu_parity.py).
+ * h = NULL reads/changes the process defaults used by the handle-less ops below and by handles
+ * created afterwards. */
 int mmf_set_option(mmf_handle* h, const char* name, int value);
 int mmf_get_option(mmf_handle* h, const char* name, int* value);
 /* Device bytes currently owned by the handle (weights, workspaces, vault). */
