@@ -132,11 +132,13 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kOOB = 0x80000000u;  // an offset past every buffer the launchers allow
-// Cache policy of the raw-buffer epilogue stores: sc1 (bit 4).  Interleaved A/B on MI355X
-// (tools/ab_lib.py): 2-13 % faster encoder GEMMs at K <= 768, where every CU's epilogue writes
-// its tile in the same burst; neutral for the streaming 1x1 convolutions.
+// Cache policy of the raw-buffer epilogue stores: plain (0: the written lines stay in the XCD's L2
+// and the Infinity Cache for the next kernel, which reads them).  Write-through sc1 (16) made the
+// isolated encoder GEMMs 2-13 % faster (tools/ab_lib.py: nothing re-reads their outputs) but the
+// whole analyze step 2.7 % slower (tools/lib_step_ab.sh: 14.46 -> 14.08 ms with plain stores, three
+// interleaved rounds; sc0 ties with plain).
 #ifndef MMF_STORE_AUX
-#define MMF_STORE_AUX 16
+#define MMF_STORE_AUX 0
 #endif
 MMF_DEV rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? (int)bytes : 0, 0x00020000);
