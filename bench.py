@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="time budget of CPU mode (i)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event-timed pass")
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs[1..3] lines")
+    ap.add_argument("--no-per-sample", action="store_true", help="skip the B=1 / per-row API lines")
     return ap.parse_args()
 
 
@@ -182,6 +183,67 @@ def config_lines(eng, t, steps, warmup, det):
     return out
 
 
+def per_sample_lines(n_lat: int = 200, n_rows: int = 64, warmup: int = 10):
+    """The reference's per-sample callers through the drop-in API:
+    * `analyze(text, image)` one pair per call -- the dashboard path (forensics_dashboard.py:180-185):
+      p50 / p99 / mean latency from the call to the returned dict, B = 1;
+    * FusionTrainingDataset.__getitem__'s extraction (train_fusion_judge.py:72-86): analyze_text,
+      analyze_image, analyze_consistency, search_vault (no caption) per row -> rows/s.
+    Inputs: 224x224 PIL images in memory (decode excluded), L = 128 texts, 77-token captions through an
+    id-table tokenizer (tokenisation is a dict lookup), 2170-row vault with titles."""
+    from PIL import Image
+    import mmf_amd.synthetic as syn
+    from mmf_amd.api import MisinfoForensics
+    n = max(n_lat, n_rows) + warmup
+    seed = benchrun.input_seed(0) + 200
+    texts, rob, clp = syn.text_tables(n, seed)
+    pils = [Image.fromarray(a) for a in syn.images(n, seed)]
+    tid, tm = syn.clip_ids(2170, 77, 99, np.random.default_rng(5).integers(3, 78, 2170).tolist())
+    meta = []
+    for j in range(2170):
+        clp.table[f"title {j}"] = tid[j, :int(tm[j].sum())].tolist()
+        meta.append({"title": f"title {j}", "url": "N/A", "date": "N/A"})
+    mf = MisinfoForensics(fusion_weights="", faiss_index_path="", synthetic_seed=0, roberta_tokenizer=rob,
+                          clip_processor=clp, verbose=False)
+    mf.set_vault(syn.vault(2170, 512, 77), meta)
+    benchrun.progress("per-sample lines: analyze() at B=1")
+    for i in range(warmup):
+        mf.analyze(text=texts[i], image_path=pils[i], verbose=False)
+    lat = []
+    for i in range(warmup, warmup + n_lat):
+        t0 = time.perf_counter()
+        mf.analyze(text=texts[i], image_path=pils[i], verbose=False)
+        lat.append(time.perf_counter() - t0)
+    lat_ms = np.asarray(lat) * 1e3
+    benchrun.progress("per-sample lines: FusionTrainingDataset rows")
+
+    def row(i):
+        ts = mf.analyze_text(texts[i])
+        im = mf.analyze_image(pils[i])
+        cs = mf.analyze_consistency(texts[i], pils[i])
+        vr = mf.search_vault(pils[i])
+        return [ts["ai_score"], ts["misinfo_score"], im["deepfake_score"], cs["clip_similarity"],
+                vr["vault_discrepancy"]]
+    for i in range(warmup):
+        row(i)
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + n_rows):
+        row(i)
+    dt = time.perf_counter() - t0
+    mf.engine.close()
+    return {"analyze_b1": {"config": "analyze(text, image) one pair per call (dashboard path, "
+                                     "forensics_dashboard.py:180-185), 224x224 PIL image, L=128 text",
+                           "p50_ms": round(float(np.percentile(lat_ms, 50)), 3),
+                           "p99_ms": round(float(np.percentile(lat_ms, 99)), 3),
+                           "mean_ms": round(float(lat_ms.mean()), 3), "calls": n_lat,
+                           "value": round(1000.0 / float(lat_ms.mean()), 1), "unit": "pairs/s"},
+            "fusion_dataset_rows": {"config": "FusionTrainingDataset.__getitem__ extraction (train_fusion_judge.py:"
+                                              "72-86): analyze_text + analyze_image + analyze_consistency + "
+                                              "search_vault per row",
+                                    "value": round(n_rows / dt, 1), "unit": "rows/s",
+                                    "ms_per_row": round(1000 * dt / n_rows, 3), "rows": n_rows}}
+
+
 def main():
     a = parse()
     world, rank, local = benchrun.rank_env()
@@ -224,6 +286,9 @@ def main():
     configs = None
     if world == 1 and not a.no_configs:
         configs = config_lines(eng, t, a.steps, a.warmup, det)
+    per_sample = None
+    if world == 1 and not a.no_per_sample:
+        per_sample = per_sample_lines()
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.cpu_seconds)
@@ -242,7 +307,7 @@ def main():
                "hbm_resident": {"value": round(hbm, 2), "unit": "pairs/s", "ms_per_step": round(1000 * dt_hbm / a.steps, 3),
                                 "note": "same step with inputs already in HBM and results left on the device"},
                "achieved_tflops_whole_path": round(value * GFLOP_PER_PAIR / 1e3, 1),
-               "roofline": roofline, "configs": configs, "cpu_baseline": cpu}
+               "roofline": roofline, "configs": configs, "per_sample": per_sample, "cpu_baseline": cpu}
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -31,6 +31,7 @@ extern "C" {
 #define MMF_EINVAL (-22)
 #define MMF_ENOMEM (-12)
 #define MMF_EIO (-5)
+#define MMF_ERANGE (-34) /* an input outside a kernel's supported range (mmf_resize_pil: too many taps) */
 
 #define MMF_DTYPE_F32 0
 #define MMF_DTYPE_I64 1
@@ -107,9 +108,15 @@ int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, 
  * (host arrays) -> out_effnet uint8 [B,224,224,3] =
  * Image.resize((224,224), BILINEAR) and out_clip uint8 [B,224,224,3] = shortest edge -> 224 BICUBIC
  * + centre crop, both bit-exact with Pillow's resampler (either output may be NULL).  Returns after
- * the work on `stream` has completed. */
+ * the work on `stream` has completed; MMF_ERANGE (nothing launched) when an image needs more taps
+ * per output pixel than the kernels hold (mmf_resize_supported). */
 int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, const int32_t* wh, int B,
                    int pixel_bytes, uint8_t* out_effnet, uint8_t* out_clip, void* stream);
+
+/* 1 if a width x height image fits mmf_resize_pil's tap budget in both geometries (bicubic CLIP:
+ * shortest side <= ~5264 px; bilinear EfficientNet: either side <= ~10528 px), else 0.  Host-only,
+ * no handle: callers route the few larger images to a host resampler. */
+int mmf_resize_supported(int width, int height);
 
 /* Truth-Vault (misinfo_forensics.py:214-246, 443-445): host fp32 [N, D=512] raw embeddings; rows
  * are L2-normalised once here instead of on every search call. */

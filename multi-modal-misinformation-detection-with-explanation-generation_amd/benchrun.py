@@ -1,6 +1,6 @@
 """Rank plumbing of the benchmark (bench.py), factored out so that the multi-process path runs in
-the CPU test suite exactly as it runs on an 8-GPU node (tests/test_bench_multirank_cpu.py drives
-these functions over a gloo world of 2 with a CPU stand-in engine).
+the CPU test suite exactly as it runs on an 8-GPU node (tests/test_multiproc_cpu.py::
+test_benchrun_gloo_world2 drives these functions over a gloo world of 2 with a CPU stand-in engine).
 
 One process per GPU (torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE and
 MASTER_*); the batch is sharded by rank with no collective on the data path:

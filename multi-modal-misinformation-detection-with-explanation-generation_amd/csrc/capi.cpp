@@ -1551,7 +1551,7 @@ int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, co
       if (!o) continue;
       ResizeJob J;
       if (!plan_job(w, ht, geom, &J))
-        return fail(MMF_EINVAL, "image %d (%dx%d): downscale beyond %d taps per output pixel", i, w, ht, kResizeKMax);
+        return fail(MMF_ERANGE, "image %d (%dx%d): downscale beyond %d taps per output pixel", i, w, ht, kResizeKMax);
       J.src_off = offsets[i];
       J.ps = pixel_bytes;
       J.tmp_off = tmp;
@@ -1583,6 +1583,12 @@ int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, co
   HIPCHK(launch_resize_pil(src, R.jobs, (int)nj, max_rows, R.coef, R.bounds, R.tmp, R.outs, s));
   HIPCHK(hipStreamSynchronize(s));  // the host job tables above are released on return
   return 0;
+}
+
+int mmf_resize_supported(int width, int height) {
+  if (width <= 0 || height <= 0) return 0;
+  ResizeJob J;
+  return plan_job(width, height, 0, &J) && plan_job(width, height, 1, &J) ? 1 : 0;
 }
 
 int64_t mmf_device_bytes(mmf_handle* h) {

@@ -372,12 +372,15 @@ hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, 
     hipLaunchKernelGGL(vault_topk_kernel<KK>, grid, blk, 0, s, S, B, N, thresh, sims, idx, disc, disc_stride, \
                        text_emb, title_emb, D, text_sim);                                                      \
     break;
-  if (k < 1 || k > N) return hipErrorInvalidValue;
+  // k > N is the reference's argsort(...)[-k:] on a short vault: it keeps all N rows.  The
+  // register kernels pad slots N..k-1 with (-inf, -1) (the host drops idx < 0), so a fixed k = 5
+  // (mmf_analyze_batch) serves a vault of any size; the sort kernel pads the same way up to P.
+  if (k < 1 || N < 1) return hipErrorInvalidValue;
   switch (k) {
     TOPK_CASE(1) TOPK_CASE(2) TOPK_CASE(3) TOPK_CASE(4) TOPK_CASE(5) TOPK_CASE(6) TOPK_CASE(7) TOPK_CASE(8)
     default: {
 #define SORT_CASE(PP)                                                                                            \
-  if (N <= PP) {                                                                                                 \
+  if (N <= PP && k <= PP) {                                                                                      \
     hipLaunchKernelGGL(vault_sort_topk_kernel<PP>, dim3(B), dim3(1024), 0, s, S, B, N, k, thresh, sims, idx, disc, \
                        disc_stride, text_emb, title_emb, D, text_sim);                                          \
     return hipGetLastError();                                                                                    \

@@ -96,6 +96,10 @@ class Engine:
                                                 stream_ptr()), "mmf_set_vault_titles")
 
     # ------------------------------------------------------------------ host-input geometry
+    def resize_supported(self, width: int, height: int) -> bool:
+        """Whether mmf_resize_pil's tap budget covers a width x height image (both geometries)."""
+        return bool(self.lib.mmf_resize_supported(int(width), int(height)))
+
     def resize_images(self, images, effnet: bool = True, clip: bool = True):
         """Decoded uint8 images (HxWx3 RGB or HxWx4 RGBX numpy arrays -- all of one kind --, any
         sizes) -> device uint8 [B,224,224,3] EfficientNet squash-resize and CLIP shortest-edge +

@@ -31,6 +31,7 @@ SIGNATURES = {
     "mmf_clip_text": (_I, [_P, _P, _P, _I, _I, _P, _P]),
     "mmf_clip_consistency": (_I, [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
     "mmf_resize_pil": (_I, [_P, _P, _P, _P, _I, _I, _P, _P, _P]),
+    "mmf_resize_supported": (_I, [_I, _I]),
     "mmf_set_vault": (_I, [_P, _P, _I, _I]),
     "mmf_set_vault_normalized": (_I, [_P, _P, _I, _I]),
     "mmf_set_vault_titles": (_I, [_P, _P, _P, _I, _I, _P]),

@@ -42,7 +42,8 @@ def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:
         if counts[k] == 0:
             continue
         name = lib.mmf_profile_kind_name(k).decode()
-        mfma = name.startswith("gemm") or name == "attention"
+        # attention reads qkv once at ~4.2 TB/s for ~210 TFLOP/s: an HBM kernel
+        mfma = name.startswith("gemm")
         rows.append({"kernel": name, "launches_per_step": counts[k] / steps, "ms_per_step": ms[k] / steps,
                      "avg_launch_us": 1000.0 * ms[k] / counts[k],
                      "tflops": fl[k] / (ms[k] / 1e3) / 1e12, "gbs": by[k] / (ms[k] / 1e3) / 1e9,

@@ -92,3 +92,38 @@ def fusion_inputs(batch: int = 1024, seed: int = 1234) -> np.ndarray:
     hit = g.uniform(0, 1, batch) < 0.25
     x[:, 4] = np.where(hit, g.uniform(0.86, 1.0, batch), 0.0)
     return x
+
+
+class IdTableTokenizer:
+    """Tokenizer-call interface over a {text: token-id list} table (the vocab files are absent):
+    RoBERTa's call of misinfo_forensics.py:327-333 (``max_length`` truncation) and the CLIP
+    processor's text call of :386-391 / :473-478 (``truncation`` at 77); right padding with
+    ``pad_id``.  Used by the per-sample bench lines, which time the API around a tokenizer."""
+
+    def __init__(self, table, pad_id: int, clip: bool = False):
+        self.table, self.pad_id, self.clip = table, pad_id, clip
+
+    def __call__(self, text=None, images=None, return_tensors="pt", max_length=512, truncation=False,
+                 padding=True):
+        import torch
+        texts = [text] if isinstance(text, str) else list(text)
+        cap = 77 if self.clip else max_length
+        seqs = [list(self.table[s])[:cap] if truncation else list(self.table[s]) for s in texts]
+        L = max(len(s) for s in seqs)
+        ids = torch.full((len(seqs), L), self.pad_id, dtype=torch.long)
+        mask = torch.zeros((len(seqs), L), dtype=torch.long)
+        for i, s in enumerate(seqs):
+            ids[i, :len(s)] = torch.tensor(s)
+            mask[i, :len(s)] = 1
+        return {"input_ids": ids, "attention_mask": mask}
+
+
+def text_tables(n: int, seed: int = 1234, rob_len: int = 128, clip_len: int = 77):
+    """n texts "pair i" -> (RoBERTa ids of ``rob_len`` tokens, CLIP ids of ``clip_len`` tokens),
+    the same ids the batched bench uses for the same seed."""
+    rid, _ = roberta_ids(n, rob_len, seed)
+    cid, _ = clip_ids(n, clip_len, seed)
+    texts = [f"pair {i}" for i in range(n)]
+    rob = {t: rid[i].tolist() for i, t in enumerate(texts)}
+    clp = {t: cid[i].tolist() for i, t in enumerate(texts)}
+    return texts, IdTableTokenizer(rob, 1), IdTableTokenizer(clp, CLIP_TEXT["eos_id"], clip=True)

@@ -38,3 +38,20 @@ def test_missing_library_fails_loudly(tmp_path):
     import mmf_amd.hip as hip
     with pytest.raises(hip.MMFError):
         hip.load(str(tmp_path / "nope.so"))
+
+
+def test_resize_tap_budget_host_only():
+    """mmf_resize_supported (host arithmetic only, no device): Pillow's tap count per output pixel,
+    ks = 2 * ceil(support) + 1 with support = filter_support * scale, must fit kResizeKMax = 96 in
+    both geometries -- bicubic CLIP (support 2) on the shortest side, bilinear EfficientNet squash
+    (support 1) on each side."""
+    import mmf_amd.hip as hip
+    lib = hip.load()
+    assert lib.mmf_resize_supported(224, 224) == 1
+    assert lib.mmf_resize_supported(640, 480) == 1
+    assert lib.mmf_resize_supported(5264, 5264) == 1   # scale 23.5 -> support 47 -> 95 taps
+    assert lib.mmf_resize_supported(5265, 5265) == 0   # 97 taps
+    assert lib.mmf_resize_supported(8000, 6000) == 0   # a 48 MP photo: host Pillow for that image
+    assert lib.mmf_resize_supported(10528, 200) == 1   # squash: scale 47 -> 95 taps
+    assert lib.mmf_resize_supported(10529, 200) == 0
+    assert lib.mmf_resize_supported(0, 10) == 0

@@ -160,7 +160,7 @@ def test_retrained_fusion_layer_reaches_the_kernel(forensics):
     got = forensics.fusion_verdict(s)
     det.eval()
     with torch.no_grad():
-        p = torch.softmax(det.forward_fusion(torch.tensor([[0.4, 0.6, 0.2, 0.1, 0.0]])), 1)[0]
+        p = torch.softmax(det.forward_fusion(torch.tensor([[0.4, 0.6, 0.2, 0.1, 0.0]], device=forensics.device)), 1)[0]
     assert abs(got["fake_probability"] - p[1].item()) < 1e-5
     det.fusion_layer.load_state_dict(saved)
     forensics.detector.sync_fusion(force=True)

@@ -1,0 +1,172 @@
+"""train_fusion_judge.py on the MI355X.
+
+The detector lives on ``forensics.device`` like the reference's (misinfo_forensics.py:172), so the
+reference's training script runs unchanged against it:
+
+* ``FusionTrainingDataset.__getitem__`` (train_fusion_judge.py:53-104): four per-sample calls per
+  row (analyze_text, analyze_image, analyze_consistency, search_vault without caption) -> [5];
+  compared with the scores the reference's own analyze() produced (tests/golden/golden.json);
+* the freeze / AdamW / CosineAnnealingLR / CrossEntropy / ``torch.cuda.amp`` autocast + GradScaler
+  loop body of train_fusion_judge.py:139-227, on CUDA tensors;
+* the checkpoint of :259-267 (device tensors) reloaded through test_fusion_model's path
+  (:294-297: ``torch.load(map_location=forensics.device)`` + strict ``load_state_dict``);
+* after training, the HIP fusion kernel (``fusion_verdict``) equals the on-device
+  ``forward_fusion`` softmax at 1e-5.
+"""
+import os
+import sys
+import warnings
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _tables(golden, gi):
+    rob, clp = {}, {}
+    for i in range(golden["rob_ids"].shape[0]):
+        t = f"sample text {i}"
+        rob[t] = golden["rob_ids"][i, :gi["rob_lens"][i]].tolist()
+        clp[t] = golden["clip_ids"][i, :gi["clip_lens"][i]].tolist()
+    for j, ids in enumerate(gi["title_ids"]):
+        clp[f"Guardian article {j}"] = ids.tolist()
+    return rob, clp
+
+
+def _forensics(golden, golden_inputs, det_sd, clip_sd, fusion_weights="/nonexistent"):
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from tables import TableClipProcessor, TableRobertaTokenizer
+    from misinfo_forensics import MisinfoForensics
+    rob, clp = _tables(golden, golden_inputs)
+    mf = MisinfoForensics(fusion_weights=fusion_weights, faiss_index_path="/nonexistent",
+                          roberta_tokenizer=TableRobertaTokenizer(rob), clip_processor=TableClipProcessor(clp),
+                          detector_state=det_sd, clip_state=clip_sd, max_batch=16, verbose=False)
+    mf.set_vault(golden_inputs["vault"], golden_inputs["meta"])
+    return mf
+
+
+def _row_scores(forensics, text, image_path):
+    """train_fusion_judge.py:72-94 (FusionTrainingDataset.__getitem__'s extraction)."""
+    text_scores = forensics.analyze_text(text)
+    image_scores = forensics.analyze_image(image_path)
+    consistency_scores = forensics.analyze_consistency(text, image_path)
+    vault_results = forensics.search_vault(image_path)
+    return torch.tensor([text_scores["ai_score"], text_scores["misinfo_score"], image_scores["deepfake_score"],
+                         consistency_scores["clip_similarity"], vault_results["vault_discrepancy"]],
+                        dtype=torch.float32)
+
+
+def test_detector_lives_on_the_device(golden, golden_inputs, det_sd, clip_sd):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    mf = _forensics(golden, golden_inputs, det_sd, clip_sd)
+    devs = {p.device for p in mf.detector.parameters()} | {b.device for b in mf.detector.buffers()}
+    assert devs == {mf.device}, devs
+    sd = mf.detector.state_dict()
+    assert all(v.device == mf.device for v in sd.values())
+    mf.engine.close()
+
+
+def test_fusion_training_loop_on_device(golden, golden_json, golden_inputs, det_sd, clip_sd, tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from PIL import Image
+    from misinfo_forensics import MisinfoForensics
+    forensics = _forensics(golden, golden_inputs, det_sd, clip_sd)
+    device = forensics.device
+
+    # ---- FusionTrainingDataset rows (train_fusion_judge.py:53-104), 8 samples ---------------
+    rows = []
+    for i in range(8):
+        p = str(tmp_path / f"img{i}.png")
+        Image.fromarray(golden_inputs["imgs"][i]).save(p)
+        rows.append((f"sample text {i}", p, i % 2))
+    feats = torch.stack([_row_scores(forensics, t, p) for t, p, _ in rows])
+    for i, ref in enumerate(golden_json["analyze"][:8]):
+        want = [ref["scores"][k] for k in ("ai_score", "misinfo_score", "deepfake_score", "clip_similarity",
+                                           "vault_discrepancy")]
+        np.testing.assert_allclose(feats[i].numpy(), want, atol=1e-3, err_msg=f"row {i}")
+    labels_all = torch.tensor([lb for _, _, lb in rows], dtype=torch.long)
+
+    # ---- train_fusion_judge.py:139-153: freeze everything but the fusion layer ---------------
+    forensics.detector.eval()
+    for param in forensics.detector.parameters():
+        param.requires_grad = False
+    for param in forensics.detector.fusion_layer.parameters():
+        param.requires_grad = True
+    trainable = sum(p.numel() for p in forensics.detector.parameters() if p.requires_grad)
+    assert trainable == 5 * 64 + 64 + 64 * 32 + 32 + 32 * 2 + 2
+
+    # ---- :179-227 verbatim loop body (DataLoader(batch_size=4, shuffle) replaced by fixed slices)
+    from torch.cuda.amp import GradScaler, autocast
+    lr = 1e-2
+    optimizer = torch.optim.AdamW(forensics.detector.fusion_layer.parameters(), lr=lr, weight_decay=0.01)
+    scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=3, eta_min=lr * 0.1)
+    criterion = nn.CrossEntropyLoss()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", FutureWarning)  # torch.cuda.amp.* deprecation notices
+        scaler = GradScaler()
+        before = {k: v.clone() for k, v in forensics.detector.fusion_layer.state_dict().items()}
+        for epoch in range(1, 4):
+            forensics.detector.fusion_layer.train()
+            for s in range(0, 8, 4):
+                scores = feats[s:s + 4].to(device)
+                labels = labels_all[s:s + 4].to(device)
+                optimizer.zero_grad()
+                with autocast():
+                    logits = forensics.detector.forward_fusion(scores)
+                    loss = criterion(logits, labels)
+                scaler.scale(loss).backward()
+                scaler.step(optimizer)
+                scaler.update()
+                assert logits.device == device and torch.isfinite(loss)
+                _, predicted = torch.max(logits, 1)
+                (predicted == labels).sum().item()
+            scheduler.step()
+    after = forensics.detector.fusion_layer.state_dict()
+    assert any(not torch.equal(before[k], after[k]) for k in before), "the optimizer never stepped"
+    assert forensics.detector.roberta.encoder.layer[0].attention.self.query.weight.grad is None
+
+    # ---- the trained layer reaches the HIP fusion kernel --------------------------------------
+    forensics.detector.eval()
+    x = feats.to(device)
+    with torch.no_grad():
+        p_ref = torch.softmax(forensics.detector.forward_fusion(x), 1).cpu().numpy()
+    for i in range(8):
+        s = dict(zip(("ai_score", "misinfo_score", "deepfake_score", "clip_similarity", "vault_discrepancy"),
+                     feats[i].tolist()))
+        v = forensics.fusion_verdict(s)
+        assert abs(v["fake_probability"] - p_ref[i, 1]) < 1e-5 and abs(v["real_probability"] - p_ref[i, 0]) < 1e-5
+        assert v["verdict"] == int(p_ref[i, 1] > 0.5)
+    assert forensics.detector.uploads["fusion"] >= 2 and forensics.detector.uploads["text"] == 1
+
+    # ---- checkpoint (:259-267, device tensors) and test_fusion_model's reload (:294-313) ------
+    ck_path = str(tmp_path / "forensics_master_final.pth")
+    torch.save({"epoch": 3, "fusion_layer_state_dict": forensics.detector.fusion_layer.state_dict(),
+                "full_model_state_dict": forensics.detector.state_dict(),
+                "optimizer_state_dict": optimizer.state_dict(), "scheduler_state_dict": scheduler.state_dict(),
+                "loss": float(loss.item()), "accuracy": 50.0}, ck_path)
+    pairs_before = forensics.analyze_pairs([t for t, _, _ in rows], [p for _, p, _ in rows])
+    forensics.engine.close()
+
+    # a fresh system whose constructor finds the checkpoint (misinfo_forensics.py:175-182) ...
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from tables import TableClipProcessor, TableRobertaTokenizer
+    rob, clp = _tables(golden, golden_inputs)
+    fresh = MisinfoForensics(fusion_weights=ck_path, faiss_index_path="/nonexistent",
+                             roberta_tokenizer=TableRobertaTokenizer(rob), clip_processor=TableClipProcessor(clp),
+                             detector_state=det_sd, clip_state=clip_sd, max_batch=16, verbose=False)
+    fresh.set_vault(golden_inputs["vault"], golden_inputs["meta"])
+    # ... and test_fusion_model's explicit strict reload (weights_only: files this test wrote)
+    checkpoint = torch.load(ck_path, map_location=fresh.device, weights_only=True)
+    fresh.detector.load_state_dict(checkpoint["full_model_state_dict"])
+    for k, v in fresh.detector.fusion_layer.state_dict().items():
+        assert torch.equal(v, after[k].to(v.device)), k
+    pairs_after = fresh.analyze_pairs([t for t, _, _ in rows], [p for _, p, _ in rows])
+    for a, b in zip(pairs_before, pairs_after):
+        assert a["verdict"] == b["verdict"] and a["explanation"] == b["explanation"]
+        assert a["scores"] == b["scores"], (a["scores"], b["scores"])
+    fresh.engine.close()

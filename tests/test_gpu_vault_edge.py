@@ -107,3 +107,36 @@ def test_vault_reload_frees_device_memory(engine):
     torch.cuda.synchronize()
     assert engine.device_bytes == b0
     assert abs(torch.cuda.mem_get_info()[0] - f0) < 8 << 20
+
+
+@pytest.mark.parametrize("n_rows", [1, 2, 3])
+def test_analyze_batch_with_short_vault(det_sd, clip_sd, n_rows):
+    """A vault of fewer than 5 rows through the 5-signal batch: the reference's
+    argsort(sims)[-5:][::-1] keeps all N rows, so analyze_batch returns N matches per pair (slots
+    N..4 hold idx -1, which the dict builder drops), ranked as search_vault ranks them, and the
+    discrepancy of the top-1 row."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    B = 4
+    eng = Engine(0, det_sd, clip_sd, max_batch=B, max_text_len=32)
+    try:
+        rid, rm = syn.roberta_ids(B, 32, 5, [32, 20, 7, 3])
+        cid, cm = syn.clip_ids(B, 77, 5, [77, 12, 5, 2])
+        imgs = syn.images(B, 5)
+        emb = eng.clip_image(imgs)
+        vault = syn.vault(n_rows, 512, 7)
+        vault[0] = emb[1].cpu().numpy() * 2.0  # a planted hit for pair 1 (> 0.85)
+        eng.set_vault(vault)
+        out = eng.analyze_batch(rid, rm, cid, cm, imgs)
+        s_all, i_all, d_all, _ = eng.vault_topk(emb, n_rows, 0.85)
+        torch.cuda.synchronize()
+        idx = out["top_idx"].cpu().numpy()
+        assert (idx[:, n_rows:] == -1).all()
+        np.testing.assert_array_equal(idx[:, :n_rows], i_all.cpu().numpy())
+        np.testing.assert_allclose(out["top_sims"].cpu().numpy()[:, :n_rows], s_all.cpu().numpy(), atol=1e-6)
+        np.testing.assert_allclose(out["scores"].cpu().numpy()[:, 4], d_all.cpu().numpy(), atol=1e-6)
+        assert out["scores"][1, 4].item() > 0.85
+    finally:
+        eng.close()

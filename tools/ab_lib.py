@@ -30,17 +30,17 @@ def main():
     shapes = ([(n, M, N, K, act, sc, rs, rpb) for n, M, N, K, act, sc, rs, rpb in EFFNET] if a.effnet else
               [(n, M, N, K, act, 0, 0, 1) for n, M, N, K, act, _ in SHAPES + ROUND])
     for name, M, N, K, act, sc, rs, rpb in shapes:
-        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.float16)
+        W = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.float16)
         bias = torch.randn(N, device=dev)
         S = torch.rand((M + rpb - 1) // rpb, K, device=dev) if sc else None
-        R = torch.randn(M, N, device=dev).to(torch.bfloat16) if rs else None
-        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        R = torch.randn(M, N, device=dev).to(torch.float16) if rs else None
+        C = torch.empty(M, N, device=dev, dtype=torch.float16)
         times = [[], []]
         for _ in range(a.rounds):
             for i, lib in enumerate(libs):
                 def call():
-                    hip.check(lib.mmf_gemm_bf16_ex(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R),
+                    hip.check(lib.mmf_gemm_f16_ex(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), hip.ptr(R),
                                                    hip.ptr(S), rpb, C.data_ptr(), N, M, N, K, act,
                                                    hip.stream_ptr()))
                 call()
