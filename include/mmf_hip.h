@@ -173,6 +173,10 @@ const char* mmf_profile_kind_name(int kind);
  * (EfficientNet tower with fp32 activations, fp32-FMA 1x1 convs and precise SiLU: the mode for
  * checkpoints whose logits amplify fp16 storage rounding past 1e-3; ~4x the tower time).  With the
  * defaults a row's results do not depend on the batch it runs in (tests/test_gpu_parity.py).
+ * "text_hilo" = -1 (default) picks RoBERTa's residual-stream layout when the weights are packed:
+ * fp16 hi + lo if the LayerNorm parameters bound the stream above 64 (max_c |beta_c| + 4|gamma_c|,
+ * trained-model outlier channels), fp16 alone otherwise; the read-only name "text_hilo_effective"
+ * (mmf_get_option with a handle) returns the layout in use.
  * h = NULL reads/changes the process defaults used by the handle-less ops below and by handles
  * created afterwards. */
 int mmf_set_option(mmf_handle* h, const char* name, int value);

@@ -22,6 +22,7 @@ from typing import Dict, List, Optional, Sequence, Tuple, Union
 import numpy as np
 import torch
 import torch.nn as nn
+import xxhash
 
 from . import explain, io_utils, weights as W
 from .engine import Engine, SCORE_KEYS
@@ -324,6 +325,8 @@ class MisinfoForensics:
         if self.gemini_api_key:
             self._log("⚠ Gemini client not available in this build. Using fallback explanations.")
 
+        self._emb_cache = None  # (hash of the CLIP input window, its image embedding): _image_emb
+        self.vit_passes = 0  # single-image ViT launches (observability, tests)
         self.roberta_tokenizer = roberta_tokenizer
         self.clip_processor = clip_processor
         if self.roberta_tokenizer is None:
@@ -474,7 +477,20 @@ class MisinfoForensics:
         return {"deepfake_score": float(sc.cpu().numpy()[0])}
 
     def _image_emb(self, pil) -> torch.Tensor:
-        return self.engine.clip_image(io_utils.clip_pixels(pil)[None])
+        """CLIP image embedding [1,512] of one image.  analyze_consistency and search_vault both
+        embed the image (quirk Q6: the reference runs the ViT twice per pair, misinfo_forensics.py:395,
+        438; FusionTrainingDataset calls them back to back, train_fusion_judge.py:81-85): the last
+        embedding is kept with a 128-bit hash of its 224x224 input window, and an identical window
+        reuses it -- the same kernels on the same bytes, so the value is the one a second ViT pass
+        would return."""
+        px = io_utils.clip_pixels(pil)
+        key = xxhash.xxh3_128_digest(px.tobytes())
+        if self._emb_cache is not None and self._emb_cache[0] == key:
+            return self._emb_cache[1]
+        emb = self.engine.clip_image(px[None])
+        self._emb_cache = (key, emb)
+        self.vit_passes += 1
+        return emb
 
     def analyze_consistency(self, text: str, image_path) -> Dict[str, float]:
         """misinfo_forensics.py:375-408."""

@@ -154,7 +154,7 @@ def test_retrained_fusion_layer_reaches_the_kernel(forensics):
     det = forensics.detector
     saved = {k: v.clone() for k, v in det.fusion_layer.state_dict().items()}
     with torch.no_grad():
-        det.fusion_layer[5].bias.add_(torch.tensor([0.3, -0.3]))
+        det.fusion_layer[5].bias.add_(torch.tensor([0.3, -0.3], device=forensics.device))
     s = {"ai_score": 0.4, "misinfo_score": 0.6, "deepfake_score": 0.2, "clip_similarity": 0.1,
          "vault_discrepancy": 0.0}
     got = forensics.fusion_verdict(s)

@@ -84,7 +84,9 @@ def test_fusion_training_loop_on_device(golden, golden_json, golden_inputs, det_
         p = str(tmp_path / f"img{i}.png")
         Image.fromarray(golden_inputs["imgs"][i]).save(p)
         rows.append((f"sample text {i}", p, i % 2))
+    v0 = forensics.vit_passes
     feats = torch.stack([_row_scores(forensics, t, p) for t, p, _ in rows])
+    assert forensics.vit_passes - v0 == 8  # search_vault reused analyze_consistency's embedding
     for i, ref in enumerate(golden_json["analyze"][:8]):
         want = [ref["scores"][k] for k in ("ai_score", "misinfo_score", "deepfake_score", "clip_similarity",
                                            "vault_discrepancy")]
@@ -128,7 +130,8 @@ def test_fusion_training_loop_on_device(golden, golden_json, golden_inputs, det_
             scheduler.step()
     after = forensics.detector.fusion_layer.state_dict()
     assert any(not torch.equal(before[k], after[k]) for k in before), "the optimizer never stepped"
-    assert forensics.detector.roberta.encoder.layer[0].attention.self.query.weight.grad is None
+    prm = dict(forensics.detector.named_parameters())
+    assert prm["roberta.encoder.layer.0.attention.self.query.weight"].grad is None
 
     # ---- the trained layer reaches the HIP fusion kernel --------------------------------------
     forensics.detector.eval()
