@@ -131,6 +131,7 @@ struct Options {
   int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
   int dw_v2 = 0;        // depthwise phases with one channel group per wave, weights in SGPRs (effnet.hip)
+  int gemm_ring = 0;    // plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -140,7 +141,7 @@ const OptName kOptNames[] = {
     {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
-    {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},
+    {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},            {"gemm_ring", &Options::gemm_ring, "MMF_GEMM_RING"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -159,6 +160,7 @@ void apply_options(const Options& o, GemmArgs* g) {
   g->no_splitk = o.gemm_splitk ? 0 : 1;
   g->group_m = o.gemm_group_m;
   g->prio = o.gemm_prio;
+  g->ring = o.gemm_ring;
 }
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the

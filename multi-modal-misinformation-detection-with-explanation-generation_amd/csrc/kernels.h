@@ -23,6 +23,7 @@ struct GemmArgs {
   int no_splitk;                 // 1 = never split K on the skinny-M path (A/B option)
   int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
   int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
+  int ring;                      // 1 = plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
@@ -43,6 +44,10 @@ int gemm_ln_tn(const GemmArgs& a);
 // results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
 int gemm_splitk_factor(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
+// ring-pipelined 256x192 kernel (gemm_ring.hip): epi 0, fp16 output only, bias, no residual / A scale,
+// K % 64 == 0, N % 8 == 0
+bool gemm_ring_ok(const GemmArgs& a);
+hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
 const char* gemm_config_name(int c);
 // streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable
