@@ -327,6 +327,7 @@ class MisinfoForensics:
 
         self._emb_cache = None  # (hash of the CLIP input window, its image embedding): _image_emb
         self.vit_passes = 0  # single-image ViT launches (observability, tests)
+        self.reuse_image_embedding = True  # False: a ViT pass per call, as the reference (A/B)
         self.roberta_tokenizer = roberta_tokenizer
         self.clip_processor = clip_processor
         if self.roberta_tokenizer is None:
@@ -484,8 +485,8 @@ class MisinfoForensics:
         reuses it -- the same kernels on the same bytes, so the value is the one a second ViT pass
         would return."""
         px = io_utils.clip_pixels(pil)
-        key = xxhash.xxh3_128_digest(px.tobytes())
-        if self._emb_cache is not None and self._emb_cache[0] == key:
+        key = xxhash.xxh3_128_digest(px.tobytes()) if self.reuse_image_embedding else None
+        if key is not None and self._emb_cache is not None and self._emb_cache[0] == key:
             return self._emb_cache[1]
         emb = self.engine.clip_image(px[None])
         self._emb_cache = (key, emb)

@@ -778,8 +778,8 @@ static int forced_config(const GemmArgs& a) {
   const int c = a.force_cfg - 1;
   if (((c >= 4 && c <= 8) || c >= 10) && !glds_ok(a)) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
-  if (c == 12 && !gemm_ring_ok(a)) return -1;
-  return (c >= 0 && c <= 12) ? c : -1;
+  if (c >= 12 && !gemm_ring_ok(a)) return -1;
+  return (c >= 0 && c <= 14) ? c : -1;
 }
 
 // persistent 256-row LDS-DMA tiles: the column tile that minimises whole "rounds" of 256 CUs x
@@ -840,8 +840,8 @@ const char* gemm_config_name(int c) {
                                 "gemm_f16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
                                 "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
                                 "pw_conv", "gemm_glds_pipe2<256,192,4,2>", "gemm_glds_pipe2<256,256,2,4>",
-                                "gemm_ring<256,192,4,2>"};
-  return (c >= 0 && c < 13) ? names[c] : "gemm_f16<?>";
+                                "gemm_ring<256,192,4,2>", "gemm_ring_dma_only", "gemm_ring_compute_only"};
+  return (c >= 0 && c < 15) ? names[c] : "gemm_f16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
@@ -853,6 +853,7 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
     return gemm_config(a) == 11 ? run_glds_epi<256, 256, 2, 4>(a, s) : run_glds_epi<256, 192, 4, 2>(a, s);
   }
   const int cfg = gemm_config(a);
+  if (cfg == 13 || cfg == 14) return launch_gemm_ring(a, s, cfg - 12);  // measurement builds (garbage out)
   if (cfg == 12 || (a.ring && (cfg == 10 || cfg == 11 || cfg == 5) && gemm_ring_ok(a))) return launch_gemm_ring(a, s);
   switch (cfg) {
     case 0: return run<256, 32, 4, 1>(a, s);

@@ -61,7 +61,10 @@ MMF_DEV void wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-template <int ACT, int NS>
+// DBG (measurement builds, forced configs 13 / 14 only): 1 = LDS-DMA, waits and barriers only (no
+// fragment reads, no MFMA: the fill rate of the ring), 2 = no LDS-DMA (fragment reads, MFMAs and
+// barriers on whatever the LDS holds: the compute side alone).  Outputs are garbage in both.
+template <int ACT, int NS, int DBG = 0>
 __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tilesN, int tiles) {
   static_assert(NS >= 4, "the ring needs a slot being read, one being filled and >= 1 in flight");
   __shared__ __attribute__((aligned(16))) char lds[NS * kSlotBytes + 2 * kBiasBytes];
@@ -89,6 +92,7 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
   auto chunk_of = [&](int row) { return (lane & 3) ^ (((row >> 3) & 1) << 1); };
 
   auto issue = [&](int gs) {
+    if constexpr (DBG == 2) return;
     int i = gs / nk, kt = gs - i * nk;
     if (i >= my_tiles) {  // past the last stage: re-load it (a free slot), so every step issues
       i = my_tiles - 1;   // the same number of DMAs and the counted waits stay exact
@@ -149,6 +153,7 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
     }
   };
   auto mfmas_with_reads = [&](const f16x8* wc, const f16x8* xc, int gs_next, f16x8* wn_, f16x8* xn_) {
+    if constexpr (DBG == 1) return;
     read_frags(gs_next, wn_, xn_);
 #pragma unroll
     for (int i = 0; i < RNI; ++i)
@@ -230,12 +235,20 @@ bool gemm_ring_ok(const GemmArgs& a) {
          a.K >= 128 && (a.N % 8) == 0 && a.N >= 8 && a.M > 0 && (size_t)(a.M + RBM) * a.ldc * 2 < lim;
 }
 
-hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s) {
+hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s, int dbg) {
   if (!gemm_ring_ok(a)) return hipErrorInvalidValue;
   const int tilesM = (a.M + RBM - 1) / RBM, tilesN = (a.N + RBN - 1) / RBN;
   const int tiles = tilesM * tilesN;
   const int grid = tiles < 256 ? tiles : 256;
   constexpr int NS = 5;
+  if (dbg == 1) {
+    hipLaunchKernelGGL((gemm_ring_kernel<ACT_NONE, NS, 1>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+    return hipGetLastError();
+  }
+  if (dbg == 2) {
+    hipLaunchKernelGGL((gemm_ring_kernel<ACT_NONE, NS, 2>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);
+    return hipGetLastError();
+  }
 #define MMF_RING_CASE(ACT)                                                                                      \
   case ACT:                                                                                                     \
     hipLaunchKernelGGL((gemm_ring_kernel<ACT, NS>), dim3(grid), dim3(512), 0, s, a, tilesN, tiles);             \

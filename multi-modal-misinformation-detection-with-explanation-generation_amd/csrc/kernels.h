@@ -47,7 +47,7 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 // ring-pipelined 256x192 kernel (gemm_ring.hip): epi 0, fp16 output only, bias, no residual / A scale,
 // K % 64 == 0, N % 8 == 0
 bool gemm_ring_ok(const GemmArgs& a);
-hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s);
+hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s, int dbg = 0);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
 const char* gemm_config_name(int c);
 // streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable
