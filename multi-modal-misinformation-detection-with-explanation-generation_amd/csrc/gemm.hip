@@ -266,7 +266,9 @@ MMF_DEV void tile_coords(int t, int tilesM, int tilesN, int gm, int& tm, int& tn
 // the second K-step and combined into (mean, rstd) per row at the top of the third.
 constexpr int kLnPMax = 8;  // partials per row a reader accepts
 
-template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0>
+// DBG (measurement builds, forced configs 15 / 16 only; outputs garbage): 1 = LDS-DMA + barriers only,
+// 2 = fragment reads + MFMAs + barriers only
+template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
                                                                      int gm) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
@@ -313,6 +315,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   if (t >= tiles) return;
   if ((g.prio == 1 && wave >= NW / 2) || (g.prio == 2 && wave < NW / 2)) __builtin_amdgcn_s_setprio(1);
   auto stage = [&](int buf, int tile, int kt) {
+    if constexpr (DBG == 2) return;
     int tm_, tn_;
     tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);
     f16_t* nb = lds + buf * STAGE;
@@ -422,7 +425,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
       else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
       const f16_t* Xs = lds + cur * STAGE;
       const f16_t* Ws = Xs + BM * BK;
-      if constexpr (PIPE2) {
+      if constexpr (DBG == 1) {
+      } else if constexpr (PIPE2) {
         // half-step pipeline: the second K-half's fragment reads are issued between the first
         // half's MFMAs (1 read per 2 MFMAs), so only the first half's reads are exposed after the
         // barrier
@@ -642,7 +646,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false>
+template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false, int DBG = 0>
 hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
@@ -652,9 +656,14 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int gm = a.group_m;  // tile-order option (handle option "gemm_group_m"; 0 = row-major)
 #define MMF_GLDS_CASE(ACT)                                                                                  \
   case ACT:                                                                                                 \
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2>), dim3(grid), blk, 0, s, a, tilesN, tiles, tilesM, \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, a, tilesN, tiles, tilesM, \
                        gm);                                                                                      \
     break;
+  if constexpr (DBG != 0) {
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT_NONE, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, a, tilesN,
+                       tiles, tilesM, gm);
+    return hipGetLastError();
+  }
   switch (a.act) {
     MMF_GLDS_CASE(ACT_NONE)
     MMF_GLDS_CASE(ACT_GELU)
@@ -778,8 +787,8 @@ static int forced_config(const GemmArgs& a) {
   const int c = a.force_cfg - 1;
   if (((c >= 4 && c <= 8) || c >= 10) && !glds_ok(a)) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
-  if (c >= 12 && !gemm_ring_ok(a)) return -1;
-  return (c >= 0 && c <= 14) ? c : -1;
+  if (c >= 12 && c <= 14 && !gemm_ring_ok(a)) return -1;
+  return (c >= 0 && c <= 16) ? c : -1;
 }
 
 // persistent 256-row LDS-DMA tiles: the column tile that minimises whole "rounds" of 256 CUs x
@@ -840,8 +849,9 @@ const char* gemm_config_name(int c) {
                                 "gemm_f16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
                                 "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
                                 "pw_conv", "gemm_glds_pipe2<256,192,4,2>", "gemm_glds_pipe2<256,256,2,4>",
-                                "gemm_ring<256,192,4,2>", "gemm_ring_dma_only", "gemm_ring_compute_only"};
-  return (c >= 0 && c < 15) ? names[c] : "gemm_f16<?>";
+                                "gemm_ring<256,192,4,2>", "gemm_ring_dma_only", "gemm_ring_compute_only",
+                                "gemm_glds_dma_only", "gemm_glds_compute_only"};
+  return (c >= 0 && c < 17) ? names[c] : "gemm_f16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
@@ -854,6 +864,8 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
   }
   const int cfg = gemm_config(a);
   if (cfg == 13 || cfg == 14) return launch_gemm_ring(a, s, cfg - 12);  // measurement builds (garbage out)
+  if (cfg == 15) return run_glds<256, 192, 4, 2, true, 1>(a, s);
+  if (cfg == 16) return run_glds<256, 192, 4, 2, true, 2>(a, s);
   if (cfg == 12 || (a.ring && (cfg == 10 || cfg == 11 || cfg == 5) && gemm_ring_ok(a))) return launch_gemm_ring(a, s);
   switch (cfg) {
     case 0: return run<256, 32, 4, 1>(a, s);

@@ -91,8 +91,10 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
   const int lrow = lane >> 2;
   auto chunk_of = [&](int row) { return (lane & 3) ^ (((row >> 3) & 1) << 1); };
 
-  auto issue = [&](int gs) {
-    if constexpr (DBG == 2) return;
+  // the LDS-DMA pieces of stage gs for this wave: A segments 2w, 2w+1; W segments 2w, 2w+1
+  // (waves 0-3) or 8 + (w - 4) (waves 4-7, whose 4th piece is the tile's bias at kt = 0, wave 7)
+  struct Pieces { const void* src[4]; uint32_t dst[4]; bool has3; };
+  auto plan = [&](int gs, Pieces& d) {
     int i = gs / nk, kt = gs - i * nk;
     if (i >= my_tiles) {  // past the last stage: re-load it (a free slot), so every step issues
       i = my_tiles - 1;   // the same number of DMAs and the counted waits stay exact
@@ -103,26 +105,37 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
     const uint32_t sb = lds0 + (uint32_t)(gs % NS) * kSlotBytes;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int s = 2 * wave + j, row = 16 * s + lrow;
+      const int sg = 2 * wave + j, row = 16 * sg + lrow;
       const int gm = min(m0 + row, M - 1);
-      dma16(g.A + (size_t)gm * g.lda + k0 + chunk_of(row) * 8, __builtin_amdgcn_readfirstlane(sb + s * 1024));
+      d.src[j] = g.A + (size_t)gm * g.lda + k0 + chunk_of(row) * 8;
+      d.dst[j] = __builtin_amdgcn_readfirstlane(sb + sg * 1024);
     }
     if (w4) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int s = 2 * wave + j, row = 16 * s + lrow;
+        const int sg = 2 * wave + j, row = 16 * sg + lrow;
         const int gn = min(n0 + row, N - 1);
-        dma16(g.W + (size_t)gn * g.ldw + k0 + chunk_of(row) * 8,
-              __builtin_amdgcn_readfirstlane(sb + kWOff + s * 1024));
+        d.src[2 + j] = g.W + (size_t)gn * g.ldw + k0 + chunk_of(row) * 8;
+        d.dst[2 + j] = __builtin_amdgcn_readfirstlane(sb + kWOff + sg * 1024);
       }
+      d.has3 = true;
     } else {
-      const int s = 8 + (wave - 4), row = 16 * s + lrow;
+      const int sg = 8 + (wave - 4), row = 16 * sg + lrow;
       const int gn = min(n0 + row, N - 1);
-      dma16(g.W + (size_t)gn * g.ldw + k0 + chunk_of(row) * 8, __builtin_amdgcn_readfirstlane(sb + kWOff + s * 1024));
-      if (kt == 0 && wave == 7)  // the tile's bias, into the buffer of its parity
-        dma16(g.bias + min(n0 + lane * 4, N - 4),
-              __builtin_amdgcn_readfirstlane(lds0 + NS * kSlotBytes + (uint32_t)(i & 1) * kBiasBytes));
+      d.src[2] = g.W + (size_t)gn * g.ldw + k0 + chunk_of(row) * 8;
+      d.dst[2] = __builtin_amdgcn_readfirstlane(sb + kWOff + sg * 1024);
+      d.has3 = kt == 0 && wave == 7;  // the tile's bias, into the buffer of its parity
+      d.src[3] = g.bias + min(n0 + lane * 4, N - 4);
+      d.dst[3] = __builtin_amdgcn_readfirstlane(lds0 + NS * kSlotBytes + (uint32_t)(i & 1) * kBiasBytes);
     }
+  };
+  auto issue = [&](int gs) {
+    if constexpr (DBG == 2) return;
+    Pieces d;
+    plan(gs, d);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dma16(d.src[c], d.dst[c]);
+    if (d.has3) dma16(d.src[3], d.dst[3]);
   };
 
   auto read_frags = [&](int gs, f16x8* wf, f16x8* xf) {
@@ -152,20 +165,50 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
       else wait_barrier<3 * (NS - 3)>();
     }
   };
-  auto mfmas_with_reads = [&](const f16x8* wc, const f16x8* xc, int gs_next, f16x8* wn_, f16x8* xn_) {
-    if constexpr (DBG == 1) return;
-    read_frags(gs_next, wn_, xn_);
+  // one 32-deep step: the wait + barrier for stage gs + 1, then the 24 MFMAs of stage gs in four
+  // groups of 6 with one LDS-DMA piece of stage gs + NS - 1 issued ahead of each group and the 10
+  // fragment reads of stage gs + 1 between the MFMAs (3, 3, 2, 2 per group).  A piece issued as a
+  // block at the top of the step stalls both waves of a SIMD at once (measured: fill and MFMA
+  // time added up, tools/gemm_bench.py configs 13 / 14); spread out, the other wave keeps the MFMA
+  // pipe busy while one waits on its DMA issue.
+  auto step = [&](const f16x8* wc, const f16x8* xc, int gs, f16x8* wnx, f16x8* xnx, bool after_epi) {
+    top_wait(after_epi);
+    Pieces d;
+    if constexpr (DBG != 2) plan(gs + NS - 1, d);
+    const f16_t* xs = reinterpret_cast<const f16_t*>(lds + ((gs + 1) % NS) * kSlotBytes);
+    const f16_t* ws = reinterpret_cast<const f16_t*>(lds + ((gs + 1) % NS) * kSlotBytes + kWOff);
 #pragma unroll
-    for (int i = 0; i < RNI; ++i)
+    for (int c = 0; c < 4; ++c) {
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DBG != 2) {
+        if (c < 3 || d.has3) dma16(d.src[c], d.dst[c]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DBG != 1) {
+        constexpr int r0[5] = {0, 3, 6, 8, 10};
 #pragma unroll
-      for (int j = 0; j < RMI; ++j) acc[i][j] = mfma16x16x32(wc[i], xc[j], acc[i][j]);
-    // interleave: one fragment read per two MFMAs, the rest of the MFMAs after
+        for (int r = r0[c]; r < r0[c + 1]; ++r) {
+          if (r < RNI) wnx[r] = as_f16x8(*reinterpret_cast<const uint4*>(ws + rswz(wn * RTN + r * 16 + fr, fg)));
+          else xnx[r - RNI] = as_f16x8(*reinterpret_cast<const uint4*>(xs + rswz(wm * RTM + (r - RNI) * 16 + fr, fg)));
+        }
 #pragma unroll
-    for (int qq = 0; qq < RNI + RMI; ++qq) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+        for (int q6 = 0; q6 < 6; ++q6) {
+          const int ii = (6 * c + q6) / RMI, jj = (6 * c + q6) % RMI;
+          acc[ii][jj] = mfma16x16x32(wc[ii], xc[jj], acc[ii][jj]);
+        }
+        // DS read, 2 MFMAs, ... (literal arguments: one call site per pattern)
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if (c < 2) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+      }
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, RNI * RMI - 2 * (RNI + RMI), 0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -183,13 +226,9 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
     const int m0 = tm * RBM, n0 = tn * RBN;
 #pragma unroll 1
     for (int kt = 0; kt < nk; kt += 2) {
-      top_wait(i > 0 && kt < NS - 2);
-      issue(gs + NS - 1);
-      mfmas_with_reads(wa, xa, gs + 1, wb, xb);
+      step(wa, xa, gs, wb, xb, i > 0 && kt < NS - 2);
       ++gs;
-      top_wait(i > 0 && kt + 1 < NS - 2);
-      issue(gs + NS - 1);
-      mfmas_with_reads(wb, xb, gs + 1, wa, xa);
+      step(wb, xb, gs, wa, xa, i > 0 && kt + 1 < NS - 2);
       ++gs;
     }
     (void)G;
