@@ -787,17 +787,20 @@ static int forced_config(const GemmArgs& a) {
   const int c = a.force_cfg - 1;
   if (((c >= 4 && c <= 8) || c >= 10) && !glds_ok(a)) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
-  if (c >= 12 && c <= 14 && !gemm_ring_ok(a)) return -1;
-  return (c >= 0 && c <= 16) ? c : -1;
+  if (((c >= 12 && c <= 14) || c >= 17) && !gemm_ring_ok(a)) return -1;
+  return (c >= 0 && c <= 19) ? c : -1;
 }
 
 // persistent 256-row LDS-DMA tiles: the column tile that minimises whole "rounds" of 256 CUs x
 // per-tile time (wider tiles are more efficient per flop); with_128 = also consider 256x128
 static int glds_pick(const GemmArgs& a, bool with_128) {
-  // (the 256- and 192-column tiles run the half-step-pipelined K loop, configs 11 / 10)
+  // (the 256- and 192-column tiles run the half-step-pipelined K loop, configs 11 / 10; with the
+  // option gemm_ring, 192-column tiles that gemm_lc_kernel can serve run it instead, config 17)
   const long tm = (a.M + 255) / 256;
-  const int bns[3] = {256, 192, 128}, cfg[3] = {11, 10, 5};
-  const double eff[3] = {1.0, 0.88, 0.80};  // measured per-flop efficiency (tools/gemm_bench.py)
+  const bool lc = a.ring && gemm_ring_ok(a);
+  const int bns[3] = {256, 192, 128}, cfg[3] = {11, lc ? 17 : 10, 5};
+  // measured per-flop efficiency (tools/gemm_bench.py; the loader / consumer kernel 0.95)
+  const double eff[3] = {1.0, lc ? 0.95 : 0.88, 0.80};
   int best = 11;
   double bc = 1e30;
   for (int i = 0; i < (with_128 ? 3 : 2); ++i) {
@@ -850,8 +853,9 @@ const char* gemm_config_name(int c) {
                                 "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
                                 "pw_conv", "gemm_glds_pipe2<256,192,4,2>", "gemm_glds_pipe2<256,256,2,4>",
                                 "gemm_ring<256,192,4,2>", "gemm_ring_dma_only", "gemm_ring_compute_only",
-                                "gemm_glds_dma_only", "gemm_glds_compute_only"};
-  return (c >= 0 && c < 17) ? names[c] : "gemm_f16<?>";
+                                "gemm_glds_dma_only", "gemm_glds_compute_only", "gemm_lc<256,192,8+4>", "gemm_lc_dma_only",
+                                "gemm_lc_compute_only"};
+  return (c >= 0 && c < 20) ? names[c] : "gemm_f16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
@@ -864,9 +868,10 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
   }
   const int cfg = gemm_config(a);
   if (cfg == 13 || cfg == 14) return launch_gemm_ring(a, s, cfg - 12);  // measurement builds (garbage out)
+  if (cfg >= 17 && cfg <= 19) return launch_gemm_lc(a, s, cfg - 17);
   if (cfg == 15) return run_glds<256, 192, 4, 2, true, 1>(a, s);
   if (cfg == 16) return run_glds<256, 192, 4, 2, true, 2>(a, s);
-  if (cfg == 12 || (a.ring && (cfg == 10 || cfg == 11 || cfg == 5) && gemm_ring_ok(a))) return launch_gemm_ring(a, s);
+  if (cfg == 12) return launch_gemm_ring(a, s);
   switch (cfg) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);

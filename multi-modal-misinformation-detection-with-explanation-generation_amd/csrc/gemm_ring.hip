@@ -266,12 +266,179 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g, int tiles
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Loader / consumer split (gemm_lc_kernel).  Measured on the two kernels above (tools/gemm_bench.py,
+// measurement configs 13-16): the LDS-DMA fill of a 256 x 192 tile runs at ~52 GB/s per CU
+// (DMA-only: 1.07 us per 64-deep K-step of 56 KB, full 128-B lines; 64-B half lines cost 12 %
+// more), the fragment reads + MFMAs alone at 0.86 us -- and the full kernels take 1.42 us (two
+// stages) / 1.70 us (ring): fill and compute ADD UP, because a wave that issues LDS-DMA pieces
+// stalls on their issue and every wave of the workgroup issues them.  Here 4 dedicated loader
+// waves issue every piece and the 8 MFMA waves never touch the vector-memory queue in the K loop:
+//  * 768 threads: waves 0-7 compute (4 x 2, wave tile 64 x 96), waves 8-11 load (14 pieces of
+//    8 rows x 128 B each per stage, full lines, XOR-swizzled on the source address as gemm.hip);
+//  * two 56-KB stages (BK = 64); per step the loaders issue stage k+1, wait for their own DMA
+//    (vmcnt(0)) and meet the compute waves at ONE barrier, after which stage k+1 has landed and
+//    stage k's slot is free -- fill of k+1 runs entirely under the MFMAs of k;
+//  * the tile's bias is one more piece (loader wave 11, with the tile's first stage), so the
+//    compute waves' only vector-memory ops are their epilogue stores, issued after the barrier.
+// Accumulation order per element (32-deep chunks, ascending K) is the one of gemm_glds_kernel:
+// bit-identical results.
+// ---------------------------------------------------------------------------------------------
+constexpr int LBK = 64, kLcStage = (RBM + RBN) * LBK;  // halfs per stage (56 KB)
+constexpr int kLcLoaders = 4, kLcPieces = (RBM + RBN) / 8, kLcPerLoader = kLcPieces / kLcLoaders;
+static_assert(kLcPieces % kLcLoaders == 0, "pieces split evenly over the loader waves");
+typedef __attribute__((address_space(3))) void lds_void;
+
+MMF_DEV int lswz(int row, int kc) { return row * LBK + ((kc ^ (row & 7)) << 3); }
+
+template <int ACT, int DBG = 0>
+__global__ __launch_bounds__(768, 3) void gemm_lc_kernel(GemmArgs g, int tilesN, int tiles) {
+  __shared__ __attribute__((aligned(16))) f16_t lds[2 * kLcStage + 2 * 256];  // + bias[2][256] fp32 (as halfs)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  if (wgid >= tiles) return;
+  const int my_tiles = (tiles - wgid + nwg - 1) / nwg;
+  const int nk = g.K / LBK;
+  const int G = my_tiles * nk;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = g.M, N = g.N;
+  float* bias_lds = reinterpret_cast<float*>(lds + 2 * kLcStage);
+
+  if (wave >= 8) {  // ---------------- loaders
+    const int li = wave - 8;
+    const int prow = lane >> 3, pc = (lane & 7) ^ prow;  // row within a piece, source 16-B chunk
+    auto stage = [&](int gs) {
+      if constexpr (DBG == 2) return;
+      const int i = gs / nk, kt = gs - i * nk;
+      const int t = wgid + i * nwg, tm = t / tilesN, tn = t - tm * tilesN;
+      const int m0 = tm * RBM, n0 = tn * RBN, k0 = kt * LBK;
+      f16_t* base = lds + (gs & 1) * kLcStage;
+#pragma unroll
+      for (int j = 0; j < kLcPerLoader; ++j) {
+        const int p = li + kLcLoaders * j;
+        const f16_t* src;
+        if (p < RBM / 8) {
+          const int gm = min(m0 + 8 * p + prow, M - 1);
+          src = g.A + (size_t)gm * g.lda + k0 + pc * 8;
+        } else {
+          const int gn = min(n0 + 8 * (p - RBM / 8) + prow, N - 1);
+          src = g.W + (size_t)gn * g.ldw + k0 + pc * 8;
+        }
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + p * 512), 16, 0, 0);
+      }
+      if (kt == 0 && li == kLcLoaders - 1)  // 256 bias floats (192 used; clamped source, N % 4 == 0)
+        __builtin_amdgcn_global_load_lds((const void*)(g.bias + min(n0 + lane * 4, N - 4)),
+                                         (lds_void*)(bias_lds + (i & 1) * 256), 16, 0, 0);
+    };
+    stage(0);
+    __syncthreads();
+#pragma unroll 1
+    for (int gs = 0; gs < G; ++gs) {
+      if (gs + 1 < G) stage(gs + 1);
+      __syncthreads();  // vmcnt(0) (own DMAs landed) + barrier
+    }
+    return;
+  }
+
+  // ---------------- MFMA waves
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const uint32_t out_elems = (uint32_t)(M - 1) * g.ldc + N;
+  const rsrc_t rc16 = make_rsrc(g.c16, out_elems * 2u);
+  f32x4 acc[RNI][RMI];
+#pragma unroll
+  for (int i = 0; i < RNI; ++i)
+#pragma unroll
+    for (int j = 0; j < RMI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // stage 0 landed
+  int gs = 0;
+#pragma unroll 1
+  for (int i = 0; i < my_tiles; ++i) {
+    const int t = wgid + i * nwg, tm = t / tilesN, tn = t - tm * tilesN;
+    const int m0 = tm * RBM, n0 = tn * RBN;
+#pragma unroll 1
+    for (int kt = 0; kt < nk; ++kt, ++gs) {
+      const f16_t* xs = lds + (gs & 1) * kLcStage;
+      const f16_t* ws = xs + RBM * LBK;
+#pragma unroll
+      for (int ks = 0; ks < (DBG == 1 ? 0 : 2); ++ks) {
+        f16x8 wf[RNI], xf[RMI];
+#pragma unroll
+        for (int ii = 0; ii < RNI; ++ii)
+          wf[ii] = as_f16x8(*reinterpret_cast<const uint4*>(ws + lswz(wn * RTN + ii * 16 + fr, ks * 4 + fg)));
+#pragma unroll
+        for (int j = 0; j < RMI; ++j)
+          xf[j] = as_f16x8(*reinterpret_cast<const uint4*>(xs + lswz(wm * RTM + j * 16 + fr, ks * 4 + fg)));
+#pragma unroll
+        for (int ii = 0; ii < RNI; ++ii)
+#pragma unroll
+          for (int j = 0; j < RMI; ++j) acc[ii][j] = mfma16x16x32(wf[ii], xf[j], acc[ii][j]);
+      }
+      __syncthreads();  // stage gs + 1 landed; stage gs's slot may be refilled
+    }
+    // epilogue (after the barrier: the loaders already fill the next tile's stages)
+    const float* bias_l = bias_lds + (i & 1) * 256;
+#pragma unroll
+    for (int j = 0; j < RMI; ++j) {
+      const uint32_t m = m0 + wm * RTM + j * 16 + fr;
+#pragma unroll
+      for (int ii = 0; ii < RNI; ii += 2) {
+        uint2 pk[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const float4 bi = *reinterpret_cast<const float4*>(bias_l + wn * RTN + (ii + h2) * 16 + fg * 4);
+          float v[4] = {acc[ii + h2][j][0] + bi.x, acc[ii + h2][j][1] + bi.y, acc[ii + h2][j][2] + bi.z,
+                        acc[ii + h2][j][3] + bi.w};
+          if (ACT != ACT_NONE) act4<ACT>(v);
+          pk[h2] = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
+        }
+        const bool odd = fg & 1;
+        const int n8 = n0 + wn * RTN + (odd ? (ii + 1) * 16 + (fg - 1) * 4 : ii * 16 + fg * 4);
+        buf_store_u4(rc16, n8 < N ? (m * (uint32_t)g.ldc + n8) * 2u : kOOB, pair_rows16(pk[0], pk[1]));
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < RNI; ++ii)
+#pragma unroll
+      for (int j = 0; j < RMI; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 }  // namespace
 
 bool gemm_ring_ok(const GemmArgs& a) {
   const size_t lim = (size_t)1 << 31;
   return a.epi == 0 && !a.ascale && !a.res32 && !a.res16 && !a.c32 && a.c16 && a.bias && (a.K % 64) == 0 &&
          a.K >= 128 && (a.N % 8) == 0 && a.N >= 8 && a.M > 0 && (size_t)(a.M + RBM) * a.ldc * 2 < lim;
+}
+
+hipError_t launch_gemm_lc(const GemmArgs& a, hipStream_t s, int dbg) {
+  if (!gemm_ring_ok(a)) return hipErrorInvalidValue;
+  const int tilesM = (a.M + RBM - 1) / RBM, tilesN = (a.N + RBN - 1) / RBN;
+  const int tiles = tilesM * tilesN;
+  const int grid = tiles < 256 ? tiles : 256;
+  if (dbg == 1 || dbg == 2) {
+    if (dbg == 1) hipLaunchKernelGGL((gemm_lc_kernel<ACT_NONE, 1>), dim3(grid), dim3(768), 0, s, a, tilesN, tiles);
+    else hipLaunchKernelGGL((gemm_lc_kernel<ACT_NONE, 2>), dim3(grid), dim3(768), 0, s, a, tilesN, tiles);
+    return hipGetLastError();
+  }
+#define MMF_LC_CASE(ACT)                                                                                   \
+  case ACT:                                                                                                \
+    hipLaunchKernelGGL((gemm_lc_kernel<ACT>), dim3(grid), dim3(768), 0, s, a, tilesN, tiles);                \
+    break;
+  switch (a.act) {
+    MMF_LC_CASE(ACT_NONE)
+    MMF_LC_CASE(ACT_GELU)
+    MMF_LC_CASE(ACT_QUICK_GELU)
+    MMF_LC_CASE(ACT_SILU)
+    MMF_LC_CASE(ACT_RELU)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef MMF_LC_CASE
+  return hipGetLastError();
 }
 
 hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s, int dbg) {

@@ -48,6 +48,7 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 // K % 64 == 0, N % 8 == 0
 bool gemm_ring_ok(const GemmArgs& a);
 hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s, int dbg = 0);
+hipError_t launch_gemm_lc(const GemmArgs& a, hipStream_t s, int dbg = 0);  // loader / consumer waves (same conditions)
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
 const char* gemm_config_name(int c);
 // streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable

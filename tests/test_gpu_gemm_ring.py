@@ -1,4 +1,4 @@
-"""The ring-pipelined encoder GEMM (csrc/gemm_ring.hip) against the two-stage LDS-DMA kernel it
+"""The pipelined encoder GEMMs of csrc/gemm_ring.hip (ring, loader / consumer) against the two-stage LDS-DMA kernel it
 replaces and against a torch fp32 reference of the same op (C = act(A W^T + b), fp16 in / out,
 fp32 accumulation).
 
@@ -28,8 +28,9 @@ def _run(lib, hip, A, W, bias, M, N, K, act, cfg):
     return C
 
 
+@pytest.mark.parametrize("cfg", [12, 17])  # 12 ring, 17 loader / consumer waves
 @pytest.mark.parametrize("M,N,K,act", SHAPES)
-def test_ring_matches_two_stage_bitwise(M, N, K, act):
+def test_ring_matches_two_stage_bitwise(M, N, K, act, cfg):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import mmf_amd.hip as hip
@@ -39,7 +40,7 @@ def test_ring_matches_two_stage_bitwise(M, N, K, act):
     W = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) * 0.05).to(torch.float16)
     bias = torch.randn(N, device="cuda", generator=g)
     try:
-        ring = _run(lib, hip, A, W, bias, M, N, K, act, 12)
+        ring = _run(lib, hip, A, W, bias, M, N, K, act, cfg)
         ref_cfg = 10 if K >= 192 else 6  # the pipelined two-stage kernel needs >= 3 K-steps of 64
         base = _run(lib, hip, A, W, bias, M, N, K, act, ref_cfg)
     finally:
