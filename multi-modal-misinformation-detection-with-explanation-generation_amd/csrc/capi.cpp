@@ -132,6 +132,7 @@ struct Options {
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
   int dw_v2 = 0;        // depthwise phases with one channel group per wave, weights in SGPRs (effnet.hip)
   int gemm_ring = 0;    // plain fp16-output encoder GEMMs on the loader / consumer kernel (gemm_ring.hip)
+  int pw32_mfma = 1;    // fp32 tower's 1x1 convs on the fp32-input MFMA (1) or the fp32-FMA VALU kernel (0)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -142,6 +143,7 @@ const OptName kOptNames[] = {
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
     {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},            {"gemm_ring", &Options::gemm_ring, "MMF_GEMM_RING"},
+    {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -742,7 +744,8 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   }
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = h->r_layers[i];
-    GemmArgs g = gemm_args(w.r_xb, 768, Ly.qkv, M);
+    // (M <= 512, a single text or a few: split-K through the workspace, gemm_splitk_factor)
+    GemmArgs g = with_ws(gemm_args(w.r_xb, 768, Ly.qkv, M), w.sk_text, w.sk_elems);
     g.c16 = w.r_qkv;
     CHK(gemm(h, g, s));
     CHK(attn(h, w.r_qkv, 2304, mask, w.r_ctx, 768, B, L, 12, 0, s));
@@ -753,16 +756,16 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       // out-proj and FFN-2 write their fp16 branch output y; the residual add happens in fp32
       // inside add+LN (y lives in r_h, free until FFN-1, then in r_ctx, free after out-proj)
       f16_t* y = w.r_h;
-      g = gemm_args(w.r_ctx, 768, Ly.o, M);
+      g = with_ws(gemm_args(w.r_ctx, 768, Ly.o, M), w.sk_text, w.sk_elems);
       g.c16 = y;
       CHK(gemm(h, g, s));
       CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln1, M, s));
-      g = gemm_args(w.r_xb, 768, Ly.fc1, M);
+      g = with_ws(gemm_args(w.r_xb, 768, Ly.fc1, M), w.sk_text, w.sk_elems);
       g.act = 1;  // GELU-erf
       g.c16 = w.r_h;
       CHK(gemm(h, g, s));
       y = w.r_ctx;
-      g = gemm_args(w.r_h, 3072, Ly.fc2, M);
+      g = with_ws(gemm_args(w.r_h, 3072, Ly.fc2, M), w.sk_text, w.sk_elems);
       g.c16 = y;
       CHK(gemm(h, g, s));
       CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln2, M, s));
@@ -802,7 +805,13 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
 // into compact buffers (xc fp32, ctxc fp16); on return xc holds them (before the final LN).
 // independent of the batch size: rows must not change with the batch they run in (the lazy and
 // materialised LayerNorms round differently), so sharding rows over GPUs keeps results bit-identical
-bool clip_lazy(mmf_handle* h, int /*M*/) { return h->opt.lazy_ln && h->opt.clip_res16; }
+// The exception is the latency regime: below kLazyMinRows rows (a ViT batch of <= 5 images, a text
+// batch of <= 3 captions: analyze() one pair at a time) the 256-row lazy-LN tiles leave all but a
+// few CUs idle (4-12 workgroups walking K = 768-3072: 20-37 us per GEMM at B = 1), so those batches
+// run the materialised LayerNorms with split-K GEMMs; rows of batches >= 8 (the bench, shards) stay
+// bit-identical across batch sizes (tests/test_gpu_parity.py), small batches match them to rounding.
+constexpr int kLazyMinRows = 256;
+bool clip_lazy(mmf_handle* h, int M) { return h->opt.lazy_ln && h->opt.clip_res16 && M >= kLazyMinRows; }
 
 int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, f16_t* xb, f16_t* qkv,
                      f16_t* ctx, f16_t* hid, const int32_t* mask, int causal, int B, int L,
@@ -817,7 +826,8 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
   int sti = 0;
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = layers[i];
-    GemmArgs g = lazy ? ln_consumer(x16, H, Ly.qkv_f, Ly.qkv_u, cur, M) : gemm_args(xb, H, Ly.qkv, M);
+    GemmArgs g = lazy ? ln_consumer(x16, H, Ly.qkv_f, Ly.qkv_u, cur, M)
+                      : with_ws(gemm_args(xb, H, Ly.qkv, M), skws, sk_elems);
     g.c16 = qkv;
     CHK(gemm(h, g, s));
     CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
@@ -854,16 +864,17 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
     }
     // out-proj / FFN-2 write their fp16 branch output y (out-proj into `hid`, free until FFN-1;
     // FFN-2 into `ctx`, free after out-proj); add+LN adds it to the fp32 residual stream x in place
-    g = gemm_args(ctx, H, Ly.o, M);
+    // (skinny M <= 512: split-K through the tower's workspace, gemm_splitk_factor)
+    g = with_ws(gemm_args(ctx, H, Ly.o, M), skws, sk_elems);
     g.c16 = hid;
     CHK(gemm(h, g, s));
     CHK(x16 ? add_ln(h, x16, H, hid, H, Ly.ln2, xb, H, M, H, s)
             : add_ln(h, x, H, hid, H, Ly.ln2, x, nullptr, xb, H, M, H, s));
-    g = gemm_args(xb, H, Ly.fc1, M);
+    g = with_ws(gemm_args(xb, H, Ly.fc1, M), skws, sk_elems);
     g.act = 2;  // quick_gelu
     g.c16 = hid;
     CHK(gemm(h, g, s));
-    g = gemm_args(hid, I, Ly.fc2, M);
+    g = with_ws(gemm_args(hid, I, Ly.fc2, M), skws, sk_elems);
     g.c16 = ctx;
     CHK(gemm(h, g, s));
     // layer i + 1 < 12 always holds here (layer 11 takes the compact branch above)
@@ -980,7 +991,8 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
     const float* src = cur;
     if (b.expand != 1) {
       ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * b.cin * b.cexp, 4.0 * B * H * W * (b.cin + b.cexp));
-      HIPCHK(launch_pw32(cur, b.e.w32, b.e.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, b.cexp, b.cin, 3 /* SiLU */, s));
+      HIPCHK(launch_pw32(cur, b.e.w32, b.e.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, b.cexp, b.cin, 3 /* SiLU */, s,
+                             h->opt.pw32_mfma));
       src = w.e32_exp;
     }
     {
@@ -999,7 +1011,7 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
       ProfScope ps(h, s, PK_PW32, 2.0 * B * Ho * Wo * b.cexp * b.cout,
                    4.0 * B * Ho * Wo * (b.cexp + b.cout * (b.residual ? 2 : 1)));
       HIPCHK(launch_pw32(w.e32_dw, b.p.w32, b.p.b, w.e_scale, Ho * Wo, b.residual ? cur : nullptr, nxt, B * Ho * Wo,
-                         b.cout, b.cexp, 0, s));
+                         b.cout, b.cexp, 0, s, h->opt.pw32_mfma));
     }
     std::swap(cur, nxt);
     H = Ho;
@@ -1007,7 +1019,8 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
   }
   {
     ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * 320 * 1280, 4.0 * B * H * W * (320 + 1280));
-    HIPCHK(launch_pw32(cur, h->e_head.w32, h->e_head.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, 1280, 320, 3, s));
+    HIPCHK(launch_pw32(cur, h->e_head.w32, h->e_head.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, 1280, 320, 3, s,
+                       h->opt.pw32_mfma));
   }
   ProfScope ps(h, s, PK_GAP, (double)B * H * W * 1280 + 4.0 * B * 1280, (double)B * H * W * 1280 * 4);
   HIPCHK(launch_gap32(w.e32_exp, H * W, 1280, h->e_cls_w, h->e_cls_b, logits, score, score_stride, B, s));
@@ -1227,7 +1240,9 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
       CHK(A((void**)&w.t_st[i], stats_rows(Mt)));
     }
   }
-  w.sk_elems = (size_t)B * 9216;  // max over the compact layers of (K / 256) * N
+  // max over the skinny-M GEMMs (compact last layers: B rows; whole encoders of small batches: up to
+  // the 512 rows gemm_config sends to the split-K path) of (K / 256) * N = 9216 per row
+  w.sk_elems = (size_t)std::max(B, 512) * 9216;
   CHK(A((void**)&w.sk_text, w.sk_elems * 4));
   CHK(A((void**)&w.sk_vit, w.sk_elems * 4));
   CHK(A((void**)&w.sk_ctext, w.sk_elems * 4));

@@ -79,6 +79,106 @@ __global__ __launch_bounds__(256) void pw32_kernel(const float* __restrict__ A, 
   }
 }
 
+// The same contraction on the fp32-input MFMA (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fp32
+// fmaf chain, cdna_hip_programming.md §3) -- BIT-IDENTICAL to pw32_kernel (products in ascending k
+// from a zero accumulator, then bias / activation / residual in the same order) at the f32 MFMA rate
+// instead of an LDS-read-bound VALU loop.  64 x 64 tile, 4 waves of 32 x 32 (2 x 2 MFMA blocks),
+// K in chunks of 16 staged through LDS (double buffer, register-staged global loads).  The chunk is
+// stored k-transposed ([row][g][s] = A[row][4 s + g]) so a lane of group g reads its four MFMA
+// steps' operands (k = g, 4 + g, 8 + g, 12 + g) with ONE ds_read_b128, and step s covers
+// k = 4 s .. 4 s + 3 in lane-group order: the chain runs in ascending k.  Operands are swapped
+// (W rows are the MFMA's A operand) so each lane ends with 4 consecutive output columns.
+constexpr int QB = 64, QK = 16;
+// float offset of (row, lane group g) in a [QB][QK] chunk; chunk ^= 2 * bit3(row) makes the
+// 16-lane ds_read_b128 groups conflict-free (the 64-B-row swizzle of gemm_ring.hip)
+MMF_DEV int q_off(int row, int g) { return row * QK + ((g ^ (((row >> 3) & 1) << 1)) << 2); }
+
+__global__ __launch_bounds__(256) void pw32m_kernel(const float* __restrict__ A, const float* __restrict__ Wt,
+                                                    const float* __restrict__ bias, const float* __restrict__ ascale,
+                                                    int rows_per_image, const float* __restrict__ res,
+                                                    float* __restrict__ C, int M, int N, int K, int act) {
+  __shared__ __attribute__((aligned(16))) float As[2][QB * QK];
+  __shared__ __attribute__((aligned(16))) float Ws[2][QB * QK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fg = lane >> 4;
+  const int m0 = blockIdx.x * QB, n0 = blockIdx.y * QB;
+  // loader: thread -> (row lr, k quad lc) of the 64 x 16 chunk
+  const int lr = tid >> 2, lc = tid & 3;
+  const int am = m0 + lr, wr = n0 + lr;
+  const float* sc = (ascale && am < M) ? ascale + (size_t)(am / rows_per_image) * K : nullptr;
+  auto gload = [&](int k0, float4& a, float4& w) {
+    const int k = k0 + lc * 4;  // K % 4 == 0: a quad is in or out whole
+    a = make_float4(0.f, 0.f, 0.f, 0.f);
+    w = a;
+    if (am < M && k < K) {
+      a = *reinterpret_cast<const float4*>(A + (size_t)am * K + k);
+      if (sc) {
+        const float4 s4 = *reinterpret_cast<const float4*>(sc + k);
+        a.x *= s4.x; a.y *= s4.y; a.z *= s4.z; a.w *= s4.w;
+      }
+    }
+    if (wr < N && k < K) w = *reinterpret_cast<const float4*>(Wt + (size_t)wr * K + k);
+  };
+  auto lstore = [&](int buf, const float4& a, const float4& w) {  // k = 4 lc + e -> [lr][g = e][s = lc]
+    const float av[4] = {a.x, a.y, a.z, a.w}, wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      As[buf][q_off(lr, e) + lc] = av[e];
+      Ws[buf][q_off(lr, e) + lc] = wv[e];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 a, w;
+  gload(0, a, w);
+  lstore(0, a, w);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += QK) {
+    const bool more = k0 + QK < K;
+    if (more) gload(k0 + QK, a, w);
+    float4 wf[2], xf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) wf[i] = *reinterpret_cast<const float4*>(&Ws[buf][q_off(wn * 32 + i * 16 + fr, fg)]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) xf[j] = *reinterpret_cast<const float4*>(&As[buf][q_off(wm * 32 + j * 16 + fr, fg)]);
+    const float wfs[2][4] = {{wf[0].x, wf[0].y, wf[0].z, wf[0].w}, {wf[1].x, wf[1].y, wf[1].z, wf[1].w}};
+    const float xfs[2][4] = {{xf[0].x, xf[0].y, xf[0].z, xf[0].w}, {xf[1].x, xf[1].y, xf[1].z, xf[1].w}};
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wfs[i][st], xfs[j][st], acc[i][j], 0, 0, 0);
+    if (more) lstore(buf ^ 1, a, w);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // lane: C[m][n .. n + 3] of each 16 x 16 block (operands swapped)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = m0 + wm * 32 + j * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = n0 + wn * 32 + i * 16 + fg * 4;
+      if (n >= N) continue;  // N % 4 == 0
+      const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+      float o[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act_precise(o[e], act);
+      if (res) {
+        const float4 r = *reinterpret_cast<const float4*>(res + (size_t)m * N + n);
+        o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
+      }
+      *reinterpret_cast<float4*>(C + (size_t)m * N + n) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 // torchvision pads (k - 1) / 2 on every side; output edge (H - 1) / S + 1
 template <int K, int S>
 __global__ __launch_bounds__(256) void dw32_kernel(const float* __restrict__ in, const float* __restrict__ w,
@@ -163,10 +263,15 @@ __global__ __launch_bounds__(256) void gap32_kernel(const float* __restrict__ x,
 }  // namespace
 
 hipError_t launch_pw32(const float* A, const float* W, const float* bias, const float* ascale, int rows_per_image,
-                       const float* res, float* C, int M, int N, int K, int act, hipStream_t s) {
+                       const float* res, float* C, int M, int N, int K, int act, hipStream_t s, int mfma) {
   if (M <= 0 || N <= 0 || K <= 0 || (N % 4) || (K % 4) || (ascale && rows_per_image <= 0) ||
       (act != ACT_NONE && act != ACT_SILU))
     return hipErrorInvalidValue;
+  if (mfma) {
+    const dim3 grid((M + QB - 1) / QB, (N + QB - 1) / QB);
+    hipLaunchKernelGGL(pw32m_kernel, grid, dim3(256), 0, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act);
+    return hipGetLastError();
+  }
   const dim3 grid((M + PB - 1) / PB, (N + PB - 1) / PB);
   hipLaunchKernelGGL(pw32_kernel, grid, dim3(256), 0, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act);
   return hipGetLastError();

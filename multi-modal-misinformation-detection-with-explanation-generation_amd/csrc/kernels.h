@@ -179,7 +179,7 @@ hipError_t launch_effnet_stem32(const uint8_t* img, const float* x_nchw, const f
                                 float* out, int B, hipStream_t s);
 // C[M][N] = act((A .* ascale[m / rows_per_image]) W^T + bias) (+ res); W fp32 [N][K]; N, K % 4 == 0
 hipError_t launch_pw32(const float* A, const float* W, const float* bias, const float* ascale, int rows_per_image,
-                       const float* res, float* C, int M, int N, int K, int act, hipStream_t s);
+                       const float* res, float* C, int M, int N, int K, int act, hipStream_t s, int mfma = 1);
 // w tap-major [k*k][C]
 hipError_t launch_dw32(const float* in, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                        int k, int stride, hipStream_t s);

@@ -63,6 +63,28 @@ def test_effnet_fp32_tower_vs_golden(engine, golden, golden_inputs):
     np.testing.assert_allclose(sc.cpu().numpy(), _sm1(golden["effnet_logits"]), atol=1e-5)
 
 
+def test_fp32_tower_mfma_pointwise_bit_identical(det_sd, clip_sd):
+    """The fp32 tower's 1x1 convolutions on the fp32-input MFMA (option pw32_mfma = 1, default:
+    v_mfma_f32_16x16x4_f32 is a k-ordered fp32 fmaf chain) against the fp32-FMA VALU kernel
+    (pw32_mfma = 0): every logit bit-identical, on the ill-conditioned He draw the mode exists for."""
+    import mmf_amd.synthetic as syn
+    import mmf_amd.weights as W
+    from mmf_amd.engine import Engine
+    eng = Engine(0, W.synthetic_detector_state(0, effnet_gain=2 ** 0.5), None, max_batch=64)
+    try:
+        eng.set_option("effnet_fp32", 1)
+        imgs = syn.images(64, 29)
+        eng.set_option("pw32_mfma", 0)
+        lg0, _ = eng.effnet_forward(imgs)
+        eng.set_option("pw32_mfma", 1)
+        lg1, _ = eng.effnet_forward(imgs)
+        torch.cuda.synchronize()
+        assert torch.isfinite(lg1).all()
+        assert torch.equal(lg0, lg1), (lg0 - lg1).abs().max().item()
+    finally:
+        eng.close()
+
+
 def test_clip_embeddings(engine, golden, golden_inputs):
     ie = engine.clip_image(golden_inputs["imgs"]).cpu().numpy()
     te = engine.clip_text(golden["clip_ids"], golden["clip_mask"]).cpu().numpy()
