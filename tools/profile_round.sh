@@ -12,9 +12,9 @@ mkdir -p $OUT
 export MMF_CONCURRENT=0
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/trace -o run -- \
-  python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-configs > $OUT/bench_trace.log 2>&1
+  python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-configs --no-per-sample > $OUT/bench_trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch -o run -- \
-  python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-configs > $OUT/bench_fetch.log 2>&1
+  python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-configs --no-per-sample > $OUT/bench_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write -o run -- \
-  python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-configs > $OUT/bench_write.log 2>&1
+  python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-configs --no-per-sample > $OUT/bench_write.log 2>&1
 echo done > $OUT/ok
