@@ -60,10 +60,11 @@ def kind_symbol(kind: str) -> str:
         return kind
     dims = m.group(2).split(",")
     epi = m.group(4) or "0"
+    # (the last template argument is the measurement-build selector DBG, 0 in production)
     if m.group(1) == "glds":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi, '0'])}>"
     if m.group(1) == "glds_pipe2":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi, '0'])}>"
     return f"gemm_f16_kernel<{', '.join(dims)}>"
 
 
