@@ -45,8 +45,7 @@ def _pil(gi, i):
 
 def _check(got, ref, tol=TOL):
     for k, v in ref["scores"].items():  # scores first: their message names the signal that moved
-        t = 2e-3 if k == "text_similarity" else tol
-        assert abs(got["scores"][k] - v) < t, (k, got["scores"][k], v)
+        assert abs(got["scores"][k] - v) < tol, (k, got["scores"][k], v)
     assert got["verdict"] == ref["verdict"] and got["verdict_text"] == ref["verdict_text"]
     assert abs(got["confidence"] - ref["confidence"]) < tol
     assert [m["title"] for m in got["vault_matches"]] == [m["title"] for m in ref["vault_matches"]]
@@ -216,7 +215,7 @@ def test_analyze_video_matches_reference(forensics, golden, golden_json, golden_
                                           max_frames=c["max_frames"], stride_seconds=c["stride_seconds"])
             for k in ("deepfake_score", "clip_similarity", "vault_discrepancy"):
                 assert abs(got[k] - ref[k]) < TOL, (c, k, got[k], ref[k])
-            assert abs(got["text_similarity"] - ref["text_similarity"]) < 2e-3
+            assert abs(got["text_similarity"] - ref["text_similarity"]) < TOL
             assert [m["title"] for m in got["vault_matches"]] == [m["title"] for m in ref["vault_matches"]]
             for a, b in zip(got["vault_matches"], ref["vault_matches"]):
                 assert abs(a["similarity"] - b["similarity"]) < TOL

@@ -132,9 +132,8 @@ def test_analyze_batch_vs_golden(engine, golden, golden_inputs):
     np.testing.assert_array_equal(o["verdict"], (golden["fusion_probs"][:, 1] > 0.5).astype(np.int32))
     np.testing.assert_array_equal(o["top_idx"], golden["vault_top_idx"])
     np.testing.assert_allclose(o["top_sims"], golden["vault_top_sim"], atol=TOL)
-    # text_similarity (misinfo_forensics.py:467-484) is a cosine between two separately fp16-computed
-    # CLIP text embeddings and is NOT one of the five fusion inputs (quirk Q7): 2e-3 bound.
-    np.testing.assert_allclose(o["text_similarity"], golden["text_similarity"], atol=2e-3)
+    # text_similarity (misinfo_forensics.py:467-484, not a fusion input: quirk Q7) at the same bar
+    np.testing.assert_allclose(o["text_similarity"], golden["text_similarity"], atol=TOL)
 
 
 def test_fusion_config1(engine, golden):
