@@ -151,3 +151,21 @@ def test_video_frame_sampling_matches_reference():
         sys.modules.pop("cv2", None)
         if saved is not None:
             sys.modules["cv2"] = saved
+
+
+def test_fingerprint_sees_dtype_round_trip():
+    """.half() then .float() re-creates every tensor without bumping a version counter
+    and could land on the packed state's old addresses.  The detector holds the storages of its
+    last packed state, so the round trip always reads as stale (-> re-packed before the next call)."""
+    from mmf_amd.api import MultiModalMisinfoDetector, ALL_COMPONENTS
+    det = MultiModalMisinfoDetector()
+    for c in ALL_COMPONENTS:  # what sync() records after packing a component
+        det._synced[c] = det._fingerprint(c)
+        det._held[c] = [t.untyped_storage() for t in det._tensors[c]]
+    assert det.stale_components() == []
+    det.fusion_layer.half()
+    det.fusion_layer.float()
+    assert det.stale_components() == ["fusion"]
+    with torch.no_grad():
+        det.ai_head[0].bias.add_(1.0)  # in place: version counter
+    assert det.stale_components() == ["text", "fusion"]
