@@ -133,6 +133,7 @@ struct Options {
   int dw_v2 = 0;        // depthwise phases with one channel group per wave, weights in SGPRs (effnet.hip)
   int gemm_ring = 0;    // plain fp16-output encoder GEMMs on the loader / consumer kernel (gemm_ring.hip)
   int pw32_mfma = 1;    // fp32 tower's 1x1 convs on the fp32-input MFMA (1) or the fp32-FMA VALU kernel (0)
+  int gemm_wide = 0;    // 256x384 tiles where they save a persistent round (gemm.hip glds_pick; step A/B: a tie)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -143,7 +144,7 @@ const OptName kOptNames[] = {
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
     {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},            {"gemm_ring", &Options::gemm_ring, "MMF_GEMM_RING"},
-    {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},
+    {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -163,6 +164,7 @@ void apply_options(const Options& o, GemmArgs* g) {
   g->group_m = o.gemm_group_m;
   g->prio = o.gemm_prio;
   g->ring = o.gemm_ring;
+  g->wide = o.gemm_wide;
 }
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the

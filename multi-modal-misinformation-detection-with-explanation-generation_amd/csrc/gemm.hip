@@ -22,6 +22,9 @@
 namespace {
 
 constexpr int BK = 64;
+#ifndef WIDE_XD
+#define WIDE_XD 2  // 256x384 tiles: X fragments read ahead of their MFMAs
+#endif
 
 template <int BM, int BN, int WGM, int WGN>
 struct Cfg {
@@ -240,6 +243,25 @@ MMF_DEV void glds_tile(const f16_t* __restrict__ G, int ld, int row0, int rowmax
   }
 }
 
+// The same fill through a buffer descriptor (buffer_load_dwordx4 ... lds): the per-lane part of
+// the source address is ONE loop-invariant VGPR (lane_off: row within the 8-row piece, swizzled
+// chunk), the piece's row base and k0 ride in the scalar soffset.  glds_tile keeps a 64-bit
+// pointer per piece live across the K loop (20 VGPRs for 640 rows), which the 256x384 tiles'
+// accumulators leave no room for.  Full tiles only (soffset is outside the descriptor's range
+// check; the caller takes glds_tile for a ragged last row panel).
+template <int ROWS, int NW>
+MMF_DEV void glds_tile_buf(rsrc_t r, uint32_t row_bytes, int row0, int k0, uint32_t lane_off, f16_t* tile, int wave) {
+  constexpr int PER_WAVE = ROWS / (8 * NW);
+  static_assert(PER_WAVE * 8 * NW == ROWS, "rows must split evenly over the waves");
+#pragma unroll
+  for (int j = 0; j < PER_WAVE; ++j) {
+    const int seg = wave * PER_WAVE + j;
+    const uint32_t soff = (uint32_t)(row0 + seg * 8) * row_bytes + (uint32_t)k0 * 2u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)((__attribute__((address_space(3))) f16_t*)tile + seg * 512),
+                                             16, lane_off, soff, 0, 0);
+  }
+}
+
 // Tile t -> (row panel, column panel).  gm > 0: grouped order -- gm row panels are walked
 // column by column, so the tiles one XCD runs together share A panels and W panels in its L2.
 MMF_DEV void tile_coords(int t, int tilesM, int tilesN, int gm, int& tm, int& tn) {
@@ -281,6 +303,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int STAGE = (BM + BN) * BK;
   static_assert(NW == 8 || NW == 4, "4 or 8 waves");
+  // 256x384 tiles (two stages = all 160 KB of LDS; 192 accumulator registers per lane): the bias
+  // columns are fetched after the K loop and the residual rows without look-ahead, so that neither
+  // is live beside the accumulators
+  constexpr bool WIDE = BN == 384;
+  static_assert(!WIDE || (EPI == 0 && !PIPE2), "256x384 tiles: plain epilogues, one-step K loop");
   __shared__ __attribute__((aligned(16))) f16_t lds[2 * STAGE];
   constexpr bool ROWST = EPI == 1;  // reads row statistics
   static_assert(EPI == 0 || BM == 256, "lazy-LN epilogues assume 256-row tiles");
@@ -314,11 +341,26 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   int t = wgid;
   if (t >= tiles) return;
   if ((g.prio == 1 && wave >= NW / 2) || (g.prio == 2 && wave < NW / 2)) __builtin_amdgcn_s_setprio(1);
+  // WIDE: descriptor fills (glds_tile_buf; the launcher checks the 32-bit byte extents)
+  const rsrc_t ra = make_rsrc(g.A, WIDE ? (uint32_t)M * (uint32_t)g.lda * 2u : 0u);
+  const rsrc_t rw = make_rsrc(g.W, WIDE ? (uint32_t)N * (uint32_t)g.ldw * 2u : 0u);
+  const uint32_t lchunk = (uint32_t)(((lane & 7) ^ (lane >> 3)) * 16);
+  const uint32_t aoff = (uint32_t)(lane >> 3) * (uint32_t)g.lda * 2u + lchunk;
+  const uint32_t woff = (uint32_t)(lane >> 3) * (uint32_t)g.ldw * 2u + lchunk;
   auto stage = [&](int buf, int tile, int kt) {
     if constexpr (DBG == 2) return;
     int tm_, tn_;
     tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);
     f16_t* nb = lds + buf * STAGE;
+    if constexpr (WIDE) {
+      if (tm_ * BM + BM <= M) {  // (N % 384 == 0: every column panel is full)
+        glds_tile_buf<BM, NW>(ra, (uint32_t)g.lda * 2u, tm_ * BM, kt * BK, aoff, nb, wave);
+      } else {
+        glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
+      }
+      glds_tile_buf<BN, NW>(rw, (uint32_t)g.ldw * 2u, tn_ * BN, kt * BK, woff, nb + BM * BK, wave);
+      return;
+    }
     glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
     glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
   };
@@ -356,7 +398,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
 #pragma unroll
       for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     float4 bias_r[ROWST ? 1 : NI];  // this lane's epilogue bias columns, fetched under the K loop
-    if constexpr (!ROWST) {
+    if constexpr (!ROWST && !WIDE) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
     }
@@ -458,6 +500,32 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
 #pragma unroll
           for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(w1[i], x1[j], acc[i][j]);
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (WIDE) {
+        // 256x384 (wave tile 128x96, 192 accumulator registers): the 6 W fragments of a 32-deep
+        // half-step are held, the 8 X fragments stream through two registers sets, one read per
+        // 6 MFMAs (sched_barriers keep hipcc from hoisting all 14 reads, which would spill)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          constexpr int XD = WIDE_XD;  // X fragments in flight
+          f16x8 wf[NI], xf[XD + 1];
+          xf[0] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + fr, ks * 4 + fg)));
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+            wf[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
+#pragma unroll
+          for (int j = 1; j < XD; ++j)
+            xf[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < MI; ++j) {
+            if (j + XD < MI)
+              xf[(j + XD) % (XD + 1)] =
+                  as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + (j + XD) * 16 + fr, ks * 4 + fg)));
+#pragma unroll
+            for (int i = 0; i < NI; ++i) acc[i][j] = mfma16x16x32(wf[i], xf[j % (XD + 1)], acc[i][j]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
       } else if constexpr (BN == 192) {
         // 256x192 (wave tile 64x96): all 20 fragment reads of the K-step first, then its 48 MFMAs,
         // then the barrier -- pinned with sched_barriers (hipcc otherwise interleaves 2 reads +
@@ -502,6 +570,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
       cur ^= 1;
     }
 
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
+    }
     // Epilogue.  The activation is a compile-time parameter (no per-element branch).  All traffic
     // is raw-buffer: out-of-range rows/columns read 0 / drop their stores, so there is no divergent
     // branch and no load that has to wait on the stores issued before it -- bias columns were
@@ -619,10 +691,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
           }
         }
       };
-      load_res(rcur, 0);
+      if constexpr (!WIDE) load_res(rcur, 0);
 #pragma unroll
       for (int j = 0; j < MI; ++j) {
-        if (j + 1 < MI) load_res(rnext, j + 1);
+        if constexpr (WIDE) load_res(rcur, j);
+        else if (j + 1 < MI) load_res(rnext, j + 1);
         const uint32_t m = m0 + wm * TM + j * 16 + fr;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -637,8 +710,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
           if (g.c32) buf_store_f4(rc32, e * 4u, make_float4(v[0], v[1], v[2], v[3]));
           if (g.c16) buf_store_u2(rc16, e * 2u, make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3])));
         }
+        if constexpr (!WIDE) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i) rcur[i] = rnext[i];
+          for (int i = 0; i < NI; ++i) rcur[i] = rnext[i];
+        }
       }
     };
     if (g.res32) epilogue(std::true_type{});
@@ -781,6 +856,12 @@ static bool glds_ok(const GemmArgs& a) {
   return (a.K % BK) == 0 && !a.ascale && rows * a.ldc * 4 < lim && rows * (a.ldr > 0 ? a.ldr : 0) * 4 < lim;
 }
 
+// 256x384 tiles: whole column panels and 32-bit descriptor extents for both operands
+static bool wide_ok(const GemmArgs& a) {
+  const size_t lim = (size_t)1 << 32;
+  return glds_ok(a) && a.N % 384 == 0 && (size_t)a.M * a.lda * 2 < lim && (size_t)a.N * a.ldw * 2 < lim;
+}
+
 static int forced_config(const GemmArgs& a) {
   // handle option "gemm_config" (benchmarking override, tools/gemm_bench.py); ignored if inapplicable
   if (a.force_cfg <= 0) return -1;
@@ -788,7 +869,8 @@ static int forced_config(const GemmArgs& a) {
   if (((c >= 4 && c <= 8) || c >= 10) && !glds_ok(a)) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
   if (((c >= 12 && c <= 14) || c >= 17) && !gemm_ring_ok(a)) return -1;
-  return (c >= 0 && c <= 19) ? c : -1;
+  if (c == 20 && !wide_ok(a)) return -1;
+  return (c >= 0 && c <= 20) ? c : -1;
 }
 
 // persistent 256-row LDS-DMA tiles: the column tile that minimises whole "rounds" of 256 CUs x
@@ -807,6 +889,15 @@ static int glds_pick(const GemmArgs& a, bool with_128) {
     const long tiles = tm * ((a.N + bns[i] - 1) / bns[i]);
     const double c = (double)((tiles + 255) / 256) * bns[i] / eff[i];
     if (c < bc) { bc = c; best = cfg[i]; }
+  }
+  // 256x384 (config 20, plain epilogues): per flop no faster than 256x256 (its fill is exposed:
+  // profiles/r03_gemm_clock_probe.txt) and slower in a single round (no next tile to hide the
+  // first slab and the epilogue under), so it is taken only with >= 2 rounds and when it saves a
+  // round: RoBERTa QKV (N = 2304: 3 rounds instead of 4.5) +11-15 % isolated
+  if (a.wide && a.epi == 0 && wide_ok(a)) {
+    const long tiles = tm * (a.N / 384);
+    const double c = (double)((tiles + 255) / 256) * 384 / 0.97;
+    if (tiles >= 512 && c < bc) best = 20;
   }
   return best;
 }
@@ -854,8 +945,8 @@ const char* gemm_config_name(int c) {
                                 "pw_conv", "gemm_glds_pipe2<256,192,4,2>", "gemm_glds_pipe2<256,256,2,4>",
                                 "gemm_ring<256,192,4,2>", "gemm_ring_dma_only", "gemm_ring_compute_only",
                                 "gemm_glds_dma_only", "gemm_glds_compute_only", "gemm_lc<256,192,8+4>", "gemm_lc_dma_only",
-                                "gemm_lc_compute_only"};
-  return (c >= 0 && c < 20) ? names[c] : "gemm_f16<?>";
+                                "gemm_lc_compute_only", "gemm_glds<256,384,2,4>"};
+  return (c >= 0 && c < 21) ? names[c] : "gemm_f16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
@@ -888,6 +979,7 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
     case 9: return launch_pw(a, s);
     case 10: return run_glds<256, 192, 4, 2, true>(a, s);
     case 11: return run_glds<256, 256, 2, 4, true>(a, s);
+    case 20: return run_glds<256, 384, 2, 4>(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

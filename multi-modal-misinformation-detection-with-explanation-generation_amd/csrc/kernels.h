@@ -24,6 +24,7 @@ struct GemmArgs {
   int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
   int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
   int ring;                      // 1 = plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
+  int wide;                      // 1 = 256x384 tiles may be picked (gemm.hip glds_pick)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
