@@ -654,6 +654,8 @@ class MisinfoForensics:
             return []
 
         def host_stage(a, b):
+            # (tokenising on a third thread while the images decode measured a tie for one chunk and
+            # 33 % slower for four: DESIGN §6)
             rob = io_utils.tokenize_roberta_batch(self.roberta_tokenizer, texts[a:b])
             rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
             cid, cm = self._clip_ids(list(texts[a:b]))

@@ -149,8 +149,19 @@ def tokenize_roberta_batch(tok, texts: List[str]) -> List[List[int]]:
         enc = tok(list(texts), return_tensors="pt", max_length=512, truncation=True, padding=True)
     except (TypeError, KeyError, ValueError):  # a tokenizer object that only takes single strings
         return [tokenize_roberta(tok, t) for t in texts]
-    ids, mask = enc["input_ids"], enc["attention_mask"]
-    return [_to_list(ids[i])[:int(sum(_to_list(mask[i])))] for i in range(len(texts))]
+    return _strip_padded(enc["input_ids"], enc["attention_mask"], len(texts))
+
+
+def _strip_padded(ids, mask, n: int) -> List[List[int]]:
+    """Per-row unpadded id lists of a right-padded batch encoding (one vectorised length count
+    instead of a Python sum per row)."""
+    try:
+        a, m = np.asarray(ids).reshape(n, -1), np.asarray(mask).reshape(n, -1)
+    except ValueError:  # ragged lists (a tokenizer that ignores padding=True): row by row
+        return [_to_list(ids[i])[:int(sum(_to_list(mask[i])))] for i in range(n)]
+    lens = m.sum(axis=1).tolist()
+    rows = a.tolist()
+    return [[int(v) for v in rows[i][:lens[i]]] for i in range(n)]
 
 
 def tokenize_clip(proc, texts: List[str], truncation: bool = False) -> List[List[int]]:
@@ -160,12 +171,7 @@ def tokenize_clip(proc, texts: List[str], truncation: bool = False) -> List[List
     if truncation:
         kw["truncation"] = True
     enc = proc(**kw)
-    ids, mask = enc["input_ids"], enc["attention_mask"]
-    out = []
-    for i in range(len(texts)):
-        n = int(sum(_to_list(mask[i])))
-        out.append(_to_list(ids[i])[:n])
-    return out
+    return _strip_padded(enc["input_ids"], enc["attention_mask"], len(texts))
 
 
 # ---------------------------------------------------------------------------------------------
