@@ -22,6 +22,48 @@ MMF_DEV T* at_bytes(T* base, uint32_t byte_off) {
   return reinterpret_cast<T*>(reinterpret_cast<char*>(const_cast<typename std::remove_const<T>::type*>(base)) + byte_off);
 }
 
+// Diagnostic build only (-DMMF_EFF_STAMP, tools/effnet_stamps.py): per-block phase stamps of the
+// depthwise / fused-front kernels into a buffer of their own (slots [region][block][32]: 0 / 1 =
+// s_memrealtime at start / end, 2.. = s_memtime after each phase, 31 = the number of stamps).  In
+// the production build every EST_* macro is empty.
+#ifdef MMF_EFF_STAMP
+constexpr int kStampBlocks = 16384, kStampSlots = 32;
+__device__ unsigned long long* g_eff_stamp;
+MMF_DEV unsigned long long est_time() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define EST_BEGIN(REGION)                                                                                   \
+  unsigned long long* est_ = nullptr;                                                                        \
+  int est_n_ = 2;                                                                                            \
+  {                                                                                                          \
+    const unsigned est_b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                   \
+    if (g_eff_stamp && est_b < (unsigned)kStampBlocks)                                                       \
+      est_ = g_eff_stamp + ((size_t)(REGION) * kStampBlocks + est_b) * kStampSlots;                         \
+    const unsigned long long est_r = __builtin_amdgcn_s_memrealtime();                                       \
+    const unsigned long long est_t = est_time();                                                             \
+    if (est_ && threadIdx.x == 0) { est_[0] = est_r; est_[2] = est_t; }                                      \
+  }
+#define EST()                                                                                                \
+  {                                                                                                          \
+    const unsigned long long est_t = est_time();                                                             \
+    ++est_n_;                                                                                                \
+    if (est_ && threadIdx.x == 0 && est_n_ < kStampSlots - 1) est_[est_n_] = est_t;                          \
+  }
+#define EST_END()                                                                                            \
+  {                                                                                                          \
+    const unsigned long long est_r = __builtin_amdgcn_s_memrealtime();                                       \
+    if (est_ && threadIdx.x == 0) { est_[1] = est_r; est_[kStampSlots - 1] = (unsigned long long)est_n_; }   \
+  }
+#else
+#define EST_BEGIN(REGION)
+#define EST()
+#define EST_END()
+#endif
+
 // One thread per output pixel, all 32 channels; weights transposed in LDS to [tap][channel] so
 // every tap is 8 broadcast float4 reads.  ToTensor + Normalize folded into one FMA per input.
 // F32 = true: input is an already-normalised fp32 NCHW tensor (detector.forward_image signature,
@@ -294,6 +336,7 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
   float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, TT > 0));  // [K*K][CW]
   float* sb = sw + K * K * CW;                                     // [CW]
   float* red = TT > 0 ? (float*)dw_smem : sb + CW;                 // [PX][CW]
+  EST_BEGIN(8 + ((K == 5) * 2 + (S == 2)) * 4 + (TT == 14 ? 1 : TT == 7 ? 2 : TT == 16 ? 3 : 0))
 
   // ---- input tile (+halo) -> LDS ----
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
@@ -341,9 +384,12 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
   }
   for (int i = tid; i < CW; i += 256) sb[i] = bias[c0 + i];
   __syncthreads();
+  EST()
 
   if constexpr (TT > 0) dw_compute_ct<K, S, TT, CWT, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C);
   else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
+  EST()
+  EST_END()
 }
 
 // MBConv front, fused: 1x1 expand (BN folded) + SiLU computed per input tile on the MFMA, straight
@@ -380,6 +426,7 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
   float* sbe = TT > 0 ? sb + CW : red + (256 / NG) * CW;           // [CW] expand bias
   f16_t* swe = (f16_t*)(sbe + CW);                        // [CW][KP] expand weights (zero-padded K)
 
+  EST_BEGIN((K == 5) * 4 + (S == 2) * 2 + (KS == 2))
   // this wave's input-pixel fragments first: their HBM latency overlaps the weight staging
   constexpr int MAXRF = 6;  // ceil(ceil(IT^2 / 16) / 4) for IT <= 19 (host-checked)
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
@@ -416,6 +463,7 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
       sbe[i] = be[c0 + i];
     }
     __syncthreads();
+    EST()
 
     // ---- expand the input tile (+halo) into LDS ----
 #pragma unroll
@@ -446,10 +494,14 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
       }
     }
     __syncthreads();
+    EST()
     if constexpr (TT > 0) dw_compute_ct<K, S, TT, CW, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C);
     else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
+    EST()
     __syncthreads();  // the next group restages sw / sb / swe / tile and rewrites red
+    EST()
   }
+  EST_END()
 }
 
 // Stem + stage-1 depthwise, fused: the stem (ImageNet normalise -> conv3x3 s2 3->32 + BN + SiLU)
@@ -492,6 +544,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
   const int ty0 = blockIdx.x / 7, tx0 = blockIdx.x - ty0 * 7;
   const int oy0 = ty0 * SD_T, ox0 = tx0 * SD_T;
   const int py0 = 2 * oy0 - 3, px0 = 2 * ox0 - 3;  // image coords of patch (0, 0)
+  EST_BEGIN(24)
 
   // (V1: depthwise weights [C][9] transposed into LDS; V2 reads `wd` as the tap-major [9][C] copy)
   const float wd0 = V2 ? 0.f : wd[(tid % CW) * 9 + tid / CW];
@@ -561,6 +614,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
     if (tid < CW) sb[tid] = bd0;
   }
   __syncthreads();
+  EST()
 
   // ---- stem: 16 tile pixels per MFMA column block ----
   for (int mt = wave; mt < NMT; mt += 4) {
@@ -596,8 +650,11 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
     }
   }
   __syncthreads();
+  EST()
   if constexpr (!V2) {
     dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW);
+    EST()
+    EST_END()
   } else {
     const int g = __builtin_amdgcn_readfirstlane(wave);  // this wave's channel group
     const int oy = lane >> 2, ox = (lane & 3) * 4;       // a run of 4 outputs of one tile row
@@ -786,6 +843,13 @@ __global__ __launch_bounds__(256) void gap_classifier_kernel(const f16_t* x, int
 }
 
 }  // namespace
+
+#ifdef MMF_EFF_STAMP
+// diagnostic build: where the stamping kernels write (nullptr = off)
+extern "C" int mmf_debug_eff_stamp(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_eff_stamp), &buf, sizeof(buf));
+}
+#endif
 
 hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, f16_t* out, int B,
                               hipStream_t s) {
