@@ -403,6 +403,10 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
 //          lane ends with 4 consecutive channels of one pixel -> 8-B LDS writes; pixels outside the
 //          image are written as 0 (the depthwise conv zero-pads E, not X).
 // grid (tiles, Cexp / CW, B); block 256 threads; KS = ceil(Cin / 32) <= 2
+// MMF_EDW_PF = 1: the next group's weights are fetched into registers under the current group
+#ifndef MMF_EDW_PF
+#define MMF_EDW_PF 1
+#endif
 template <int K, int S, int KS, int TT, int R>
 __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restrict__ x, int Cin,
                                                         const f16_t* __restrict__ we, const float* __restrict__ be,
@@ -411,8 +415,10 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
                                                         int W, int C, int CW_, int T_, int tiles_x) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
   constexpr int PAD = (K - 1) / 2, KP = KS * 32;
-  const int T = TT ? TT : T_, CW = TT ? 48 : CW_;  // compile-time only on the dw_compute_ct path
-  const int NG = CW / 8, NF = CW / 16, IT = (T - 1) * S + K;
+  constexpr int CW = 48, NF = CW / 16;  // the host launches 48-channel groups only
+  constexpr int NRF_CT = TT ? ((((TT - 1) * S + K) * ((TT - 1) * S + K)) + 15) / 16 : 0;
+  const int T = TT ? TT : T_;
+  const int NG = CW / 8, IT = (T - 1) * S + K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int bi = blockIdx.z;
@@ -446,50 +452,85 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
                                       : make_uint4(0, 0, 0, 0);
     }
   }
-  // every 48-channel group of the block's Cexp channels, reusing the input fragments above
+  // every 48-channel group of the block's Cexp channels, reusing the input fragments above.  The
+  // group's weights are fetched into registers one group ahead (issued under the previous group's
+  // expand + depthwise phases) and written to LDS after that group's trailing barrier.
+  constexpr int NPE = (CW * (KP / 8) + 255) / 256, NPD = (K * K * CW + 255) / 256;
+  uint4 pe[NPE];
+  float pd[NPD], pbias = 0.f, pbe = 0.f;
+  auto fetch_w = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < NPE; ++j) {
+      const int i = tid + j * 256, r = i / (KP / 8), kc = i - r * (KP / 8);
+      pe[j] = (i < CW * (KP / 8) && kc * 8 < Cin) ? *reinterpret_cast<const uint4*>(we + (size_t)(c0 + r) * Cin + kc * 8)
+                                                   : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NPD; ++j) {
+      const int i = tid + j * 256, t = i / CW, c = i - t * CW;
+      pd[j] = i < K * K * CW ? w[(size_t)(c0 + c) * K * K + t] : 0.f;
+    }
+    if (tid < CW) {
+      pbias = bias[c0 + tid];
+      pbe = be[c0 + tid];
+    }
+  };
+  if (MMF_EDW_PF) fetch_w(0);
   for (int c0 = 0; c0 < C; c0 += CW) {
-    for (int i = tid; i < CW * (KP / 8); i += 256) {
-      const int r = i / (KP / 8), kc = i - r * (KP / 8);
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (kc * 8 < Cin) v = *reinterpret_cast<const uint4*>(we + (size_t)(c0 + r) * Cin + kc * 8);
-      *reinterpret_cast<uint4*>(swe + r * KP + kc * 8) = v;
+    if (!MMF_EDW_PF) fetch_w(c0);
+#pragma unroll
+    for (int j = 0; j < NPE; ++j) {
+      const int i = tid + j * 256, r = i / (KP / 8), kc = i - r * (KP / 8);
+      if (i < CW * (KP / 8)) *reinterpret_cast<uint4*>(swe + r * KP + kc * 8) = pe[j];
     }
-    for (int i = tid; i < K * K * CW; i += 256) {
-      const int t = i / CW, c = i - t * CW;
-      sw[i] = w[(size_t)(c0 + c) * K * K + t];
-    }
-    for (int i = tid; i < CW; i += 256) {
-      sb[i] = bias[c0 + i];
-      sbe[i] = be[c0 + i];
+#pragma unroll
+    for (int j = 0; j < NPD; ++j)
+      if (tid + j * 256 < K * K * CW) sw[tid + j * 256] = pd[j];
+    if (tid < CW) {
+      sb[tid] = pbias;
+      sbe[tid] = pbe;
     }
     __syncthreads();
     EST()
+    if (MMF_EDW_PF && c0 + CW < C) fetch_w(c0 + CW);
 
-    // ---- expand the input tile (+halo) into LDS ----
+    // ---- expand the input tile (+halo) into LDS: every MFMA of a fragment row issued before its
+    // epilogues (the group's weight fragments and bias held in registers) ----
+    {
+      f16x8 wf[NF][KS];
+      float4 bev[NF];
 #pragma unroll
-    for (int it = 0; it < MAXRF; ++it) {
-      const int rf = wave + 4 * it;
-      if (rf >= nrf) break;
-      const int pix = rf * 16 + fr;
-      const int ty = pix / IT, tx = pix - ty * IT;
-      const int iy = iy0 + ty, ix = ix0 + tx;
-      const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
-#pragma unroll 1
       for (int nf = 0; nf < NF; ++nf) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const f16x8 wf = as_f16x8(*reinterpret_cast<const uint4*>(swe + (nf * 16 + fr) * KP + ks * 32 + fg * 8));
-          acc = mfma16x16x32(wf, as_f16x8(xr[it][ks]), acc);
-        }
-        if (pix < npix) {
-          const int cl = nf * 16 + fg * 4;
-          const float4 b = *reinterpret_cast<const float4*>(sbe + cl);
-          float e[4] = {acc[0] + b.x, acc[1] + b.y, acc[2] + b.z, acc[3] + b.w};
-          act4<ACT_SILU>(e);
+        for (int ks = 0; ks < KS; ++ks)
+          wf[nf][ks] = as_f16x8(*reinterpret_cast<const uint4*>(swe + (nf * 16 + fr) * KP + ks * 32 + fg * 8));
+        bev[nf] = *reinterpret_cast<const float4*>(sbe + nf * 16 + fg * 4);
+      }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) e[r] = inimg ? e[r] : 0.f;
-          *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + cl) = make_uint2(pack2h(e[0], e[1]), pack2h(e[2], e[3]));
+      for (int it = 0; it < MAXRF; ++it) {
+        const int rf = wave + 4 * it;
+        if ((TT > 0 && 4 * it + 3 < NRF_CT) || rf < nrf) {
+          f32x4 acc[NF];
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf) {
+            acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) acc[nf] = mfma16x16x32(wf[nf][ks], as_f16x8(xr[it][ks]), acc[nf]);
+          }
+          const int pix = rf * 16 + fr;
+          const int ty = pix / IT, tx = pix - ty * IT;
+          const int iy = iy0 + ty, ix = ix0 + tx;
+          const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf) {
+            float e[4] = {acc[nf][0] + bev[nf].x, acc[nf][1] + bev[nf].y, acc[nf][2] + bev[nf].z, acc[nf][3] + bev[nf].w};
+            act4<ACT_SILU>(e);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) e[r] = inimg ? e[r] : 0.f;
+            if (pix < npix)
+              *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + nf * 16 + fg * 4) =
+                  make_uint2(pack2h(e[0], e[1]), pack2h(e[2], e[3]));
+          }
         }
       }
     }
@@ -891,6 +932,35 @@ hipError_t launch_effnet_stem32(const uint8_t* img, const float* x, const float*
   return hipGetLastError();
 }
 
+// depthwise output runs R of the compile-time geometries (dw_compute_ct; -D overrides for A/B builds)
+#ifndef MMF_R_D16
+#define MMF_R_D16 4
+#endif
+#ifndef MMF_R_D14
+#define MMF_R_D14 2
+#endif
+#ifndef MMF_R_D8
+#define MMF_R_D8 2
+#endif
+#ifndef MMF_R_D7
+#define MMF_R_D7 1
+#endif
+#ifndef MMF_R_E21
+#define MMF_R_E21 2
+#endif
+#ifndef MMF_R_E22
+#define MMF_R_E22 2
+#endif
+#ifndef MMF_R_E32
+#define MMF_R_E32 2
+#endif
+#ifndef MMF_R_E31
+#define MMF_R_E31 1
+#endif
+#ifndef MMF_R_E41
+#define MMF_R_E41 1
+#endif
+
 // tile edge: the largest divisor of the output edge up to 16 (stride 1) / 8 (stride 2)
 static void dw_geometry(int H, int W, int C, int stride, int* T_, int* CW_, int* tiles_x_, int* ntiles_) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
@@ -929,14 +999,14 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
     return hipGetLastError();                                                                                 \
   }
   if (ct) {  // ct = 0: runtime-geometry kernels only (A/B option "dw_ct")
-    MMF_DWCT(3, 1, 16, 32, 4)
-    MMF_DWCT(3, 1, 14, 48, 2)
-    MMF_DWCT(5, 1, 14, 48, 2)
-    MMF_DWCT(3, 2, 8, 48, 2)
-    MMF_DWCT(5, 1, 7, 48, 1)
-    MMF_DWCT(3, 1, 7, 48, 1)
-    MMF_DWCT(5, 2, 7, 48, 1)
-    MMF_DWCT(3, 2, 7, 48, 1)
+    MMF_DWCT(3, 1, 16, 32, MMF_R_D16)
+    MMF_DWCT(3, 1, 14, 48, MMF_R_D14)
+    MMF_DWCT(5, 1, 14, 48, MMF_R_D14)
+    MMF_DWCT(3, 2, 8, 48, MMF_R_D8)
+    MMF_DWCT(5, 1, 7, 48, MMF_R_D7)
+    MMF_DWCT(3, 1, 7, 48, MMF_R_D7)
+    MMF_DWCT(5, 2, 7, 48, MMF_R_D7)
+    MMF_DWCT(3, 2, 7, 48, MMF_R_D7)
   }
 #undef MMF_DWCT
 #define MMF_DW(KK, SS)                                                                                        \
@@ -975,11 +1045,11 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
     return hipGetLastError();                                                                                 \
   }
   if (ct) {
-    MMF_EDWCT(3, 2, 1, 8, 2)
-    MMF_EDWCT(3, 1, 1, 14, 2)
-    MMF_EDWCT(5, 1, 2, 14, 2)
-    MMF_EDWCT(5, 2, 1, 7, 1)
-    MMF_EDWCT(3, 2, 2, 7, 1)
+    MMF_EDWCT(3, 2, 1, 8, MMF_R_E21)
+    MMF_EDWCT(3, 1, 1, 14, MMF_R_E22)
+    MMF_EDWCT(5, 1, 2, 14, MMF_R_E32)
+    MMF_EDWCT(5, 2, 1, 7, MMF_R_E31)
+    MMF_EDWCT(3, 2, 2, 7, MMF_R_E41)
   }
 #undef MMF_EDWCT
 #define MMF_EDW(KK, SS, QS)                                                                                      \
