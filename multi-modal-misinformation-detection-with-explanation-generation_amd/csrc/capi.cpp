@@ -134,6 +134,8 @@ struct Options {
   int gemm_ring = 0;    // plain fp16-output encoder GEMMs on the loader / consumer kernel (gemm_ring.hip)
   int pw32_mfma = 1;    // fp32 tower's 1x1 convs on the fp32-input MFMA (1) or the fp32-FMA VALU kernel (0)
   int gemm_wide = 0;    // 256x384 tiles where they save a persistent round (gemm.hip glds_pick; step A/B: a tie)
+  int dw_persist = 0;   // persistent depthwise kernels with the next tile's loads in flight (effnet.hip; A/B: slower)
+  int effnet_chunks = 4;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.95 -> 3.62 ms)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -145,6 +147,7 @@ const OptName kOptNames[] = {
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
     {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},            {"gemm_ring", &Options::gemm_ring, "MMF_GEMM_RING"},
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
+    {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -1029,10 +1032,25 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
   return 0;
 }
 
+// The EfficientNet activation workspaces hold max_batch images at the largest per-image size of each
+// buffer; a batch chunk that starts at image b0 works in the disjoint slice b0 * (per-image max) on,
+// so chunks of one batch can run concurrently on different streams (mmf_effnet_forward).
+struct EffWs {
+  f16_t *e_a, *e_b, *e_exp, *e_dw;
+  float *e_pool, *e_scale;
+};
+EffWs eff_ws(mmf_handle* h, int b0) {
+  const Workspace& w = h->ws;
+  const EffSizes es = eff_sizes();
+  const size_t b = (size_t)b0;
+  return EffWs{w.e_a + b * es.io, w.e_b + b * es.io, w.e_exp + b * es.exp, w.e_dw + b * es.dw,
+               w.e_pool + b * es.pool, w.e_scale + b * 1280};
+}
+
 int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score, int score_stride,
-               hipStream_t s) {
+               hipStream_t s, int img0 = 0) {
   if (h->opt.effnet_fp32) return run_effnet32(h, img, xf32, B, logits, score, score_stride, s);
-  Workspace& w = h->ws;
+  const EffWs w = eff_ws(h, img0);
   f16_t* cur = w.e_a;
   f16_t* nxt = w.e_b;
   // option fuse_stem = 0: separate stem launch + stage-1 depthwise (A/B and parity tests)
@@ -1070,7 +1088,8 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
     if (!fuse && !(&b == &b0 && fuse_stem)) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k,
                    (double)B * b.cexp * 2 * ((double)H * W + (double)Ho * Wo));
-      HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s, h->opt.dw_ct));
+      HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s,
+                            h->opt.dw_ct | (h->opt.dw_persist ? 2 : 0)));
     }
     ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, (double)B * b.cexp * 4 * (nch + 1));
     HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s));
@@ -1279,7 +1298,28 @@ int mmf_effnet_forward(mmf_handle* h, const uint8_t* img, int B, float* logits, 
   if (!(h->ready & 2)) return fail(MMF_EINVAL, "EfficientNet not loaded");
   CHK(check_cap(h, B, 1, 1));
   HIPCHK(hipSetDevice(h->device));
-  return run_effnet(h, img, nullptr, B, logits, score, 1, (hipStream_t)stream);
+  const hipStream_t s = (hipStream_t)stream;
+  // option effnet_chunks: the batch split into that many image chunks on concurrent streams (each
+  // chunk's kernels fill the other's launch tails; per-image results are unchanged: every layer is
+  // per image, and the GEMM rows do not depend on M)
+  const int nc = std::min(std::max(h->opt.effnet_chunks, 1), 4);
+  if (nc == 1 || B < 32 * nc || h->opt.effnet_fp32) return run_effnet(h, img, nullptr, B, logits, score, 1, s);
+  CHK(ensure_towers(h));
+  HIPCHK(hipEventRecord(h->fork_ev, s));
+  int b0 = 0;
+  for (int c = 0; c < nc; ++c) {
+    const int bc = B / nc + (c < B % nc ? 1 : 0);
+    const hipStream_t cs = c ? h->tower[c - 1] : s;
+    if (c) HIPCHK(hipStreamWaitEvent(cs, h->fork_ev, 0));
+    CHK(run_effnet(h, img + (size_t)b0 * 224 * 224 * 3, nullptr, bc, logits ? logits + (size_t)b0 * 2 : nullptr,
+                   score ? score + b0 : nullptr, 1, cs, b0));
+    b0 += bc;
+  }
+  for (int c = 1; c < nc; ++c) {
+    HIPCHK(hipEventRecord(h->join_ev[c - 1], h->tower[c - 1]));
+    HIPCHK(hipStreamWaitEvent(s, h->join_ev[c - 1], 0));
+  }
+  return 0;
 }
 
 int mmf_effnet_forward_f32(mmf_handle* h, const float* x, int B, float* logits, float* score, void* stream) {

@@ -213,7 +213,8 @@ MMF_DEV float fma_mix(uint32_t h2, float w, float acc) {
 // Items = NG * T * (T / R) over the first (256 / NG) * NG threads (each keeps its channel group).
 template <int K, int S, int T, int CW, int R>
 MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, float* red, f16_t* __restrict__ out,
-                           float* __restrict__ pool_part, int bi, int c0, int oy0, int ox0, int Ho, int Wo, int C) {
+                           float* __restrict__ pool_part, int bi, int c0, int oy0, int ox0, int Ho, int Wo, int C,
+                           int tix, int ntiles) {
   constexpr int NG = CW / 8, IT = (T - 1) * S + K, NR = T / R, ITEMS = NG * T * NR, IC = (R - 1) * S + K;
   constexpr int STRIDE = (256 / NG) * NG;  // active threads: a thread's channel group g never changes
   constexpr int NRED = STRIDE / NG;         // partial-sum slots per channel (<= the caller's red rows)
@@ -294,11 +295,10 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
   }
   __syncthreads();
   // fixed-order reduction over the thread slots of each channel -> one partial per (image, tile, channel)
-  const int ntiles = gridDim.x;
   for (int c = tid; c < CW; c += 256) {
     float sum = 0.f;
     for (int q = 0; q < NRED; ++q) sum += red[q * CW + c];
-    *at_bytes(pool_part + (size_t)bi * ntiles * C, (uint32_t)(blockIdx.x * C + c0 + c) * 4u) = sum;
+    *at_bytes(pool_part + (size_t)bi * ntiles * C, (uint32_t)(tix * C + c0 + c) * 4u) = sum;
   }
 }
 
@@ -386,9 +386,78 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
   __syncthreads();
   EST()
 
-  if constexpr (TT > 0) dw_compute_ct<K, S, TT, CWT, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C);
+  if constexpr (TT > 0)
+    dw_compute_ct<K, S, TT, CWT, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, blockIdx.x, gridDim.x);
   else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
   EST()
+  EST_END()
+}
+
+// Persistent form of dwconv_kernel's compile-time geometries (option dw_persist, default): a block
+// keeps one channel group (blockIdx.y) and walks the (tile, image) items blockIdx.x, + gridDim.x, ...
+// Its weights are staged once, and the NEXT item's input tile (+halo) is loaded into registers right
+// after the current one is in LDS, so its HBM latency runs under the current item's taps, stores and
+// pool reduction instead of at the head of every block (stamps: 30-57 % of a one-shot block's life).
+// Out-of-image pixels read 0 through the buffer descriptor (no divergent region around the loads).
+// Same per-(image, tile, channel) pool partials and outputs as dwconv_kernel, bit for bit.
+template <int K, int S, int TT, int CWT, int R>
+__global__ __launch_bounds__(256, 3) void dwconv_persist_kernel(const f16_t* __restrict__ in, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, f16_t* __restrict__ out,
+                                                             float* __restrict__ pool_part, int H, int W, int C,
+                                                             int tiles_x, int ntiles, int nitems) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
+  constexpr int PAD = (K - 1) / 2, CW = CWT, NG = CW / 8, IT = (TT - 1) * S + K;
+  constexpr int NL = (IT * IT * NG + 255) / 256, NW = (K * K * CW + 255) / 256;
+  const int tid = threadIdx.x, c0 = blockIdx.y * CW;
+  const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+  f16_t* tile = (f16_t*)dw_smem;                              // [IT][IT][CW]
+  float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, true));  // [K*K][CW]
+  float* sb = sw + K * K * CW;                                  // [CW]
+  float* red = (float*)dw_smem;                                 // pool slots alias the tile
+  int item = blockIdx.x;
+  if (item >= nitems) return;  // (block-uniform)
+  EST_BEGIN(8 + ((K == 5) * 2 + (S == 2)) * 4 + (TT == 14 ? 1 : TT == 7 ? 2 : TT == 16 ? 3 : 0))
+  const rsrc_t rin = make_rsrc(in, (uint32_t)((size_t)(nitems / ntiles) * H * W * C * 2));
+  uint4 v[NL];
+  auto load_item = [&](int it) {
+    const int bi = it / ntiles, t = it - bi * ntiles;
+    const int ty0 = t / tiles_x, tx0 = t - ty0 * tiles_x;
+    const int iy0 = ty0 * TT * S - PAD, ix0 = tx0 * TT * S - PAD;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int idx = tid + i * 256, g = idx % NG, pix = idx / NG;
+      const int ty = pix / IT, tx = pix - ty * IT, iy = iy0 + ty, ix = ix0 + tx;
+      const bool ok = idx < IT * IT * NG && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                 rin, ok ? (uint32_t)((((size_t)bi * H + iy) * W + ix) * C + c0 + g * 8) * 2u : kOOB, 0, 0));
+    }
+  };
+  load_item(item);
+  {
+    float wv[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int i = tid + j * 256, t = i / CW, c = i - t * CW;
+      wv[j] = i < K * K * CW ? w[(size_t)(c0 + c) * K * K + t] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NW; ++j)
+      if (tid + j * 256 < K * K * CW) sw[tid + j * 256] = wv[j];
+    if (tid < CW) sb[tid] = bias[c0 + tid];
+  }
+  for (; item < nitems; item += gridDim.x) {
+    const int bi = item / ntiles, t = item - bi * ntiles;
+    const int ty0 = t / tiles_x, tx0 = t - ty0 * tiles_x;
+#pragma unroll
+    for (int i = 0; i < NL; ++i)
+      if (tid + i * 256 < IT * IT * NG) *reinterpret_cast<uint4*>(tile + (size_t)(tid + i * 256) * 8) = v[i];
+    __syncthreads();
+    EST()
+    if (item + (int)gridDim.x < nitems) load_item(item + gridDim.x);
+    dw_compute_ct<K, S, TT, CW, R>(tile, sw, sb, red, out, pool_part, bi, c0, ty0 * TT, tx0 * TT, Ho, Wo, C, t, ntiles);
+    __syncthreads();  // the reduction has read `red` (aliasing the tile) before the next item's tile
+    EST()
+  }
   EST_END()
 }
 
@@ -536,7 +605,8 @@ __global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restri
     }
     __syncthreads();
     EST()
-    if constexpr (TT > 0) dw_compute_ct<K, S, TT, CW, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C);
+    if constexpr (TT > 0)
+      dw_compute_ct<K, S, TT, CW, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, blockIdx.x, gridDim.x);
     else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
     EST()
     __syncthreads();  // the next group restages sw / sb / swe / tile and rewrites red
@@ -693,7 +763,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
   __syncthreads();
   EST()
   if constexpr (!V2) {
-    dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW);
+    dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW, blockIdx.x, 49);
     EST()
     EST_END()
   } else {
@@ -991,14 +1061,39 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
   const size_t smem = (size_t)dw_tile_bytes(IT, CW, false) + (size_t)(k * k * CW + CW + PX * CW) * 4;
   const size_t smem_ct = (size_t)dw_tile_bytes(IT, CW, true) + (size_t)(k * k * CW + CW) * 4;
   const dim3 grid(ntiles, C / CW, B), blk(256);
+  // persistent form (flag 2): about four resident blocks per CU over all channel groups, and the
+  // buffer descriptor's out-of-range offset must stay past the whole input
+  const int nitems = ntiles * B;
+  const bool persist = (ct & 2) && (size_t)B * H * W * C * 2 < (size_t)kOOB;
+  // one wave of resident blocks exactly (a block that does not fit at launch would run its whole
+  // item list after the others: a tail), spread over the channel groups
+  auto pgrid = [&](const void* kern) {
+    static int ncu = 0;
+    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
+    static const void* ck[16];
+    static int co[16], nc = 0;
+    int occ = 0;
+    for (int i = 0; i < nc; ++i)
+      if (ck[i] == kern) occ = co[i];
+    if (!occ) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, smem_ct) != hipSuccess || occ < 1) occ = 1;
+      if (nc < 16) { ck[nc] = kern; co[nc++] = occ; }
+    }
+    return dim3(std::max(1, std::min(nitems, ncu * occ / (C / CW))), C / CW);
+  };
   // compile-time geometries of EfficientNet-B0 at 224^2 (output runs R chosen so that items <= 256)
 #define MMF_DWCT(KK, SS, TT, CC, RR)                                                                          \
   if (k == KK && stride == SS && T == TT && CW == CC) {                                                        \
-    hipLaunchKernelGGL((dwconv_kernel<KK, SS, TT, CC, RR>), grid, blk, smem_ct, s, in, w, bias, out, pool_part, H, W, \
-                       C, CW, T, tiles_x);                                                                    \
+    if (persist)                                                                                              \
+      hipLaunchKernelGGL((dwconv_persist_kernel<KK, SS, TT, CC, RR>),                                          \
+                         pgrid((const void*)dwconv_persist_kernel<KK, SS, TT, CC, RR>), blk, smem_ct, s, in, w,  \
+                         bias, out, pool_part, H, W, C, tiles_x, ntiles, nitems);                             \
+    else                                                                                                      \
+      hipLaunchKernelGGL((dwconv_kernel<KK, SS, TT, CC, RR>), grid, blk, smem_ct, s, in, w, bias, out, pool_part, H, \
+                         W, C, CW, T, tiles_x);                                                               \
     return hipGetLastError();                                                                                 \
   }
-  if (ct) {  // ct = 0: runtime-geometry kernels only (A/B option "dw_ct")
+  if (ct & 1) {  // bit 0 clear: runtime-geometry kernels only (A/B option "dw_ct")
     MMF_DWCT(3, 1, 16, 32, MMF_R_D16)
     MMF_DWCT(3, 1, 14, 48, MMF_R_D14)
     MMF_DWCT(5, 1, 14, 48, MMF_R_D14)

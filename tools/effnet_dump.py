@@ -1,5 +1,5 @@
 """EfficientNet logits of a fixed synthetic batch -> .npy (compare builds bit for bit:
-MMF_HIP_LIB=a.so python tools/effnet_dump.py a.npy; python tools/effnet_dump.py b.npy; cmp)."""
+MMF_HIP_LIB=a.so python tools/effnet_dump.py a.npy [opt=v ...]; python tools/effnet_dump.py b.npy; cmp)."""
 import os
 import sys
 
@@ -14,6 +14,9 @@ def main():
     import mmf_amd.weights as W
     from mmf_amd.engine import Engine
     eng = Engine(0, W.synthetic_detector_state(0), None, max_batch=256)
+    for kv in sys.argv[2:]:  # run-time options k=v (e.g. effnet_chunks=1)
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     lg, sc = eng.effnet_forward(syn.images(256, 41))
     torch.cuda.synchronize()
     np.save(sys.argv[1], lg.cpu().numpy())
