@@ -32,6 +32,7 @@ extern "C" {
 #define MMF_ENOMEM (-12)
 #define MMF_EIO (-5)
 #define MMF_ERANGE (-34) /* an input outside a kernel's supported range (mmf_resize_pil: too many taps) */
+#define MMF_EUNSUPPORTED (-95) /* a valid input of a kind this path does not handle (mmf_jpeg_*: progressive, ...) */
 
 #define MMF_DTYPE_F32 0
 #define MMF_DTYPE_I64 1
@@ -112,6 +113,33 @@ int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, 
  * per output pixel than the kernels hold (mmf_resize_supported). */
 int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, const int32_t* wh, int B,
                    int pixel_bytes, uint8_t* out_effnet, uint8_t* out_clip, void* stream);
+
+/* Device JPEG decode (the reference's Image.open(path).convert("RGB"),
+ * misinfo_forensics.py:255-258, decodes through Pillow's libjpeg-turbo).  Host: marker parsing and
+ * Huffman entropy decoding (the serial part); device: dequantisation, islow IDCT, fancy chroma
+ * upsampling and YCbCr -> RGB, pixels bit-exact with Pillow's decoder.  Supported: 8-bit baseline /
+ * extended sequential Huffman JPEGs, one scan, grayscale or YCbCr 4:4:4 / 4:2:2 / 4:2:0; anything
+ * else returns MMF_EUNSUPPORTED (decode that file on the host).
+ *
+ * mmf_jpeg_header: host-only, no handle.  info[MMF_JPEG_INFO_LEN] = {width, height, ncomp, hmax, vmax,
+ * bw0, bh0, bw1, bh1, bw2, bh2, blocks, 0...} (bw_c x bh_c = component c's MCU-padded block grid;
+ * blocks = their sum = the int16[64] blocks mmf_jpeg_entropy writes).  Returns 0 if supported. */
+#define MMF_JPEG_INFO_LEN 16
+int mmf_jpeg_header(const uint8_t* data, int64_t nbytes, int32_t* info);
+/* Host-only, thread-safe: quantised coefficients of every component as [bh_c][bw_c][64] int16
+ * (natural order, components back to back) and the components' quantisation tables qt[c][64]
+ * (natural order, uint16).  Replaces libjpeg's decode_mcu (jdhuff.c). */
+int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* coefs, uint16_t* qt);
+/* Device: B images' coefficients and tables -> uint8 RGBX pixels, bit-exact with Pillow's decoder.
+ * Every pointer is DEVICE memory: coefs int16 (image i's blocks from block offset coef_blocks[i]),
+ * qt uint16 [B][3][64] (mmf_jpeg_entropy's tables), infos int32 [B][MMF_JPEG_INFO_LEN]
+ * (mmf_jpeg_header's), out_offsets int64 [B] (byte offset of image i's [h][w][4] RGBX pixels in
+ * out_rgbx; X = 255), samples = scratch of 64 * sum(blocks) bytes (component sample planes).
+ * max_blocks / max_pixels = the largest blocks / width * height over the B images (grid sizes).
+ * Feeds mmf_resize_pil (pixel_bytes 4).  Asynchronous on `stream`. */
+int mmf_jpeg_reconstruct(mmf_handle* h, const int16_t* coefs, const uint16_t* qt, const int64_t* coef_blocks,
+                         const int32_t* infos, const int64_t* out_offsets, int B, int max_blocks, int max_pixels,
+                         uint8_t* samples, uint8_t* out_rgbx, void* stream);
 
 /* 1 if a width x height image fits mmf_resize_pil's tap budget in both geometries (bicubic CLIP:
  * shortest side <= ~5264 px; bilinear EfficientNet: either side <= ~10528 px), else 0.  Host-only,

@@ -329,6 +329,10 @@ class MisinfoForensics:
         self._emb_cache = None  # (hash of the CLIP input window, its image embedding): _image_emb
         self.vit_passes = 0  # single-image ViT launches (observability, tests)
         self.reuse_image_embedding = True  # False: a ViT pass per call, as the reference (A/B)
+        # analyze_pairs: JPEG bytes / files entropy-decoded on the host, reconstructed on the device
+        # (jpeg.py; MMF_DEVICE_JPEG=0 or False here: Pillow decodes every image, A/B)
+        self.device_jpeg = os.environ.get("MMF_DEVICE_JPEG", "1") != "0"
+        self._jpeg = None
         self.roberta_tokenizer = roberta_tokenizer
         self.clip_processor = clip_processor
         if self.roberta_tokenizer is None:
@@ -653,14 +657,28 @@ class MisinfoForensics:
         if not chunks:
             return []
 
+        use_jpeg = self.device_jpeg
+        if use_jpeg and self._jpeg is None:
+            from . import jpeg
+            self._jpeg = jpeg.JpegStager()
+
         def host_stage(a, b):
             # (tokenising on a third thread while the images decode measured a tie for one chunk and
             # 33 % slower for four: DESIGN §6)
             rob = io_utils.tokenize_roberta_batch(self.roberta_tokenizer, texts[a:b])
             rid, rm = io_utils.pad_ids(rob, W.ROBERTA["pad_id"])
             cid, cm = self._clip_ids(list(texts[a:b]))
-            # decoded pixels; the resampling to both towers' windows runs on the device
-            return rid, rm, cid, cm, io_utils.decode_rgb(images[a:b])
+            # JPEG bytes / files: entropy-decoded here, reconstructed on the device; everything else
+            # decoded by Pillow (pixels); the resampling to both towers' windows runs on the device
+            st = None
+            rest = list(range(b - a))
+            if use_jpeg:
+                from . import jpeg
+                st = self._jpeg.stage([jpeg.read_bytes(x) for x in images[a:b]])
+                done = set(st.index)
+                rest = [i for i in rest if i not in done]
+            rgb = io_utils.decode_rgb([images[a + i] for i in rest]) if rest else []
+            return rid, rm, cid, cm, (b - a, st, rest, rgb)
 
         from concurrent.futures import ThreadPoolExecutor
         res: List[Dict] = []
@@ -671,9 +689,27 @@ class MisinfoForensics:
                 if k + 1 < len(chunks):
                     fut = ex.submit(host_stage, *chunks[k + 1])
                 self._fit_text(rid.shape[1])
-                eff, clp = self._resize(rgb)
+                eff, clp = self._windows(*rgb)
                 res.extend(self.batch_to_dicts(self.analyze_batch(rid, rm, cid, cm, eff, clp)))
         return res
+
+    def _windows(self, n: int, st, rest: List[int], rgb: List[np.ndarray]):
+        """Both towers' windows of a chunk: device-decoded JPEGs (st) and Pillow-decoded pixels
+        (rest, rgb) merged back into input order."""
+        if st is None or not st.index:
+            return self._resize(rgb)
+        from . import jpeg
+        e1, c1 = jpeg.device_windows(self.engine, self._jpeg, st)
+        if not rest:
+            return e1, c1
+        eff = torch.empty((n, 224, 224, 3), dtype=torch.uint8, device=self.device)
+        clp = torch.empty_like(eff)
+        sel = torch.as_tensor(st.index, device=self.device)
+        eff[sel], clp[sel] = e1, c1
+        e2, c2 = self._resize(rgb)
+        sel = torch.as_tensor(rest, device=self.device)
+        eff[sel], clp[sel] = e2, c2
+        return eff, clp
 
     def _resize(self, rgb: List[np.ndarray]):
         """Both towers' 224x224 windows of decoded images: Pillow-exact on the device

@@ -971,7 +971,7 @@ EffSizes eff_sizes() {
 // The fp32 tower (option effnet_fp32): same network, same folded weights (fp32 copies of the 1x1
 // convs), activations fp32 throughout -- no fusion, one launch per layer.
 int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score,
-                 int score_stride, hipStream_t s) {
+                 int score_stride, hipStream_t s, int img0 = 0) {
   Workspace& w = h->ws;
   if (w.e32_cap_b < h->cap_b) {
     CHK(free_group(h, AG_EFF32));
@@ -984,8 +984,15 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
     CHK(dev_alloc(h, &p, nb * es.dw, AG_EFF32)); w.e32_dw = (float*)p;
     w.e32_cap_b = h->cap_b;
   }
-  float* cur = w.e32_a;
-  float* nxt = w.e32_b;
+  // a chunk starting at image img0 works in its own slice of every workspace (mmf_effnet_forward)
+  const EffSizes es = eff_sizes();
+  const size_t b0 = (size_t)img0;
+  float* const e32_exp = w.e32_exp + b0 * es.exp;
+  float* const e32_dw = w.e32_dw + b0 * es.dw;
+  float* const e_pool = w.e_pool + b0 * es.pool;
+  float* const e_scale = w.e_scale + b0 * 1280;
+  float* cur = w.e32_a + b0 * es.io;
+  float* nxt = w.e32_b + b0 * es.io;
   {
     ProfScope ps(h, s, PK_STEM, 2.0 * B * 112 * 112 * 32 * 27, (double)B * (224 * 224 * 3 + 112 * 112 * 32 * 4));
     HIPCHK(launch_effnet_stem32(img, xf32, h->e_stem_w, h->e_stem_b, cur, B, s));
@@ -996,26 +1003,26 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
     const float* src = cur;
     if (b.expand != 1) {
       ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * b.cin * b.cexp, 4.0 * B * H * W * (b.cin + b.cexp));
-      HIPCHK(launch_pw32(cur, b.e.w32, b.e.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, b.cexp, b.cin, 3 /* SiLU */, s,
+      HIPCHK(launch_pw32(cur, b.e.w32, b.e.b, nullptr, 1, nullptr, e32_exp, B * H * W, b.cexp, b.cin, 3 /* SiLU */, s,
                              h->opt.pw32_mfma));
-      src = w.e32_exp;
+      src = e32_exp;
     }
     {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k, 4.0 * B * b.cexp * ((double)H * W + Ho * Wo));
-      HIPCHK(launch_dw32(src, b.wd_t, b.bd, w.e32_dw, B, H, W, b.cexp, b.k, b.stride, s));
+      HIPCHK(launch_dw32(src, b.wd_t, b.bd, e32_dw, B, H, W, b.cexp, b.k, b.stride, s));
     }
     {
       ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, 4.0 * B * b.cexp * ((double)Ho * Wo + 2));
       // as many pool chunks as the fp16 tower uses for this layer (fits e_pool by construction)
       const int nch = std::min(dwconv_nchunks(H, W, b.cexp, b.stride), Ho * Wo);
-      HIPCHK(launch_sum32(w.e32_dw, B, Ho * Wo, b.cexp, nch, w.e_pool, s));
-      HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s,
+      HIPCHK(launch_sum32(e32_dw, B, Ho * Wo, b.cexp, nch, e_pool, s));
+      HIPCHK(launch_se(e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, e_scale, B, b.cexp, b.csq, s,
                        true));
     }
     {
       ProfScope ps(h, s, PK_PW32, 2.0 * B * Ho * Wo * b.cexp * b.cout,
                    4.0 * B * Ho * Wo * (b.cexp + b.cout * (b.residual ? 2 : 1)));
-      HIPCHK(launch_pw32(w.e32_dw, b.p.w32, b.p.b, w.e_scale, Ho * Wo, b.residual ? cur : nullptr, nxt, B * Ho * Wo,
+      HIPCHK(launch_pw32(e32_dw, b.p.w32, b.p.b, e_scale, Ho * Wo, b.residual ? cur : nullptr, nxt, B * Ho * Wo,
                          b.cout, b.cexp, 0, s, h->opt.pw32_mfma));
     }
     std::swap(cur, nxt);
@@ -1024,11 +1031,11 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
   }
   {
     ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * 320 * 1280, 4.0 * B * H * W * (320 + 1280));
-    HIPCHK(launch_pw32(cur, h->e_head.w32, h->e_head.b, nullptr, 1, nullptr, w.e32_exp, B * H * W, 1280, 320, 3, s,
+    HIPCHK(launch_pw32(cur, h->e_head.w32, h->e_head.b, nullptr, 1, nullptr, e32_exp, B * H * W, 1280, 320, 3, s,
                        h->opt.pw32_mfma));
   }
   ProfScope ps(h, s, PK_GAP, (double)B * H * W * 1280 + 4.0 * B * 1280, (double)B * H * W * 1280 * 4);
-  HIPCHK(launch_gap32(w.e32_exp, H * W, 1280, h->e_cls_w, h->e_cls_b, logits, score, score_stride, B, s));
+  HIPCHK(launch_gap32(e32_exp, H * W, 1280, h->e_cls_w, h->e_cls_b, logits, score, score_stride, B, s));
   return 0;
 }
 
@@ -1049,7 +1056,7 @@ EffWs eff_ws(mmf_handle* h, int b0) {
 
 int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score, int score_stride,
                hipStream_t s, int img0 = 0) {
-  if (h->opt.effnet_fp32) return run_effnet32(h, img, xf32, B, logits, score, score_stride, s);
+  if (h->opt.effnet_fp32) return run_effnet32(h, img, xf32, B, logits, score, score_stride, s, img0);
   const EffWs w = eff_ws(h, img0);
   f16_t* cur = w.e_a;
   f16_t* nxt = w.e_b;
@@ -1303,7 +1310,7 @@ int mmf_effnet_forward(mmf_handle* h, const uint8_t* img, int B, float* logits, 
   // chunk's kernels fill the other's launch tails; per-image results are unchanged: every layer is
   // per image, and the GEMM rows do not depend on M)
   const int nc = std::min(std::max(h->opt.effnet_chunks, 1), 4);
-  if (nc == 1 || B < 32 * nc || h->opt.effnet_fp32) return run_effnet(h, img, nullptr, B, logits, score, 1, s);
+  if (nc == 1 || B < 32 * nc) return run_effnet(h, img, nullptr, B, logits, score, 1, s);
   CHK(ensure_towers(h));
   HIPCHK(hipEventRecord(h->fork_ev, s));
   int b0 = 0;
@@ -1625,6 +1632,20 @@ bool plan_job(int w, int h, int geom, ResizeJob* J) {
   return true;
 }
 }  // namespace
+
+int mmf_jpeg_reconstruct(mmf_handle* h, const int16_t* coefs, const uint16_t* qt, const int64_t* coef_blocks,
+                         const int32_t* infos, const int64_t* out_offsets, int B, int max_blocks, int max_pixels,
+                         uint8_t* samples, uint8_t* out_rgbx, void* stream) {
+  if (!h || B < 0) return fail(MMF_EINVAL, "null argument");
+  if (B == 0) return 0;
+  if (!coefs || !qt || !coef_blocks || !infos || !out_offsets || !samples || !out_rgbx)
+    return fail(MMF_EINVAL, "null argument");
+  if (max_blocks <= 0 || max_pixels <= 0) return fail(MMF_EINVAL, "max_blocks / max_pixels must be positive");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(launch_jpeg_reconstruct(coefs, qt, coef_blocks, infos, out_offsets, B, max_blocks, max_pixels, samples,
+                                 out_rgbx, (hipStream_t)stream));
+  return 0;
+}
 
 int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, const int32_t* wh, int B,
                    int pixel_bytes, uint8_t* out_effnet, uint8_t* out_clip, void* stream) {

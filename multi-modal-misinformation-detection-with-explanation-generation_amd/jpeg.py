@@ -1,0 +1,175 @@
+"""Device JPEG decode for the host input stage.
+
+The reference decodes every image with `Image.open(path).convert("RGB")`
+(misinfo_forensics.py:255-258) -- Pillow's libjpeg-turbo on one host core.  Here the only serial
+part, marker parsing + Huffman entropy decoding, runs in C on the host threads
+(csrc/jpeg_host.cpp: mmf_jpeg_header / mmf_jpeg_entropy, called through ctypes, which releases the
+GIL) straight into a pinned staging buffer; one H2D copy moves the quantised coefficients, and the
+device reconstructs the pixels (csrc/jpeg.hip: islow IDCT, fancy chroma upsampling, YCbCr -> RGB,
+bit-exact with Pillow) as RGBX images that feed the Pillow-exact resampler (mmf_resize_pil).
+Files the C decoder does not take (progressive, CMYK, 4:4:0, ...) report MMF_EUNSUPPORTED and are
+decoded by Pillow on the host, as before.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import hip
+
+INFO_LEN = 16
+MMF_EUNSUPPORTED = -95
+
+
+def read_bytes(item) -> Optional[bytes]:
+    """Encoded bytes of an image argument (bytes, or a path to a file), None for anything else
+    (PIL images, arrays): those keep the Pillow path."""
+    if isinstance(item, (bytes, bytearray, memoryview)):
+        return bytes(item)
+    if isinstance(item, (str, os.PathLike)) and os.path.isfile(item):
+        with open(item, "rb") as f:
+            return f.read()
+    return None
+
+
+def _align(n: int, a: int = 256) -> int:
+    return (n + a - 1) // a * a
+
+
+class Staged:
+    """One chunk's entropy-decoded JPEGs in a pinned buffer: which inputs, their header infos and
+    the byte layout of the buffer (coefficients | tables | infos | block offsets | RGBX offsets)."""
+
+    def __init__(self):
+        self.index: List[int] = []  # positions (within the chunk) decoded by the device path
+        self.infos = None
+        self.slot = 0
+        self.nbytes = 0
+        self.sections = {}
+        self.blocks = self.pixels = 0
+        self.max_blocks = self.max_pixels = 0
+
+
+class JpegStager:
+    """Host half: headers + entropy decoding of a chunk into one of two pinned buffers (the other
+    may still be feeding the previous chunk's H2D copy: each slot's copy is fenced by an event)."""
+
+    def __init__(self, workers: Optional[int] = None):
+        self.lib = hip.load()
+        self.workers = workers or min(16, len(os.sched_getaffinity(0)))
+        self.buf = [None, None]
+        self.copied = [None, None]  # torch.cuda.Event recorded after the H2D copy of each slot
+        self.next_slot = 0
+        self._pool = ThreadPoolExecutor(max_workers=self.workers)
+
+    def close(self):
+        self._pool.shutdown(wait=False)
+
+    def stage(self, datas: List[Optional[bytes]]) -> Staged:
+        st = Staged()
+        lib = self.lib
+
+        def header(d):
+            if d is None:
+                return None
+            info = np.zeros(INFO_LEN, np.int32)
+            rc = lib.mmf_jpeg_header(d, len(d), info.ctypes.data)
+            return info if rc == 0 else None
+        infos = list(self._pool.map(header, datas)) if len(datas) > 1 else [header(d) for d in datas]
+        st.index = [i for i, inf in enumerate(infos) if inf is not None]
+        n = len(st.index)
+        if n == 0:
+            return st
+        inf = np.stack([infos[i] for i in st.index]).astype(np.int32)
+        blocks = inf[:, 11].astype(np.int64)
+        pixels = inf[:, 0].astype(np.int64) * inf[:, 1]
+        coef_blocks = np.zeros(n, np.int64)
+        coef_blocks[1:] = np.cumsum(blocks)[:-1]
+        out_off = np.zeros(n, np.int64)
+        out_off[1:] = np.cumsum(pixels * 4)[:-1]
+        st.blocks, st.pixels = int(blocks.sum()), int(pixels.sum())
+        st.max_blocks, st.max_pixels = int(blocks.max()), int(pixels.max())
+        sec = {}
+        off = 0
+        for name, size in (("coefs", st.blocks * 128), ("qt", n * 192 * 2), ("infos", n * INFO_LEN * 4),
+                           ("coef_blocks", n * 8), ("out_off", n * 8)):
+            sec[name] = off
+            off = _align(off + size)
+        st.sections, st.nbytes, st.infos = sec, off, inf
+        st.out_off = out_off
+        slot = self.next_slot
+        self.next_slot ^= 1
+        st.slot = slot
+        if self.copied[slot] is not None:
+            self.copied[slot].synchronize()  # the previous H2D from this slot has finished
+        if self.buf[slot] is None or self.buf[slot].numel() < off:
+            self.buf[slot] = torch.empty(max(off, 1 << 20) * 5 // 4, dtype=torch.uint8).pin_memory()
+        host = self.buf[slot].numpy()
+        base = host.ctypes.data
+        host[sec["infos"]:sec["infos"] + n * INFO_LEN * 4] = inf.view(np.uint8).reshape(-1)
+        host[sec["coef_blocks"]:sec["coef_blocks"] + n * 8] = coef_blocks.view(np.uint8)
+        host[sec["out_off"]:sec["out_off"] + n * 8] = out_off.view(np.uint8)
+
+        def entropy(k):
+            d = datas[st.index[k]]
+            return lib.mmf_jpeg_entropy(d, len(d), base + sec["coefs"] + int(coef_blocks[k]) * 128,
+                                        base + sec["qt"] + k * 384)
+        rcs = list(self._pool.map(entropy, range(n))) if n > 1 else [entropy(0)]
+        bad = [k for k, rc in enumerate(rcs) if rc != 0]
+        if bad:  # (a header that parsed but a scan that did not: never seen; decode those on the host)
+            raise hip.MMFError(f"mmf_jpeg_entropy failed for chunk positions {[st.index[k] for k in bad]}")
+        return st
+
+
+def device_windows(engine, stager: JpegStager, st: Staged):
+    """Device half: H2D of the staged coefficients, reconstruction to RGBX, both towers' 224x224
+    windows (Pillow-exact) -> (eff, clp) uint8 [n,224,224,3] device tensors for st.index."""
+    lib, dev = engine.lib, engine.device
+    n = len(st.index)
+    src = stager.buf[st.slot][:st.nbytes].to(dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    stager.copied[st.slot] = ev
+    sec = st.sections
+    p = src.data_ptr()
+    need = st.pixels * 4 + st.blocks * 64
+    if getattr(engine, "_jpeg_dev", None) is None or engine._jpeg_dev.numel() < need:
+        engine._jpeg_dev = torch.empty(need * 5 // 4, dtype=torch.uint8, device=dev)
+    rgbx = engine._jpeg_dev.data_ptr()
+    samples = rgbx + st.pixels * 4
+    hip.check(lib.mmf_jpeg_reconstruct(engine.h, p + sec["coefs"], p + sec["qt"], p + sec["coef_blocks"],
+                                       p + sec["infos"], p + sec["out_off"], n, st.max_blocks, st.max_pixels,
+                                       samples, rgbx, hip.stream_ptr()), "mmf_jpeg_reconstruct")
+    wh = np.ascontiguousarray(st.infos[:, :2]).reshape(-1)
+    eff = torch.empty((n, 224, 224, 3), dtype=torch.uint8, device=dev)
+    clp = torch.empty((n, 224, 224, 3), dtype=torch.uint8, device=dev)
+    hip.check(lib.mmf_resize_pil(engine.h, rgbx, st.out_off.ctypes.data_as(ctypes.c_void_p),
+                                 wh.ctypes.data_as(ctypes.c_void_p), n, 4, hip.ptr(eff), hip.ptr(clp),
+                                 hip.stream_ptr()), "mmf_resize_pil")
+    return eff, clp
+
+
+def device_rgb(engine, stager: JpegStager, st: Staged) -> List[np.ndarray]:
+    """Decoded pixels only (tests / tools): [h][w][3] uint8 host arrays for st.index."""
+    dev = engine.device
+    src = stager.buf[st.slot][:st.nbytes].to(dev)
+    sec = st.sections
+    p = src.data_ptr()
+    n = len(st.index)
+    out = torch.empty(st.pixels * 4 + st.blocks * 64, dtype=torch.uint8, device=dev)
+    hip.check(engine.lib.mmf_jpeg_reconstruct(engine.h, p + sec["coefs"], p + sec["qt"], p + sec["coef_blocks"],
+                                              p + sec["infos"], p + sec["out_off"], n, st.max_blocks, st.max_pixels,
+                                              out.data_ptr() + st.pixels * 4, out.data_ptr(), hip.stream_ptr()),
+              "mmf_jpeg_reconstruct")
+    host = out[:st.pixels * 4].cpu().numpy()
+    res = []
+    for k in range(n):
+        w, h = int(st.infos[k, 0]), int(st.infos[k, 1])
+        o = int(st.out_off[k])
+        res.append(host[o:o + w * h * 4].reshape(h, w, 4)[..., :3].copy())
+    return res

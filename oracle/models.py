@@ -10,9 +10,9 @@ functional PyTorch fp32 on CPU over a plain ``{state-dict name: tensor}`` mappin
   56-155 embeddings, 158-251 self-attention, 329-399 layer, 401-465 encoder), called from
   ``MultiModalMisinfoDetector.forward_text`` (misinfo_forensics.py:92-100).
 * Dual heads: misinfo_forensics.py:57-69, 97-98, softmax[:,1] 342-347.
-* EfficientNet-B0: torchvision ``efficientnet_b0`` (unpinned; torchvision is not installed —
-  SURVEY.md §8c) with the 2-class classifier of misinfo_forensics.py:72-76, preprocessing
-  misinfo_forensics.py:249-253.
+* EfficientNet-B0: torchvision ``efficientnet_b0`` (proxy-pinned, see "Parity status" below;
+  torchvision is not installed — SURVEY.md §8c) with the 2-class classifier of
+  misinfo_forensics.py:72-76, preprocessing misinfo_forensics.py:249-253.
 * CLIP ViT-B/32: HF ``CLIPModel`` (TF:models/clip/modeling_clip.py 138-219 embeddings,
   280-385 attention/MLP/layer, 494-590 text tower incl. EOS pooling 561-582, 594-657 vision
   tower, 683-751 get_*_features).

@@ -1,0 +1,66 @@
+"""JPEG test inputs shared by tests/test_jpeg_cpu.py and tests/test_gpu_jpeg.py: encoded in the test
+run by Pillow's encoder (deterministic), covering the decoder paths -- 4:2:0 / 4:2:2 / 4:4:4 /
+grayscale, odd sizes and 1x1, optimised Huffman tables, restart intervals (per blocks and per MCU
+rows), low and high quality -- plus files the device path must hand back to Pillow."""
+import io
+
+import numpy as np
+from PIL import Image
+
+
+def photo_like(w, h, seed=0):
+    """Smooth gradients + texture + noise: coefficient statistics of a photo, not of white noise."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = np.stack([(xx * 3 + yy) % 256, (yy * 2 + 40) % 256, ((xx + yy) * 5) % 256], -1).astype(np.float64)
+    tex = 40 * np.sin(xx[..., None] / 3.0 + np.array([0, 1, 2])) * np.cos(yy[..., None] / 5.0)
+    a = base * 0.75 + tex + rng.normal(0, 12, (h, w, 3))
+    return np.clip(a, 0, 255).astype(np.uint8)
+
+
+def encode(a, mode="RGB", **kw):
+    im = Image.fromarray(a)
+    if mode != "RGB":
+        im = im.convert(mode)
+    b = io.BytesIO()
+    im.save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+# (w, h, mode, save kwargs)
+SUPPORTED = [
+    (64, 48, "RGB", dict(quality=90, subsampling=2)),
+    (65, 49, "RGB", dict(quality=75, subsampling=2)),
+    (33, 17, "RGB", dict(quality=95, subsampling=1)),
+    (40, 40, "RGB", dict(quality=50, subsampling=0)),
+    (31, 23, "L", dict(quality=80)),
+    (97, 61, "RGB", dict(quality=85, subsampling=2, optimize=True)),
+    (8, 8, "RGB", dict(quality=100, subsampling=2)),
+    (1, 1, "RGB", dict(quality=90)),
+    (3, 5, "RGB", dict(quality=10, subsampling=2)),
+    (300, 200, "RGB", dict(quality=90, subsampling=2, restart_marker_blocks=7)),
+    (301, 203, "RGB", dict(quality=70, subsampling=1, restart_marker_rows=1)),
+    (70, 50, "L", dict(quality=60, restart_marker_blocks=3)),
+    (127, 129, "RGB", dict(quality=98, subsampling=0, optimize=True)),
+]
+LARGE = [(640, 480, "RGB", dict(quality=90, subsampling=2)), (1023, 767, "RGB", dict(quality=80, subsampling=1))]
+
+
+def supported_jpegs(large=False):
+    cases = SUPPORTED + (LARGE if large else [])
+    return [(f"{w}x{h}-{m}-{kw}", encode(photo_like(w, h, seed=w * 31 + h), m, **kw)) for w, h, m, kw in cases]
+
+
+def unsupported_files():
+    """Files the device path declines (MMF_EUNSUPPORTED or not JPEG): Pillow decodes them."""
+    a = photo_like(48, 40, seed=5)
+    out = [("progressive", encode(a, quality=90, progressive=True)),
+           ("cmyk", encode(a, "CMYK", quality=90))]
+    b = io.BytesIO()
+    Image.fromarray(a).save(b, "PNG")
+    out.append(("png", b.getvalue()))
+    return out
+
+
+def pillow_rgb(data: bytes) -> np.ndarray:
+    return np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
