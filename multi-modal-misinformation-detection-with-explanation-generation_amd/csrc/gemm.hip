@@ -39,7 +39,12 @@ struct Cfg {
 
 MMF_DEV int swz(int row, int kc) { return row * BK + ((kc ^ (row & 7)) << 3); }
 
-template <int BM, int BN, int WGM, int WGN>
+// PF = 2: the global loads of K-step kt + 2 are issued at step kt into a second register set, so
+// two K-steps of compute cover each load's latency instead of one (long-K, few-workgroup launches:
+// the EfficientNet SE-scaled projects, M = B * 49 or B * 196 rows, K = 480 ... 1152)
+// ASC: the A operand carries an SE scale (g.ascale); instantiated apart so that plain launches keep
+// their register budget
+template <int BM, int BN, int WGM, int WGN, int PF = 1, bool ASC = false>
 __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
   using C = Cfg<BM, BN, WGM, WGN>;
   __shared__ __attribute__((aligned(16))) f16_t lds[2 * (BM + BN) * BK];
@@ -64,28 +69,35 @@ __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
   const int M = g.M, N = g.N, K = g.K;
   const int nk = (K + BK - 1) / BK;
 
+  // A chunks are loaded raw with their SE scales (ascale: 8 fp32 per 16-B chunk) and scaled when
+  // they are stored to LDS: the loads stay in flight under the compute phase (scaling at load
+  // time made every K-step wait for its own loads)
   uint4 xr[C::XC], wr[C::WC];
+  float4 sr[ASC ? C::XC : 1][2];
+  uint4 xr2[PF == 2 ? C::XC : 1], wr2[PF == 2 ? C::WC : 1];
+  float4 sr2[PF == 2 && ASC ? C::XC : 1][2];
 
-  auto load_regs = [&](int kt) {
+  auto load_to = [&](int kt, uint4* xd, float4 (*sd)[2], uint4* wd) {
     const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < C::XC; ++i) {
       const int c = tid + 256 * i, row = c >> 3, kc = c & 7;
       const int m = m0 + row, k = k0 + kc * 8;
       uint4 v = make_uint4(0, 0, 0, 0);
+      float4 s0 = make_float4(1.f, 1.f, 1.f, 1.f), s1 = s0;
       if (m < M && k < K) {
         v = *reinterpret_cast<const uint4*>(g.A + (size_t)m * g.lda + k);
-        if (g.ascale) {
-          const float* s = g.ascale + (size_t)(m / g.rows_per_batch) * K + k;
-          const float4 s0 = *reinterpret_cast<const float4*>(s);
-          const float4 s1 = *reinterpret_cast<const float4*>(s + 4);
-          v.x = pack2h(lo_h(v.x) * s0.x, hi_h(v.x) * s0.y);
-          v.y = pack2h(lo_h(v.y) * s0.z, hi_h(v.y) * s0.w);
-          v.z = pack2h(lo_h(v.z) * s1.x, hi_h(v.z) * s1.y);
-          v.w = pack2h(lo_h(v.w) * s1.z, hi_h(v.w) * s1.w);
+        if constexpr (ASC) {
+          const float* sp = g.ascale + (size_t)(m / g.rows_per_batch) * K + k;
+          s0 = *reinterpret_cast<const float4*>(sp);
+          s1 = *reinterpret_cast<const float4*>(sp + 4);
         }
       }
-      xr[i] = v;
+      xd[i] = v;
+      if constexpr (ASC) {
+        sd[i][0] = s0;
+        sd[i][1] = s1;
+      }
     }
 #pragma unroll
     for (int i = 0; i < C::WC; ++i) {
@@ -93,19 +105,27 @@ __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
       const int n = n0 + row, k = k0 + kc * 8;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (n < N && k < K) v = *reinterpret_cast<const uint4*>(g.W + (size_t)n * g.ldw + k);
-      wr[i] = v;
+      wd[i] = v;
     }
   };
-  auto store_lds = [&](int buf) {
+  auto store_from = [&](int buf, const uint4* xs, const float4 (*ss)[2], const uint4* ws) {
 #pragma unroll
     for (int i = 0; i < C::XC; ++i) {
       const int c = tid + 256 * i;
-      *reinterpret_cast<uint4*>(Xs(buf) + swz(c >> 3, c & 7)) = xr[i];
+      uint4 v = xs[i];
+      if constexpr (ASC) {  // SE excitation, rounded to fp16 like the unscaled operand
+        const float4 s0 = ss[i][0], s1 = ss[i][1];
+        v.x = pack2h(lo_h(v.x) * s0.x, hi_h(v.x) * s0.y);
+        v.y = pack2h(lo_h(v.y) * s0.z, hi_h(v.y) * s0.w);
+        v.z = pack2h(lo_h(v.z) * s1.x, hi_h(v.z) * s1.y);
+        v.w = pack2h(lo_h(v.w) * s1.z, hi_h(v.w) * s1.w);
+      }
+      *reinterpret_cast<uint4*>(Xs(buf) + swz(c >> 3, c & 7)) = v;
     }
 #pragma unroll
     for (int i = 0; i < C::WC; ++i) {
       const int c = tid + 256 * i;
-      *reinterpret_cast<uint4*>(Ws(buf) + swz(c >> 3, c & 7)) = wr[i];
+      *reinterpret_cast<uint4*>(Ws(buf) + swz(c >> 3, c & 7)) = ws[i];
     }
   };
 
@@ -115,14 +135,12 @@ __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
 #pragma unroll
     for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_regs(0);
-  store_lds(0);
+  load_to(0, xr, sr, wr);
+  store_from(0, xr, sr, wr);
   __syncthreads();
 
   const int fr = lane & 15, fg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_regs(kt + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       f16x8 wf[C::NI], xf[C::MI];
@@ -141,8 +159,30 @@ __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
 #pragma unroll
         for (int j = 0; j < C::MI; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
     }
-    if (kt + 1 < nk) store_lds(buf ^ 1);
-    __syncthreads();
+  };
+  if constexpr (PF == 2) {
+    // register set A carries the odd K-steps, set B the even ones (>= 2); each set's loads are
+    // issued two compute phases before its LDS store
+    if (nk > 1) load_to(1, xr, sr, wr);
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) load_to(kt + 2, xr2, sr2, wr2);
+      compute(0);
+      if (kt + 1 < nk) store_from(1, xr, sr, wr);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) load_to(kt + 3, xr, sr, wr);
+      compute(1);
+      if (kt + 2 < nk) store_from(0, xr2, sr2, wr2);
+      __syncthreads();
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) load_to(kt + 1, xr, sr, wr);
+      compute(buf);
+      if (kt + 1 < nk) store_from(buf ^ 1, xr, sr, wr);
+      __syncthreads();
+    }
   }
 
   // epilogue: lane holds C[m][n..n+3].  All loads (bias, fp16 residual) are issued before the
@@ -781,10 +821,21 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifndef MMF_GEMM_PF2_K
+#define MMF_GEMM_PF2_K 0  // K from which the 2-deep register prefetch is used (0 = never; A/B builds)
+#endif
 template <int BM, int BN, int WGM, int WGN>
 hipError_t run(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN), dim3(256), 0, s, a, tilesN);
+  const dim3 grid(tilesM * tilesN);
+  const bool pf2 = MMF_GEMM_PF2_K > 0 && a.K >= MMF_GEMM_PF2_K;
+  if (a.ascale) {
+    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2, true>), grid, dim3(256), 0, s, a, tilesN);
+    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 1, true>), grid, dim3(256), 0, s, a, tilesN);
+  } else {
+    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2>), grid, dim3(256), 0, s, a, tilesN);
+    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), grid, dim3(256), 0, s, a, tilesN);
+  }
   return hipGetLastError();
 }
 
