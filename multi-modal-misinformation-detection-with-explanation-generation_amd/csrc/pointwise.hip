@@ -161,8 +161,12 @@ template <int KS, int CF>
 hipError_t run_pw(const GemmArgs& a, int nbn, hipStream_t s) {
   constexpr int ROWS = 4 * pw_rpw<KS>() * 16;
   const int nrb = (a.M + ROWS - 1) / ROWS;
-  // persistent in x: about four workgroups per CU across the column blocks
+  // persistent in x: about four workgroups per CU across the column blocks.  gx is a multiple of 8
+  // so that the nbn workgroups (x, 0..nbn-1), which walk the same row blocks, share an XCD (linear
+  // id x + y * gx lands on XCD (x + y * gx) % 8 = x % 8): each A row block is fetched from HBM into
+  // that XCD's L2 once instead of once per column block (N = 672: nbn = 6, gx was 171)
   int gx = (1024 + nbn - 1) / nbn;
+  if (nbn > 1) gx = gx / 8 * 8;
   if (gx > nrb) gx = nrb;
   const dim3 grid(gx, nbn);
   if (a.act == ACT_SILU)
