@@ -65,7 +65,7 @@ def kind_symbol(kind: str) -> str:
         return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi, '0'])}>"
     if m.group(1) == "glds_pipe2":
         return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi, '0'])}>"
-    return f"gemm_f16_kernel<{', '.join(dims)}>"
+    return f"gemm_f16_kernel<{', '.join(dims)}, 1, false>"  # (PF, ASC: plain launches)
 
 
 def pmc_traffic(symbol: str, path: str | None = None) -> float | None:
