@@ -135,6 +135,7 @@ struct Options {
   int pw32_mfma = 1;    // fp32 tower's 1x1 convs on the fp32-input MFMA (1) or the fp32-FMA VALU kernel (0)
   int gemm_wide = 0;    // 256x384 tiles where they save a persistent round (gemm.hip glds_pick; step A/B: a tie)
   int dw_persist = 0;   // persistent depthwise kernels with the next tile's loads in flight (effnet.hip; A/B: slower)
+  int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
@@ -148,6 +149,7 @@ const OptName kOptNames[] = {
     {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},            {"gemm_ring", &Options::gemm_ring, "MMF_GEMM_RING"},
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
+    {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -1096,7 +1098,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k,
                    (double)B * b.cexp * 2 * ((double)H * W + (double)Ho * Wo));
       HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s,
-                            h->opt.dw_ct | (h->opt.dw_persist ? 2 : 0)));
+                            h->opt.dw_ct | (h->opt.dw_persist ? 2 : 0) | (h->opt.dw_cw32 ? 8 : 0)));
     }
     ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, (double)B * b.cexp * 4 * (nch + 1));
     HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s));

@@ -477,7 +477,10 @@ __global__ __launch_bounds__(256, 3) void dwconv_persist_kernel(const f16_t* __r
 #define MMF_EDW_PF 1
 #endif
 template <int K, int S, int KS, int TT, int R>
-__global__ __launch_bounds__(256, 3) void expand_dw_kernel(const f16_t* __restrict__ x, int Cin,
+#ifndef MMF_EDW_MINB1
+#define MMF_EDW_MINB1 4  // resident blocks per CU hipcc budgets registers for (KS = 1: stage 3.1 148 -> 128 VGPRs, 4 blocks/CU; -0.9 %)
+#endif
+__global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : 3) void expand_dw_kernel(const f16_t* __restrict__ x, int Cin,
                                                         const f16_t* __restrict__ we, const float* __restrict__ be,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         f16_t* __restrict__ out, float* __restrict__ pool_part, int H,
@@ -1032,7 +1035,10 @@ hipError_t launch_effnet_stem32(const uint8_t* img, const float* x, const float*
 #endif
 
 // tile edge: the largest divisor of the output edge up to 16 (stride 1) / 8 (stride 2)
-static void dw_geometry(int H, int W, int C, int stride, int* T_, int* CW_, int* tiles_x_, int* ntiles_) {
+// narrow = true (standalone depthwise launches, option dw_cw32): 32-channel groups where C allows, for
+// 24 KB instead of 36 KB of LDS per 14x14 k5 block (more resident blocks); the tile count is unchanged
+static void dw_geometry(int H, int W, int C, int stride, int* T_, int* CW_, int* tiles_x_, int* ntiles_,
+                        bool narrow = false) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int cap = stride == 1 ? 16 : 8;
   int T = 1;
@@ -1040,7 +1046,7 @@ static void dw_geometry(int H, int W, int C, int stride, int* T_, int* CW_, int*
     if (Ho % t == 0) { T = t; break; }
   const int tx = (Wo + T - 1) / T, ty = (Ho + T - 1) / T;
   *T_ = T;
-  *CW_ = (C % 48 == 0) ? 48 : 32;
+  *CW_ = (C % 48 == 0 && !(narrow && C % 32 == 0)) ? 48 : 32;
   *tiles_x_ = tx;
   *ntiles_ = tx * ty;
 }
@@ -1054,7 +1060,7 @@ int dwconv_nchunks(int H, int W, int C, int stride) {
 hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16_t* out, float* pool_part, int B,
                          int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct) {
   int T, CW, tiles_x, ntiles;
-  dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
+  dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles, (ct & 8) != 0);
   if (C % CW) return hipErrorInvalidValue;
   *nchunks_out = ntiles;
   const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8);
@@ -1095,6 +1101,11 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
   }
   if (ct & 1) {  // bit 0 clear: runtime-geometry kernels only (A/B option "dw_ct")
     MMF_DWCT(3, 1, 16, 32, MMF_R_D16)
+    MMF_DWCT(3, 1, 14, 32, MMF_R_D14)
+    MMF_DWCT(5, 1, 14, 32, MMF_R_D14)
+    MMF_DWCT(5, 1, 7, 32, MMF_R_D7)
+    MMF_DWCT(3, 1, 7, 32, MMF_R_D7)
+    MMF_DWCT(5, 2, 7, 32, MMF_R_D7)
     MMF_DWCT(3, 1, 14, 48, MMF_R_D14)
     MMF_DWCT(5, 1, 14, 48, MMF_R_D14)
     MMF_DWCT(3, 2, 8, 48, MMF_R_D8)

@@ -166,14 +166,20 @@ def test_batch_invariance_full_size(engine, det_sd):
 def test_fused_expand_dwconv_bit_identical(engine):
     """The fused MBConv front (1x1 expand computed per tile into the depthwise conv's LDS tile)
     produces bit-identical EfficientNet outputs to the separate expand GEMM + depthwise launches
-    (same MFMA operand order over K, same bias / SiLU / fp16 rounding), on a full 256 batch."""
+    (same MFMA operand order over K, same bias / SiLU / fp16 rounding), on a full 256 batch.  The
+    separate depthwise launches run the fused kernel's 48-channel groups (dw_cw32 = 0), so the SE pool
+    partials are summed in the same order too."""
     import mmf_amd.synthetic as syn
     imgs = syn.images(256, 17)
-    engine.set_option("fuse_expand", 0)
-    lg0, _ = engine.effnet_forward(imgs)
-    engine.set_option("fuse_expand", 1)
-    lg1, _ = engine.effnet_forward(imgs)
-    torch.cuda.synchronize()
+    engine.set_option("dw_cw32", 0)
+    try:
+        engine.set_option("fuse_expand", 0)
+        lg0, _ = engine.effnet_forward(imgs)
+        engine.set_option("fuse_expand", 1)
+        lg1, _ = engine.effnet_forward(imgs)
+        torch.cuda.synchronize()
+    finally:
+        engine.set_option("dw_cw32", 1)
     assert torch.equal(lg0, lg1)
 
 
