@@ -3,7 +3,7 @@ replayed hipGraph (torch.cuda.CUDAGraph capture of mmf_analyze_batch, tower stre
 joined inside the capture), interleaved rounds, and checks that the replay's outputs are the eager
 outputs bit for bit.
 
-    python tools/graph_probe.py [--rounds 5 --iters 20]
+    python tools/graph_probe.py [--rounds 5 --iters 20 --batch 256]
 """
 import argparse
 import os
@@ -20,11 +20,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=256)
     a = ap.parse_args()
     import bench
     import mmf_amd.weights as W
     from mmf_amd.engine import Engine
-    B = 256
+    B = a.batch
     eng = Engine(0, W.synthetic_detector_state(0), W.synthetic_clip_state(0), max_batch=B)
     t = bench.build_inputs(eng, B, 0)
     out = eng.alloc_outputs(B)
