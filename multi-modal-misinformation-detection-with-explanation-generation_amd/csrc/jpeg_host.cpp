@@ -132,6 +132,9 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
       j.ncomp = s[5];
       if (j.ncomp != 1 && j.ncomp != 3) return MMF_EUNSUPPORTED;
       if (sl < 6 + 3 * j.ncomp || j.width <= 0 || j.height <= 0) return MMF_EINVAL;
+      // Pillow refuses images past 2 x MAX_IMAGE_PIXELS (178,956,970 px) as decompression bombs; the
+      // staging buffers are sized from this header, so larger claims are declined here too
+      if ((int64_t)j.width * j.height > 178956970) return MMF_EUNSUPPORTED;
       for (int i = 0; i < j.ncomp; ++i) {
         j.comp[i].id = s[6 + 3 * i];
         j.comp[i].h = s[7 + 3 * i] >> 4;
