@@ -130,16 +130,32 @@ int mmf_jpeg_header(const uint8_t* data, int64_t nbytes, int32_t* info);
  * (natural order, components back to back) and the components' quantisation tables qt[c][64]
  * (natural order, uint16).  Replaces libjpeg's decode_mcu (jdhuff.c). */
 int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* coefs, uint16_t* qt);
-/* Device: B images' coefficients and tables -> uint8 RGBX pixels, bit-exact with Pillow's decoder.
- * Every pointer is DEVICE memory: coefs int16 (image i's blocks from block offset coef_blocks[i]),
- * qt uint16 [B][3][64] (mmf_jpeg_entropy's tables), infos int32 [B][MMF_JPEG_INFO_LEN]
+/* Host-only, thread-safe: the same coefficients packed for the H2D copy (~2.8x fewer bytes than the
+ * dense planes on photos): one record per block -- uint64 mask of its nonzero ZIGZAG positions, then
+ * their int16 values in zigzag order, padded to 8 bytes -- in decode order after an all-zero record
+ * at offset 0; block_off[b] = byte offset of block b's record (b in the dense layout's order, padding
+ * blocks -> 0).  `out` must hold mmf_jpeg_packed_bound(blocks) bytes (MMF_ERANGE otherwise); *used =
+ * bytes written.  This is the format mmf_jpeg_reconstruct reads. */
+int64_t mmf_jpeg_packed_bound(int32_t blocks);
+int mmf_jpeg_entropy_packed(const uint8_t* data, int64_t nbytes, uint8_t* out, int64_t cap, uint32_t* block_off,
+                            uint16_t* qt, int64_t* used);
+/* Host-only, thread-safe: mmf_jpeg_entropy_packed for a batch staged by several threads.  Decodes
+ * into a per-thread scratch, reserves 8-aligned room by an atomic add on *cursor, sets *rec_off to it
+ * and copies the records to dst + *rec_off -- or returns MMF_ERANGE (room still reserved) when they
+ * do not fit in dst_cap bytes: grow dst and place that image again (mmf_jpeg_entropy_packed). */
+int mmf_jpeg_stage_packed(const uint8_t* data, int64_t nbytes, uint8_t* dst, int64_t dst_cap, int64_t* cursor,
+                          uint32_t* block_off, uint16_t* qt, int64_t* rec_off);
+/* Device: B images' packed coefficients and tables -> uint8 RGBX pixels, bit-exact with Pillow's
+ * decoder.  Every pointer is DEVICE memory: packed = the images' mmf_jpeg_entropy_packed records
+ * (image i's at byte offset pk_off[i]), block_off uint32 = their block-offset tables concatenated
+ * (image i's from index coef_blocks[i]), qt uint16 [B][3][64], infos int32 [B][MMF_JPEG_INFO_LEN]
  * (mmf_jpeg_header's), out_offsets int64 [B] (byte offset of image i's [h][w][4] RGBX pixels in
- * out_rgbx; X = 255), samples = scratch of 64 * sum(blocks) bytes (component sample planes).
- * max_blocks / max_pixels = the largest blocks / width * height over the B images (grid sizes).
- * Feeds mmf_resize_pil (pixel_bytes 4).  Asynchronous on `stream`. */
-int mmf_jpeg_reconstruct(mmf_handle* h, const int16_t* coefs, const uint16_t* qt, const int64_t* coef_blocks,
-                         const int32_t* infos, const int64_t* out_offsets, int B, int max_blocks, int max_pixels,
-                         uint8_t* samples, uint8_t* out_rgbx, void* stream);
+ * out_rgbx; X = 255), samples = scratch of 64 * sum(blocks) bytes (component sample planes, image i's
+ * from 64 * coef_blocks[i]).  max_blocks / max_pixels = the largest blocks / width * height over the B
+ * images (grid sizes).  Feeds mmf_resize_pil (pixel_bytes 4).  Asynchronous on `stream`. */
+int mmf_jpeg_reconstruct(mmf_handle* h, const uint8_t* packed, const uint32_t* block_off, const int64_t* pk_off,
+                         const uint16_t* qt, const int64_t* coef_blocks, const int32_t* infos, const int64_t* out_offsets,
+                         int B, int max_blocks, int max_pixels, uint8_t* samples, uint8_t* out_rgbx, void* stream);
 
 /* 1 if a width x height image fits mmf_resize_pil's tap budget in both geometries (bicubic CLIP:
  * shortest side <= ~5264 px; bilinear EfficientNet: either side <= ~10528 px), else 0.  Host-only,

@@ -1635,17 +1635,17 @@ bool plan_job(int w, int h, int geom, ResizeJob* J) {
 }
 }  // namespace
 
-int mmf_jpeg_reconstruct(mmf_handle* h, const int16_t* coefs, const uint16_t* qt, const int64_t* coef_blocks,
-                         const int32_t* infos, const int64_t* out_offsets, int B, int max_blocks, int max_pixels,
-                         uint8_t* samples, uint8_t* out_rgbx, void* stream) {
+int mmf_jpeg_reconstruct(mmf_handle* h, const uint8_t* packed, const uint32_t* block_off, const int64_t* pk_off,
+                         const uint16_t* qt, const int64_t* coef_blocks, const int32_t* infos, const int64_t* out_offsets,
+                         int B, int max_blocks, int max_pixels, uint8_t* samples, uint8_t* out_rgbx, void* stream) {
   if (!h || B < 0) return fail(MMF_EINVAL, "null argument");
   if (B == 0) return 0;
-  if (!coefs || !qt || !coef_blocks || !infos || !out_offsets || !samples || !out_rgbx)
+  if (!packed || !block_off || !pk_off || !qt || !coef_blocks || !infos || !out_offsets || !samples || !out_rgbx)
     return fail(MMF_EINVAL, "null argument");
   if (max_blocks <= 0 || max_pixels <= 0) return fail(MMF_EINVAL, "max_blocks / max_pixels must be positive");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(launch_jpeg_reconstruct(coefs, qt, coef_blocks, infos, out_offsets, B, max_blocks, max_pixels, samples,
-                                 out_rgbx, (hipStream_t)stream));
+  HIPCHK(launch_jpeg_reconstruct(packed, block_off, pk_off, qt, coef_blocks, infos, out_offsets, B, max_blocks,
+                                 max_pixels, samples, out_rgbx, (hipStream_t)stream));
   return 0;
 }
 

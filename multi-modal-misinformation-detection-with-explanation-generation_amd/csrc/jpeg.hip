@@ -4,11 +4,12 @@
 // output pixel the fancy chroma upsampling (jdsample.c h2v1 / h2v2 triangle filters, edge samples
 // replicated as jdmainct.c's context rows do) and YCbCr -> RGB (jdcolor.c tables, SCALEBITS 16),
 // written as RGBX for mmf_resize_pil.
-//   jpeg_idct_kernel : one thread per block; 128-B coefficient block in, 8 rows of 8 samples out
-//                      (adjacent threads = adjacent blocks of a block row: coalesced row stores)
+//   jpeg_idct_kernel : one thread per block; its packed record in (mask + nonzero values, ~48 B on
+//                      photos instead of 128), 8 rows of 8 samples out (adjacent threads = adjacent
+//                      blocks of a block row: coalesced row stores)
 //   jpeg_color_kernel: one thread per output pixel, one 4-B RGBX store
-// Both are HBM / latency-bound byte work (a 640x480 4:2:0 image: 0.92 MB of coefficients, 0.46 MB
-// of samples, 1.2 MB of RGBX).
+// Both are HBM / latency-bound byte work (a 640x480 4:2:0 q90 image: 0.35 MB of packed coefficients
+// -- 0.92 MB dense --, 0.46 MB of samples, 1.2 MB of RGBX).
 #include "common.h"
 #include "kernels.h"
 
@@ -63,8 +64,17 @@ MMF_DEV uint32_t range_limit_idct(int v) {
   return (uint32_t)(m < 128 ? m + 128 : m < 512 ? 255 : m < 896 ? 0 : m - 896);
 }
 
-// grid (ceil(max blocks / 256), B); block 256
-__global__ __launch_bounds__(256) void jpeg_idct_kernel(const int16_t* __restrict__ coefs, const uint16_t* __restrict__ qt,
+// zigzag position -> natural (row-major) index (ITU T.81 Figure A.6)
+__constant__ constexpr uint8_t kZigzag[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// grid (ceil(max blocks / 256), B); block 256.  Coefficients arrive packed (mmf_jpeg_entropy_packed):
+// the block's record = uint64 mask of nonzero zigzag positions + their int16 values in zigzag order.
+__global__ __launch_bounds__(256) void jpeg_idct_kernel(const uint8_t* __restrict__ packed,
+                                                        const uint32_t* __restrict__ block_off,
+                                                        const int64_t* __restrict__ pk_off, const uint16_t* __restrict__ qt,
                                                         const int64_t* __restrict__ coef_blocks,
                                                         const int32_t* __restrict__ infos, uint8_t* __restrict__ samples) {
   const int img = blockIdx.y;
@@ -81,18 +91,33 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const int16_t* __restric
   const int bw = inf[5 + 2 * c];
   const int by = rem / bw, bx = rem - by * bw;
   const int64_t b0 = coef_blocks[img];
-  const int16_t* cf = coefs + (b0 + blk) * 64;
+  const uint8_t* rec = packed + pk_off[img] + block_off[b0 + blk];
+  const uint2 mw = *reinterpret_cast<const uint2*>(rec);
+  const uint64_t mask = (uint64_t)mw.x | (uint64_t)mw.y << 32;
+  const int16_t* val = reinterpret_cast<const int16_t*>(rec + 8);
   const uint16_t* q = qt + (size_t)img * 192 + c * 64;
-  int d[64];
+  int qn[64];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const uint4 v = *reinterpret_cast<const uint4*>(cf + i * 8);
     const uint4 w0 = *reinterpret_cast<const uint4*>(q + i * 8);
-    const uint32_t cv[4] = {v.x, v.y, v.z, v.w}, qv[4] = {w0.x, w0.y, w0.z, w0.w};
+    const uint32_t qv[4] = {w0.x, w0.y, w0.z, w0.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      d[i * 8 + 2 * k] = (int)(int16_t)(cv[k] & 0xFFFF) * (int)(qv[k] & 0xFFFF);
-      d[i * 8 + 2 * k + 1] = (int)(int16_t)(cv[k] >> 16) * (int)(qv[k] >> 16);
+      qn[i * 8 + 2 * k] = (int)(qv[k] & 0xFFFF);
+      qn[i * 8 + 2 * k + 1] = (int)(qv[k] >> 16);
+    }
+  }
+  // dequantise: zigzag position k -> natural index kZigzag[k] (compile-time per unrolled k)
+  int d[64];
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    const int nat = kZigzag[k];
+    if ((mask >> k) & 1) {
+      d[nat] = (int)val[n] * qn[nat];
+      ++n;
+    } else {
+      d[nat] = 0;
     }
   }
   // pass 1: columns (d[v * 8 + u], inputs down a column) -> workspace, descaled by CONST_BITS - PASS1_BITS
@@ -176,13 +201,14 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const int64_t* __restri
 
 }  // namespace
 
-hipError_t launch_jpeg_reconstruct(const int16_t* coefs, const uint16_t* qt, const int64_t* coef_blocks,
-                                   const int32_t* infos, const int64_t* out_offsets, int B, int max_blocks,
-                                   int max_pixels, uint8_t* samples, uint8_t* out, hipStream_t s) {
+hipError_t launch_jpeg_reconstruct(const uint8_t* packed, const uint32_t* block_off, const int64_t* pk_off,
+                                   const uint16_t* qt, const int64_t* coef_blocks, const int32_t* infos,
+                                   const int64_t* out_offsets, int B, int max_blocks, int max_pixels, uint8_t* samples,
+                                   uint8_t* out, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (max_blocks <= 0 || max_pixels <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((max_blocks + 255) / 256, B), dim3(256), 0, s, coefs, qt, coef_blocks,
-                     infos, samples);
+  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((max_blocks + 255) / 256, B), dim3(256), 0, s, packed, block_off, pk_off, qt,
+                     coef_blocks, infos, samples);
   hipLaunchKernelGGL(jpeg_color_kernel, dim3((max_pixels + 255) / 256, B), dim3(256), 0, s, coef_blocks, infos,
                      samples, out, out_offsets);
   return hipGetLastError();

@@ -15,6 +15,7 @@
 // block grid; blocks outside a single-component scan's extent stay zero, as in libjpeg).
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "../../include/mmf_hip.h"
 
@@ -350,40 +351,39 @@ extern "C" int mmf_jpeg_header(const uint8_t* data, int64_t nbytes, int32_t* inf
   return 0;
 }
 
-extern "C" int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* coefs, uint16_t* qt) {
-  if (!data || !coefs || !qt) return MMF_EINVAL;
-  Jpeg j;
-  const int rc = parse(data, nbytes, j);
-  if (rc) return rc;
-  int16_t* plane[3];
+namespace {
+
+// Entropy decoding of every block of the scan(s); on_block(global block index, dc, ac, pred) decodes
+// one block into the caller's representation, on_skip(global block index) marks a block of the
+// MCU-padded grid that no scan codes (non-interleaved scans cover only the component's extent).
+template <class OnBlock, class OnSkip>
+int walk_blocks(Jpeg& j, OnBlock&& on_block, OnSkip&& on_skip) {
+  int64_t base[3];
   int bw[3], bh[3];
   int64_t off = 0;
   for (int c = 0; c < j.ncomp; ++c) {
     bw[c] = j.mcux * j.comp[c].h;
     bh[c] = j.mcuy * j.comp[c].v;
-    plane[c] = coefs + off * 64;
+    base[c] = off;
     off += (int64_t)bw[c] * bh[c];
-    memcpy(qt + 64 * c, j.qt[j.comp[c].tq], 64 * sizeof(uint16_t));
   }
   Bits b{j.scan, j.end};
   int pred[3] = {0, 0, 0};
   const int ri = j.restart;
   int64_t unit = 0;
   if (j.ncomp == 1) {
-    // non-interleaved: the component's own block extent, in raster order
     const Comp& c = j.comp[0];
     const int cw = (j.width * c.h + j.hmax - 1) / j.hmax, ch = (j.height * c.v + j.vmax - 1) / j.vmax;
     const int nbx = (cw + 7) / 8, nby = (ch + 7) / 8;
-    // blocks of the MCU-padded grid outside the component's extent are never coded: zero
     for (int by = 0; by < bh[0]; ++by)
-      for (int bx = (by < nby ? nbx : 0); bx < bw[0]; ++bx) memset(plane[0] + ((int64_t)by * bw[0] + bx) * 64, 0, 128);
+      for (int bx = (by < nby ? nbx : 0); bx < bw[0]; ++bx) on_skip((int64_t)by * bw[0] + bx);
     for (int by = 0; by < nby; ++by)
       for (int bx = 0; bx < nbx; ++bx, ++unit) {
         if (ri && unit && unit % ri == 0) {
           b.restart();
           pred[0] = 0;
         }
-        decode_block(b, j.dc[c.td], j.ac[c.ta], pred[0], plane[0] + ((int64_t)by * bw[0] + bx) * 64);
+        on_block(b, (int64_t)by * bw[0] + bx, j.dc[c.td], j.ac[c.ta], pred[0]);
       }
     return 0;
   }
@@ -398,9 +398,118 @@ extern "C" int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* co
         const Comp& c = j.comp[ci];
         for (int yy = 0; yy < c.v; ++yy)
           for (int xx = 0; xx < c.h; ++xx)
-            decode_block(b, j.dc[c.td], j.ac[c.ta], pred[ci],
-                         plane[ci] + ((int64_t)(my * c.v + yy) * bw[ci] + mx * c.h + xx) * 64);
+            on_block(b, base[ci] + (int64_t)(my * c.v + yy) * bw[ci] + mx * c.h + xx, j.dc[c.td], j.ac[c.ta],
+                     pred[ci]);
       }
     }
+  return 0;
+}
+
+// Packed block record (mmf_jpeg_entropy_packed): uint64 mask of the nonzero ZIGZAG positions, then
+// their int16 values in zigzag (= decode) order, padded to 8 bytes.  Returns the record's bytes.
+inline int decode_block_packed(Bits& b, const Huff& dc, const Huff& ac, int& pred, uint8_t* rec) {
+  uint64_t mask = 0;
+  int16_t* val = reinterpret_cast<int16_t*>(rec + 8);
+  int n = 0;
+  int t = decode_sym(b, dc);
+  int diff = 0;
+  if (t) {
+    if (b.n < t) b.fill();
+    diff = extend(b.get(t), t);
+  }
+  pred += diff;
+  if (pred) {
+    mask = 1;
+    val[n++] = (int16_t)pred;
+  }
+  for (int k = 1; k < 64; ++k) {
+    if (b.n < 16) b.fill();
+    const int32_t f = ac.acfast[b.peek(kLook)];
+    int v;
+    if (f) {
+      k += (f >> 8) & 15;
+      b.skip(f & 0xFF);
+      v = f >> 16;
+    } else {
+      const int rs = decode_sym(b, ac);
+      const int r = rs >> 4, sz = rs & 15;
+      if (!sz) {
+        if (r != 15) break;
+        k += 15;
+        continue;
+      }
+      k += r;
+      if (b.n < sz) b.fill();
+      v = extend(b.get(sz), sz);
+    }
+    if (k > 63) break;  // corrupt run past the block: libjpeg drops the coefficient
+    mask |= 1ull << k;  // (k only grows: each position is written at most once)
+    val[n++] = (int16_t)v;
+  }
+  memcpy(rec, &mask, 8);
+  for (int i = n; i & 3; ++i) val[i] = 0;  // deterministic padding
+  return (8 + 2 * n + 7) & ~7;
+}
+
+}  // namespace
+
+extern "C" int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* coefs, uint16_t* qt) {
+  if (!data || !coefs || !qt) return MMF_EINVAL;
+  Jpeg j;
+  const int rc = parse(data, nbytes, j);
+  if (rc) return rc;
+  for (int c = 0; c < j.ncomp; ++c) memcpy(qt + 64 * c, j.qt[j.comp[c].tq], 64 * sizeof(uint16_t));
+  return walk_blocks(
+      j, [&](Bits& b, int64_t gb, const Huff& dc, const Huff& ac, int& pred) { decode_block(b, dc, ac, pred, coefs + gb * 64); },
+      [&](int64_t gb) { memset(coefs + gb * 64, 0, 128); });
+}
+
+extern "C" int64_t mmf_jpeg_packed_bound(int32_t blocks) { return 8 + (int64_t)blocks * (8 + 128); }
+
+extern "C" int mmf_jpeg_entropy_packed(const uint8_t* data, int64_t nbytes, uint8_t* out, int64_t cap,
+                                       uint32_t* block_off, uint16_t* qt, int64_t* used) {
+  if (!data || !out || !block_off || !qt || !used) return MMF_EINVAL;
+  Jpeg j;
+  const int rc = parse(data, nbytes, j);
+  if (rc) return rc;
+  int64_t blocks = 0;
+  for (int c = 0; c < j.ncomp; ++c) {
+    memcpy(qt + 64 * c, j.qt[j.comp[c].tq], 64 * sizeof(uint16_t));
+    blocks += (int64_t)j.mcux * j.comp[c].h * j.mcuy * j.comp[c].v;
+  }
+  if (cap < mmf_jpeg_packed_bound((int32_t)blocks) || mmf_jpeg_packed_bound((int32_t)blocks) > 0xFFFFFFFFll)
+    return MMF_ERANGE;
+  memset(out, 0, 8);  // record 0: the all-zero block (padding blocks point here)
+  int64_t cur = 8;
+  walk_blocks(
+      j,
+      [&](Bits& b, int64_t gb, const Huff& dc, const Huff& ac, int& pred) {
+        block_off[gb] = (uint32_t)cur;
+        cur += decode_block_packed(b, dc, ac, pred, out + cur);
+      },
+      [&](int64_t gb) { block_off[gb] = 0; });
+  *used = cur;
+  return 0;
+}
+
+extern "C" int mmf_jpeg_stage_packed(const uint8_t* data, int64_t nbytes, uint8_t* dst, int64_t dst_cap,
+                                     int64_t* cursor, uint32_t* block_off, uint16_t* qt, int64_t* rec_off) {
+  if (!data || !dst || !cursor || !block_off || !qt || !rec_off) return MMF_EINVAL;
+  Jpeg j;
+  int rc = parse(data, nbytes, j);
+  if (rc) return rc;
+  int64_t blocks = 0;
+  for (int c = 0; c < j.ncomp; ++c) blocks += (int64_t)j.mcux * j.comp[c].h * j.mcuy * j.comp[c].v;
+  if (blocks > 0x7fffffff) return MMF_ERANGE;
+  const int64_t bound = mmf_jpeg_packed_bound((int32_t)blocks);
+  thread_local std::vector<uint8_t> scratch;  // per caller thread, reused: no page faults per image
+  if ((int64_t)scratch.size() < bound) scratch.resize(bound + bound / 4);
+  int64_t used = 0;
+  rc = mmf_jpeg_entropy_packed(data, nbytes, scratch.data(), (int64_t)scratch.size(), block_off, qt, &used);
+  if (rc) return rc;
+  const int64_t off = __atomic_fetch_add(cursor, (used + 7) & ~7ll, __ATOMIC_RELAXED);
+  *rec_off = off;
+  if (off + used > dst_cap) return MMF_ERANGE;
+  memcpy(dst + off, scratch.data(), used);
   return 0;
 }

@@ -157,9 +157,10 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
 // number of pool-partial chunks launch_dwconv uses for an output of Ho x Wo with C channels
 int dwconv_nchunks(int H, int W, int C, int stride);
 // JPEG reconstruction (jpeg.hip): islow IDCT per block, then fancy upsampling + YCbCr -> RGBX per pixel
-hipError_t launch_jpeg_reconstruct(const int16_t* coefs, const uint16_t* qt, const int64_t* coef_blocks,
-                                   const int32_t* infos, const int64_t* out_offsets, int B, int max_blocks,
-                                   int max_pixels, uint8_t* samples, uint8_t* out, hipStream_t s);
+hipError_t launch_jpeg_reconstruct(const uint8_t* packed, const uint32_t* block_off, const int64_t* pk_off,
+                                   const uint16_t* qt, const int64_t* coef_blocks, const int32_t* infos,
+                                   const int64_t* out_offsets, int B, int max_blocks, int max_pixels, uint8_t* samples,
+                                   uint8_t* out, hipStream_t s);
 
 // Pillow-exact resampling of decoded images to the towers' 224 x 224 windows (resize.hip)
 constexpr int kResizeKMax = 96;  // taps per output coordinate (bicubic support 2 x scale <= 47)

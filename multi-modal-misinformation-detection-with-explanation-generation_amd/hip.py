@@ -34,7 +34,10 @@ SIGNATURES = {
     "mmf_resize_supported": (_I, [_I, _I]),
     "mmf_jpeg_header": (_I, [_P, ctypes.c_int64, _P]),
     "mmf_jpeg_entropy": (_I, [_P, ctypes.c_int64, _P, _P]),
-    "mmf_jpeg_reconstruct": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
+    "mmf_jpeg_packed_bound": (ctypes.c_int64, [ctypes.c_int32]),
+    "mmf_jpeg_entropy_packed": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, _P]),
+    "mmf_jpeg_stage_packed": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, _P, _P]),
+    "mmf_jpeg_reconstruct": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "mmf_set_vault": (_I, [_P, _P, _I, _I]),
     "mmf_set_vault_normalized": (_I, [_P, _P, _I, _I]),
     "mmf_set_vault_titles": (_I, [_P, _P, _P, _I, _I, _P]),

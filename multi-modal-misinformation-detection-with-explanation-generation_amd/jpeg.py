@@ -3,9 +3,10 @@
 The reference decodes every image with `Image.open(path).convert("RGB")`
 (misinfo_forensics.py:255-258) -- Pillow's libjpeg-turbo on one host core.  Here the only serial
 part, marker parsing + Huffman entropy decoding, runs in C on the host threads
-(csrc/jpeg_host.cpp: mmf_jpeg_header / mmf_jpeg_entropy, called through ctypes, which releases the
-GIL) straight into a pinned staging buffer; one H2D copy moves the quantised coefficients, and the
-device reconstructs the pixels (csrc/jpeg.hip: islow IDCT, fancy chroma upsampling, YCbCr -> RGB,
+(csrc/jpeg_host.cpp: mmf_jpeg_header / mmf_jpeg_entropy_packed, called through ctypes, which releases
+the GIL); the quantised coefficients are packed sparse (per block a mask of the nonzero zigzag
+positions + their values: ~0.35 MB for a 640x480 q90 photo instead of 0.92 MB of dense planes) into
+a pinned staging buffer, one H2D copy moves them, and the device reconstructs the pixels (csrc/jpeg.hip: islow IDCT, fancy chroma upsampling, YCbCr -> RGB,
 bit-exact with Pillow) as RGBX images that feed the Pillow-exact resampler (mmf_resize_pil).
 Files the C decoder does not take (progressive, CMYK, 4:4:0, ...) report MMF_EUNSUPPORTED and are
 decoded by Pillow on the host, as before.
@@ -24,6 +25,7 @@ from . import hip
 
 INFO_LEN = 16
 MMF_EUNSUPPORTED = -95
+MMF_ERANGE = -34
 
 
 def read_bytes(item) -> Optional[bytes]:
@@ -43,7 +45,8 @@ def _align(n: int, a: int = 256) -> int:
 
 class Staged:
     """One chunk's entropy-decoded JPEGs in a pinned buffer: which inputs, their header infos and
-    the byte layout of the buffer (coefficients | tables | infos | block offsets | RGBX offsets)."""
+    the byte layout of the buffer (tables | infos | block bases | RGBX offsets | record offsets |
+    block-record offsets | packed records)."""
 
     def __init__(self):
         self.index: List[int] = []  # positions (within the chunk) decoded by the device path
@@ -58,6 +61,8 @@ class Staged:
 class JpegStager:
     """Host half: headers + entropy decoding of a chunk into one of two pinned buffers (the other
     may still be feeding the previous chunk's H2D copy: each slot's copy is fenced by an event)."""
+
+    guess_bytes_per_block = 64  # first sizing of a slot's packed section (grown when a chunk needs more)
 
     def __init__(self, workers: Optional[int] = None):
         self.lib = hip.load()
@@ -96,34 +101,70 @@ class JpegStager:
         st.max_blocks, st.max_pixels = int(blocks.max()), int(pixels.max())
         sec = {}
         off = 0
-        for name, size in (("coefs", st.blocks * 128), ("qt", n * 192 * 2), ("infos", n * INFO_LEN * 4),
-                           ("coef_blocks", n * 8), ("out_off", n * 8)):
+        for name, size in (("qt", n * 192 * 2), ("infos", n * INFO_LEN * 4), ("coef_blocks", n * 8),
+                           ("out_off", n * 8), ("pk_off", n * 8), ("block_off", st.blocks * 4)):
             sec[name] = off
             off = _align(off + size)
-        st.sections, st.nbytes, st.infos = sec, off, inf
+        sec["packed"] = off
+        st.sections, st.infos = sec, inf
         st.out_off = out_off
         slot = self.next_slot
         self.next_slot ^= 1
         st.slot = slot
         if self.copied[slot] is not None:
             self.copied[slot].synchronize()  # the previous H2D from this slot has finished
-        if self.buf[slot] is None or self.buf[slot].numel() < off:
-            self.buf[slot] = torch.empty(max(off, 1 << 20) * 5 // 4, dtype=torch.uint8).pin_memory()
+        # the packed records' size is known only after decoding: start from ~half the dense size
+        guess = off + st.blocks * self.guess_bytes_per_block
+        if self.buf[slot] is None or self.buf[slot].numel() < guess:
+            self.buf[slot] = torch.empty(max(guess, 1 << 16) * 5 // 4, dtype=torch.uint8).pin_memory()
         host = self.buf[slot].numpy()
-        base = host.ctypes.data
         host[sec["infos"]:sec["infos"] + n * INFO_LEN * 4] = inf.view(np.uint8).reshape(-1)
         host[sec["coef_blocks"]:sec["coef_blocks"] + n * 8] = coef_blocks.view(np.uint8)
         host[sec["out_off"]:sec["out_off"] + n * 8] = out_off.view(np.uint8)
+        pk_off = np.zeros(n, np.int64)
+        cursor = np.zeros(1, np.int64)
+        b = host.ctypes.data
+        dst, cap, cur = b + sec["packed"], self.buf[slot].numel() - sec["packed"], cursor.ctypes.data
+        boff, qt, po = b + sec["block_off"], b + sec["qt"], pk_off.ctypes.data
+        idx = st.index
 
-        def entropy(k):
-            d = datas[st.index[k]]
-            return lib.mmf_jpeg_entropy(d, len(d), base + sec["coefs"] + int(coef_blocks[k]) * 128,
-                                        base + sec["qt"] + k * 384)
+        def entropy(k):  # one C call per image (GIL released): decode, reserve room, copy
+            d = datas[idx[k]]
+            return lib.mmf_jpeg_stage_packed(d, len(d), dst, cap, cur, boff + int(coef_blocks[k]) * 4, qt + k * 384,
+                                             po + k * 8)
         rcs = list(self._pool.map(entropy, range(n))) if n > 1 else [entropy(0)]
-        bad = [k for k, rc in enumerate(rcs) if rc != 0]
+        overflow = [k for k, rc in enumerate(rcs) if rc == MMF_ERANGE]
+        bad = [k for k, rc in enumerate(rcs) if rc not in (0, MMF_ERANGE)]
         if bad:  # (a header that parsed but a scan that did not: never seen; decode those on the host)
-            raise hip.MMFError(f"mmf_jpeg_entropy failed for chunk positions {[st.index[k] for k in bad]}")
+            raise hip.MMFError(f"mmf_jpeg_stage_packed failed for chunk positions {[st.index[k] for k in bad]}")
+        total = sec["packed"] + int(cursor[0])
+        if overflow:  # grow the slot, keep what was written, then place the records that did not fit
+            old = self.buf[slot]
+            keep = sec["packed"] + cap
+            self.buf[slot] = torch.empty(total * 5 // 4, dtype=torch.uint8).pin_memory()
+            host = self.buf[slot].numpy()
+            host[:keep] = old.numpy()[:keep]
+            b = host.ctypes.data
+            for k in overflow:
+                d = datas[idx[k]]
+                used = ctypes.c_int64(0)
+                scratch = np.empty(int(lib.mmf_jpeg_packed_bound(int(blocks[k]))), np.uint8)
+                hip.check(lib.mmf_jpeg_entropy_packed(d, len(d), scratch.ctypes.data, scratch.size,
+                                                      b + sec["block_off"] + int(coef_blocks[k]) * 4,
+                                                      b + sec["qt"] + k * 384, ctypes.byref(used)),
+                          "mmf_jpeg_entropy_packed")
+                o = sec["packed"] + int(pk_off[k])
+                host[o:o + used.value] = scratch[:used.value]
+        host[sec["pk_off"]:sec["pk_off"] + n * 8] = pk_off.view(np.uint8)
+        st.nbytes = total
         return st
+
+
+def _reconstruct(lib, h, p, st: Staged, samples: int, rgbx: int) -> int:
+    sec = st.sections
+    return lib.mmf_jpeg_reconstruct(h, p + sec["packed"], p + sec["block_off"], p + sec["pk_off"], p + sec["qt"],
+                                    p + sec["coef_blocks"], p + sec["infos"], p + sec["out_off"], len(st.index),
+                                    st.max_blocks, st.max_pixels, samples, rgbx, hip.stream_ptr())
 
 
 def device_windows(engine, stager: JpegStager, st: Staged):
@@ -135,16 +176,13 @@ def device_windows(engine, stager: JpegStager, st: Staged):
     ev = torch.cuda.Event()
     ev.record()
     stager.copied[st.slot] = ev
-    sec = st.sections
     p = src.data_ptr()
     need = st.pixels * 4 + st.blocks * 64
     if getattr(engine, "_jpeg_dev", None) is None or engine._jpeg_dev.numel() < need:
         engine._jpeg_dev = torch.empty(need * 5 // 4, dtype=torch.uint8, device=dev)
     rgbx = engine._jpeg_dev.data_ptr()
     samples = rgbx + st.pixels * 4
-    hip.check(lib.mmf_jpeg_reconstruct(engine.h, p + sec["coefs"], p + sec["qt"], p + sec["coef_blocks"],
-                                       p + sec["infos"], p + sec["out_off"], n, st.max_blocks, st.max_pixels,
-                                       samples, rgbx, hip.stream_ptr()), "mmf_jpeg_reconstruct")
+    hip.check(_reconstruct(lib, engine.h, p, st, samples, rgbx), "mmf_jpeg_reconstruct")
     wh = np.ascontiguousarray(st.infos[:, :2]).reshape(-1)
     eff = torch.empty((n, 224, 224, 3), dtype=torch.uint8, device=dev)
     clp = torch.empty((n, 224, 224, 3), dtype=torch.uint8, device=dev)
@@ -158,13 +196,10 @@ def device_rgb(engine, stager: JpegStager, st: Staged) -> List[np.ndarray]:
     """Decoded pixels only (tests / tools): [h][w][3] uint8 host arrays for st.index."""
     dev = engine.device
     src = stager.buf[st.slot][:st.nbytes].to(dev)
-    sec = st.sections
     p = src.data_ptr()
     n = len(st.index)
     out = torch.empty(st.pixels * 4 + st.blocks * 64, dtype=torch.uint8, device=dev)
-    hip.check(engine.lib.mmf_jpeg_reconstruct(engine.h, p + sec["coefs"], p + sec["qt"], p + sec["coef_blocks"],
-                                              p + sec["infos"], p + sec["out_off"], n, st.max_blocks, st.max_pixels,
-                                              out.data_ptr() + st.pixels * 4, out.data_ptr(), hip.stream_ptr()),
+    hip.check(_reconstruct(engine.lib, engine.h, p, st, out.data_ptr() + st.pixels * 4, out.data_ptr()),
               "mmf_jpeg_reconstruct")
     host = out[:st.pixels * 4].cpu().numpy()
     res = []

@@ -43,6 +43,23 @@ def test_device_pixels_match_pillow(engine, stager):
         np.testing.assert_array_equal(g, C.pillow_rgb(d), err_msg=name)
 
 
+def test_staging_slot_growth(engine):
+    """A first packed-section guess far too small: records that do not fit are placed after the slot
+    grows, and the pixels are unchanged."""
+    from mmf_amd import jpeg
+    s = jpeg.JpegStager(workers=3)
+    s.guess_bytes_per_block = 1
+    try:
+        cases = C.supported_jpegs(large=True)
+        for _ in range(2):  # second pass: the grown slots are reused
+            st = s.stage([d for _, d in cases])
+            got = jpeg.device_rgb(engine, s, st)
+            for (name, d), g in zip(cases, got):
+                np.testing.assert_array_equal(g, C.pillow_rgb(d), err_msg=name)
+    finally:
+        s.close()
+
+
 def test_declined_files_are_left_to_pillow(engine, stager):
     from mmf_amd import jpeg
     files = C.unsupported_files()

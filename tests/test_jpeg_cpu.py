@@ -68,6 +68,80 @@ def test_host_entropy_decoder_matches_restatement(name, data):
         J.entropy_decode = J_entropy
 
 
+def unpack(packed, block_off, blocks):
+    """The packed records (mmf_jpeg_entropy_packed) back to dense natural-order blocks."""
+    out = np.zeros((blocks, 64), np.int16)
+    zz = J.ZIGZAG
+    for b in range(blocks):
+        o = int(block_off[b])
+        assert o % 8 == 0
+        mask = int(packed[o:o + 8].view(np.uint64)[0])
+        ks = [k for k in range(64) if mask >> k & 1]
+        vals = packed[o + 8:o + 8 + 2 * len(ks)].view(np.int16)
+        assert np.all(vals != 0)
+        for k, v in zip(ks, vals):
+            out[b, zz[k]] = v
+    return out
+
+
+@pytest.mark.parametrize("name,data", CASES, ids=[n for n, _ in CASES])
+def test_packed_records_equal_dense_coefficients(name, data):
+    """The H2D format (sparse records) carries exactly the dense decoder's coefficients and tables;
+    a too-small output buffer is refused, not overrun."""
+    L = lib()
+    rc, info, co, qt = c_decode(L, data)
+    assert rc == 0
+    blocks = int(info[11])
+    bound = int(L.mmf_jpeg_packed_bound(blocks))
+    packed = np.zeros(bound, np.uint8)
+    boff = np.full(blocks, 0xFFFFFFFF, np.uint32)
+    qt2 = np.zeros((3, 64), np.uint16)
+    used = ctypes.c_int64(-1)
+    assert L.mmf_jpeg_entropy_packed(data, len(data), packed.ctypes.data, bound, boff.ctypes.data, qt2.ctypes.data,
+                                     ctypes.byref(used)) == 0
+    assert 8 <= used.value <= bound and used.value % 8 == 0
+    assert np.all(boff < used.value)
+    np.testing.assert_array_equal(unpack(packed, boff, blocks), co)
+    np.testing.assert_array_equal(qt2, qt)
+    if used.value > 16:
+        assert L.mmf_jpeg_entropy_packed(data, len(data), packed.ctypes.data, used.value - 8, boff.ctypes.data,
+                                         qt2.ctypes.data, ctypes.byref(used)) == -34
+
+
+def test_stage_packed_reserves_and_refuses_overflow():
+    """mmf_jpeg_stage_packed (the staging call of mmf_amd/jpeg.py): records at the reserved offsets equal
+    mmf_jpeg_entropy_packed's; an image that does not fit keeps its reservation and reports ERANGE."""
+    L = lib()
+    imgs = [d for _, d in CASES[:4]]
+    infos = [c_decode(L, d)[1] for d in imgs]
+    dst = np.zeros(1 << 20, np.uint8)
+    cursor = np.zeros(1, np.int64)
+    off = np.zeros(len(imgs), np.int64)
+    for k, d in enumerate(imgs):
+        blocks = int(infos[k][11])
+        boff = np.zeros(blocks, np.uint32)
+        qt = np.zeros((3, 64), np.uint16)
+        assert L.mmf_jpeg_stage_packed(d, len(d), dst.ctypes.data, dst.size, cursor.ctypes.data, boff.ctypes.data,
+                                       qt.ctypes.data, off[k:].ctypes.data) == 0
+        ref = np.zeros(int(L.mmf_jpeg_packed_bound(blocks)), np.uint8)
+        used = ctypes.c_int64(0)
+        boff2 = np.zeros(blocks, np.uint32)
+        assert L.mmf_jpeg_entropy_packed(d, len(d), ref.ctypes.data, ref.size, boff2.ctypes.data, qt.ctypes.data,
+                                         ctypes.byref(used)) == 0
+        assert off[k] % 8 == 0 and (k == 0 or off[k] >= off[k - 1])
+        np.testing.assert_array_equal(dst[off[k]:off[k] + used.value], ref[:used.value])
+        np.testing.assert_array_equal(boff, boff2)
+    before = int(cursor[0])
+    small = np.zeros(before + 8, np.uint8)
+    d = imgs[0]
+    boff = np.zeros(int(infos[0][11]), np.uint32)
+    qt = np.zeros((3, 64), np.uint16)
+    o = np.zeros(1, np.int64)
+    assert L.mmf_jpeg_stage_packed(d, len(d), small.ctypes.data, small.size, cursor.ctypes.data, boff.ctypes.data,
+                                   qt.ctypes.data, o.ctypes.data) == -34
+    assert o[0] == before and cursor[0] > before and not small[before:].any()
+
+
 @pytest.mark.parametrize("name,data", C.unsupported_files(), ids=[n for n, _ in C.unsupported_files()])
 def test_unsupported_files_are_declined(name, data):
     L = lib()
