@@ -179,39 +179,62 @@ __global__ __launch_bounds__(256) void pw32m_kernel(const float* __restrict__ A,
   }
 }
 
-// torchvision pads (k - 1) / 2 on every side; output edge (H - 1) / S + 1
-template <int K, int S>
+#ifndef MMF_DW32_R
+#define MMF_DW32_R 7  // outputs per thread along x (every EfficientNet-B0 width is a multiple of 7)
+#endif
+
+// torchvision pads (k - 1) / 2 on every side; output edge (H - 1) / S + 1.  A thread computes R
+// horizontally adjacent outputs of one 4-channel group: per kernel row it loads the (R - 1) S + K
+// input columns and the K weights once and reuses them across the R outputs (R K loads -> R S + K).
+// Each output's fmaf chain is bias, then (ky, kx) ascending with out-of-image taps skipped -- the
+// same chain at every R (R = 1 is the one-output-per-thread kernel), so the bits do not depend on R.
+template <int K, int S, int R>
 __global__ __launch_bounds__(256) void dw32_kernel(const float* __restrict__ in, const float* __restrict__ w,
                                                    const float* __restrict__ bias, float* __restrict__ out, int H,
-                                                   int W, int C, int Ho, int Wo, size_t total4) {
+                                                   int W, int C, int Ho, int Wo, int Wg, size_t total4) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total4) return;
   const int C4 = C / 4, c4 = (int)(i % C4);
-  const size_t pix = i / C4;
-  const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho), bi = (int)(pix / ((size_t)Wo * Ho));
+  const size_t g = i / C4;
+  const int ox0 = (int)(g % Wg) * R, oy = (int)((g / Wg) % Ho), bi = (int)(g / ((size_t)Wg * Ho));
   const int c = c4 * 4;
-  float acc[4];
+  constexpr int P = (K - 1) / 2, NC = (R - 1) * S + K;
+  const float4 b4 = make_float4(bias[c], bias[c + 1], bias[c + 2], bias[c + 3]);
+  float4 acc[R];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = bias[c + j];
-  constexpr int P = (K - 1) / 2;
+  for (int r = 0; r < R; ++r) acc[r] = b4;
+  const int ix0 = ox0 * S - P;
 #pragma unroll
   for (int ky = 0; ky < K; ++ky) {
     const int iy = oy * S - P + ky;
     if (iy < 0 || iy >= H) continue;
+    const float* row = in + ((size_t)bi * H + iy) * W * C + c;
+    float4 v[NC], wt[K];
 #pragma unroll
-    for (int kx = 0; kx < K; ++kx) {
-      const int ix = ox * S - P + kx;
-      if (ix < 0 || ix >= W) continue;
-      const float4 v = *reinterpret_cast<const float4*>(in + (((size_t)bi * H + iy) * W + ix) * C + c);
-      const float4 wt = *reinterpret_cast<const float4*>(w + (size_t)(ky * K + kx) * C + c);
-      acc[0] = fmaf(v.x, wt.x, acc[0]);
-      acc[1] = fmaf(v.y, wt.y, acc[1]);
-      acc[2] = fmaf(v.z, wt.z, acc[2]);
-      acc[3] = fmaf(v.w, wt.w, acc[3]);
+    for (int kx = 0; kx < K; ++kx) wt[kx] = *reinterpret_cast<const float4*>(w + (size_t)(ky * K + kx) * C + c);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int ix = ix0 + j;
+      v[j] = (ix >= 0 && ix < W) ? *reinterpret_cast<const float4*>(row + (size_t)ix * C) : make_float4(0, 0, 0, 0);
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const int j = r * S + kx, ix = ix0 + j;
+        if (ix < 0 || ix >= W) continue;
+        acc[r].x = fmaf(v[j].x, wt[kx].x, acc[r].x);
+        acc[r].y = fmaf(v[j].y, wt[kx].y, acc[r].y);
+        acc[r].z = fmaf(v[j].z, wt[kx].z, acc[r].z);
+        acc[r].w = fmaf(v[j].w, wt[kx].w, acc[r].w);
+      }
   }
-  *reinterpret_cast<float4*>(out + pix * C + c) =
-      make_float4(silu_precise(acc[0]), silu_precise(acc[1]), silu_precise(acc[2]), silu_precise(acc[3]));
+  float* o = out + (((size_t)bi * Ho + oy) * Wo + ox0) * C + c;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (ox0 + r < Wo)
+      *reinterpret_cast<float4*>(o + (size_t)r * C) = make_float4(silu_precise(acc[r].x), silu_precise(acc[r].y),
+                                                                  silu_precise(acc[r].z), silu_precise(acc[r].w));
 }
 
 // grid (ceil(C / 64), nchunks, B): chunk j covers pixels [j HW / nchunks, (j + 1) HW / nchunks);
@@ -281,12 +304,14 @@ hipError_t launch_dw32(const float* in, const float* w, const float* bias, float
                        int k, int stride, hipStream_t s) {
   if (C % 4) return hipErrorInvalidValue;
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  const size_t total4 = (size_t)B * Ho * Wo * (C / 4);
+  constexpr int R = MMF_DW32_R;
+  const int Wg = (Wo + R - 1) / R;
+  const size_t total4 = (size_t)B * Ho * Wg * (C / 4);
   const dim3 grid((unsigned)((total4 + 255) / 256)), blk(256);
-#define MMF_DW32(KK, SS)                                                                                     \
-  if (k == KK && stride == SS) {                                                                             \
-    hipLaunchKernelGGL((dw32_kernel<KK, SS>), grid, blk, 0, s, in, w, bias, out, H, W, C, Ho, Wo, total4);   \
-    return hipGetLastError();                                                                                \
+#define MMF_DW32(KK, SS)                                                                                       \
+  if (k == KK && stride == SS) {                                                                               \
+    hipLaunchKernelGGL((dw32_kernel<KK, SS, R>), grid, blk, 0, s, in, w, bias, out, H, W, C, Ho, Wo, Wg, total4); \
+    return hipGetLastError();                                                                                  \
   }
   MMF_DW32(3, 1)
   MMF_DW32(3, 2)
