@@ -8,7 +8,8 @@
 //   pw32     C = act((A * scale[image]) W^T + bias) (+ residual): the expand / project / head convs
 //   dw32     depthwise kxk + BN + SiLU, one thread per (output pixel, 4 channels); weights
 //            tap-major [k*k][C] so a thread's 4 channels are one float4
-//   sum32    per-(image, pixel chunk, channel) sums in a fixed order -> the SE pool partials
+//   sum32    per-(image, pixel chunk, channel) sums in a fixed order -> the SE pool partials (one wave per
+//            block: 4-channel lanes x 4 pixel lanes x chunks, four float4 loads in flight per lane)
 //   gap32    global average pool + Linear(1280, 2) + softmax[:, 1]
 // The stem is effnet.hip's stem kernel with fp32 output; the SE is effnet.hip's se kernel.  Every
 // SiLU / sigmoid here is the IEEE-division, full-precision-exp form torch's CPU kernels use
@@ -237,22 +238,42 @@ __global__ __launch_bounds__(256) void dw32_kernel(const float* __restrict__ in,
                                                                   silu_precise(acc[r].z), silu_precise(acc[r].w));
 }
 
-// grid (ceil(C / 64), nchunks, B): chunk j covers pixels [j HW / nchunks, (j + 1) HW / nchunks);
-// 4 pixel lanes x 64 channels, each lane sums its pixels in order, then the 4 lane sums are added
-// in a fixed order (deterministic) -> part[b][j][c]
-__global__ __launch_bounds__(256) void sum32_kernel(const float* __restrict__ x, int HW, int C,
-                                                    float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int bi = blockIdx.z, j = blockIdx.y, nch = gridDim.y;
-  const int cl = threadIdx.x & 63, r = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
-  const int p0 = (int)((long)j * HW / nch), p1 = (int)((long)(j + 1) * HW / nch);
-  float s = 0.f;
-  if (c < C)
-    for (int p = p0 + r; p < p1; p += 4) s += x[((size_t)bi * HW + p) * C + c];
-  red[r][cl] = s;
+// Chunk j of image b covers pixels [j HW / nchunks, (j + 1) HW / nchunks).  Per channel, 4 pixel
+// lanes each sum their pixels in order (lane r: p0 + r, p0 + r + 4, ...), then the 4 lane sums are
+// added in a fixed order ((r0 + r1) + (r2 + r3)) -> part[b][j][c].  One wave: L lanes of 4 channels
+// (float4 loads) x 4 pixel lanes x 16 / L chunks; grid (C / 4 / L, ceil(nchunks L / 16), B).
+template <int L>
+__global__ __launch_bounds__(64) void sum32_kernel(const float* __restrict__ x, int HW, int C, int nch,
+                                                   float* __restrict__ part) {
+  __shared__ float4 red[64];
+  constexpr int G = 16 / L;
+  const int lane = threadIdx.x, bi = blockIdx.z;
+  const int c = (blockIdx.x * L + lane % L) * 4, r = (lane / L) & 3, j = blockIdx.y * G + lane / (4 * L);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j < nch) {
+    const int p0 = (int)((long)j * HW / nch), p1 = (int)((long)(j + 1) * HW / nch);
+    const float* xp = x + (size_t)bi * HW * C + c;
+    int p = p0 + r;
+    for (; p + 12 < p1; p += 16) {  // four loads in flight, added in pixel order
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(xp + (size_t)(p + 4 * u) * C);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w; }
+    }
+    for (; p < p1; p += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(xp + (size_t)p * C);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[lane] = a;
   __syncthreads();
-  if (r == 0 && c < C)
-    part[((size_t)bi * nch + j) * C + c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+  if (r == 0 && j < nch) {
+    const float4 s0 = red[lane], s1 = red[lane + L], s2 = red[lane + 2 * L], s3 = red[lane + 3 * L];
+    *reinterpret_cast<float4*>(part + ((size_t)bi * nch + j) * C + c) =
+        make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y), (s0.z + s1.z) + (s2.z + s3.z),
+                    (s0.w + s1.w) + (s2.w + s3.w));
+  }
 }
 
 __global__ __launch_bounds__(256) void gap32_kernel(const float* __restrict__ x, int HW, int C,
@@ -322,8 +343,13 @@ hipError_t launch_dw32(const float* in, const float* w, const float* bias, float
 }
 
 hipError_t launch_sum32(const float* x, int B, int HW, int C, int nchunks, float* part, hipStream_t s) {
-  if (nchunks < 1 || nchunks > HW) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sum32_kernel, dim3((C + 63) / 64, nchunks, B), dim3(256), 0, s, x, HW, C, part);
+  if (nchunks < 1 || nchunks > HW || (C % 16)) return hipErrorInvalidValue;
+  const int C4 = C / 4;
+  const int L = C4 % 16 == 0 ? 16 : C4 % 8 == 0 ? 8 : 4;
+  const dim3 grid(C4 / L, (nchunks * L + 15) / 16, B);
+  if (L == 16) hipLaunchKernelGGL(sum32_kernel<16>, grid, dim3(64), 0, s, x, HW, C, nchunks, part);
+  else if (L == 8) hipLaunchKernelGGL(sum32_kernel<8>, grid, dim3(64), 0, s, x, HW, C, nchunks, part);
+  else hipLaunchKernelGGL(sum32_kernel<4>, grid, dim3(64), 0, s, x, HW, C, nchunks, part);
   return hipGetLastError();
 }
 
