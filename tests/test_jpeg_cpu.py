@@ -168,3 +168,39 @@ def test_truncated_and_corrupt_streams_do_not_crash():
         i = int(rng.integers(len(bad) // 2, len(bad) - 2))
         bad[i] ^= 0x5C
         c_decode(L, bytes(bad))  # any rc; must not crash or write out of bounds
+
+
+def test_packed_staging_of_truncated_and_corrupt_streams():
+    """The product's staging call on damaged scans: records stay inside the bound, every block offset
+    points inside the written records (8-aligned), and the guard bytes after them are untouched."""
+    L = lib()
+    d = CASES[9][1]  # 300x200 with restart markers
+    info = np.zeros(16, np.int32)
+    assert L.mmf_jpeg_header(d, len(d), info.ctypes.data) == 0
+    blocks = int(info[11])
+    bound = int(L.mmf_jpeg_packed_bound(blocks))
+    rng = np.random.default_rng(7)
+    variants = [d[:len(d) * 2 // 3], d[:len(d) // 3]]
+    for _ in range(30):
+        bad = bytearray(d)
+        for _ in range(3):
+            i = int(rng.integers(len(bad) // 3, len(bad) - 2))
+            bad[i] ^= int(rng.integers(1, 256))
+        variants.append(bytes(bad))
+    for v in variants:
+        dst = np.full(bound + 64, 0xA5, np.uint8)
+        cursor = np.zeros(1, np.int64)
+        boff = np.full(blocks, 0xFFFFFFFF, np.uint32)
+        qt = np.zeros((3, 64), np.uint16)
+        off = np.zeros(1, np.int64)
+        rc = L.mmf_jpeg_stage_packed(v, len(v), dst.ctypes.data, bound, cursor.ctypes.data, boff.ctypes.data,
+                                     qt.ctypes.data, off.ctypes.data)
+        if rc != 0:
+            continue  # a header the damage made unparseable: declined, nothing written
+        used = int(cursor[0])
+        assert 8 <= used <= bound and off[0] == 0
+        assert np.all(boff % 8 == 0) and np.all(boff < used)
+        assert np.all(dst[bound:] == 0xA5)
+        for o in boff[::37]:  # each record's mask counts values that fit before the next offset bound
+            n = bin(int(dst[o:o + 8].view(np.uint64)[0])).count("1")
+            assert o + 8 + 2 * n <= used
