@@ -32,7 +32,7 @@ extern "C" {
 #define MMF_ENOMEM (-12)
 #define MMF_EIO (-5)
 #define MMF_ERANGE (-34) /* an input outside a kernel's supported range (mmf_resize_pil: too many taps) */
-#define MMF_EUNSUPPORTED (-95) /* a valid input of a kind this path does not handle (mmf_jpeg_*: progressive, ...) */
+#define MMF_EUNSUPPORTED (-95) /* a valid input of a kind this path does not handle (mmf_jpeg_*: CMYK, lossless, ...) */
 
 #define MMF_DTYPE_F32 0
 #define MMF_DTYPE_I64 1

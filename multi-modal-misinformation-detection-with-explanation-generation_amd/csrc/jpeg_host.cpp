@@ -5,8 +5,8 @@
 // jdsample.c, jdcolor.c), which is what the reference's Image.open(...).convert("RGB")
 // (misinfo_forensics.py:255-258) runs.  Restatement and pinning: oracle/jpeg_decode.py.
 //
-// Supported (mmf_jpeg_header returns 0): 8-bit baseline / extended sequential Huffman (SOF0/SOF1),
-// one scan holding every component, 1 component or 3 YCbCr components with luma sampling h, v <= 2
+// Supported (mmf_jpeg_header returns 0): 8-bit baseline / extended sequential Huffman (SOF0/SOF1)
+// with one scan holding every component, or progressive Huffman (SOF2, any scan script; jdphuff.c), 1 component or 3 YCbCr components with luma sampling h, v <= 2
 // and chroma 1x1 (4:4:4, 4:2:2, 4:2:0); anything else returns MMF_EUNSUPPORTED and the caller decodes
 // that file on the host (Pillow).
 //
@@ -105,8 +105,9 @@ struct Jpeg {
   uint16_t qt[4][64];
   bool qt_present[4] = {false, false, false, false};
   Huff dc[4], ac[4];
-  const uint8_t* scan = nullptr;  // entropy-coded segment start
+  const uint8_t* scan = nullptr;  // entropy-coded segment start (progressive: the first SOS marker)
   const uint8_t* end = nullptr;
+  bool progressive = false;
   int hmax = 1, vmax = 1, mcux = 0, mcuy = 0;
 };
 
@@ -126,8 +127,9 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
     if (L < 2 || p + L > n) return MMF_EINVAL;
     const uint8_t* s = d + p + 2;
     const int sl = L - 2;
-    if (m == 0xC0 || m == 0xC1) {
+    if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
       if (sl < 6 || s[0] != 8) return MMF_EUNSUPPORTED;  // 12-bit
+      j.progressive = m == 0xC2;
       j.height = (s[1] << 8) | s[2];
       j.width = (s[3] << 8) | s[4];
       j.ncomp = s[5];
@@ -144,8 +146,8 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
         if (j.comp[i].h < 1 || j.comp[i].v < 1) return MMF_EINVAL;
       }
       sof = true;
-    } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-      return MMF_EUNSUPPORTED;  // progressive, lossless, arithmetic
+    } else if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      return MMF_EUNSUPPORTED;  // lossless, arithmetic, hierarchical
     } else if (m == 0xDB) {
       int q = 0;
       while (q < sl) {
@@ -177,6 +179,11 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
       if (sl >= 12 && memcmp(s, "Adobe", 5) == 0) j.adobe = s[11];
     } else if (m == 0xDA) {
       if (!sof) return MMF_EINVAL;
+      if (j.progressive) {  // scans (and the tables between them) are walked by decode_progressive
+        j.scan = d + p - 2;
+        j.end = d + n;
+        break;
+      }
       j.nscan = s[0];
       if (j.nscan != j.ncomp) return MMF_EUNSUPPORTED;  // multi-scan sequential
       for (int i = 0; i < j.nscan; ++i) {
@@ -197,7 +204,8 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
   }
   if (!j.scan) return MMF_EINVAL;
   for (int c = 0; c < j.ncomp; ++c) {
-    if (!j.qt_present[j.comp[c].tq] || !j.dc[j.comp[c].td].present || !j.ac[j.comp[c].ta].present) return MMF_EINVAL;
+    if (!j.qt_present[j.comp[c].tq]) return MMF_EINVAL;
+    if (!j.progressive && (!j.dc[j.comp[c].td].present || !j.ac[j.comp[c].ta].present)) return MMF_EINVAL;
     j.hmax = j.hmax > j.comp[c].h ? j.hmax : j.comp[c].h;
     j.vmax = j.vmax > j.comp[c].v ? j.vmax : j.comp[c].v;
   }
@@ -451,6 +459,230 @@ inline int decode_block_packed(Bits& b, const Huff& dc, const Huff& ac, int& pre
   return (8 + 2 * n + 7) & ~7;
 }
 
+// ---- progressive Huffman (SOF2), restating libjpeg's jdphuff.c: every scan is decoded into the
+// dense coefficient planes (DC first / refine, AC first / refine with end-of-band runs); the
+// complete planes are what a sequential file of the same image would carry.
+
+// pack one dense natural-order block into a record (see decode_block_packed), its nonzero zigzag
+// positions given by `mask`; 0 bytes for an all-zero block (it then shares record 0)
+inline int pack_block(const int16_t* blk, uint64_t mask, uint8_t* rec) {
+  if (!mask) return 0;
+  int16_t* val = reinterpret_cast<int16_t*>(rec + 8);
+  int n = 0;
+  for (uint64_t m = mask; m; m &= m - 1) val[n++] = blk[kZigzag[__builtin_ctzll(m)]];
+  memcpy(rec, &mask, 8);
+  for (int i = n; i & 3; ++i) val[i] = 0;
+  return (8 + 2 * n + 7) & ~7;
+}
+
+inline int get_bits(Bits& b, int k) { return k ? b.get(k) : 0; }
+
+// coefs: dense [blocks][64] natural order, zeroed by the caller; nzm[block] = the zigzag positions
+// 1..63 that are nonzero once every scan is in (bit 0 is left to the caller: DC = coefs[b * 64])
+int decode_progressive(Jpeg& j, int16_t* coefs, uint64_t* nzm) {
+  int64_t base[3];
+  int bw[3], nbx[3], nby[3];
+  int64_t off = 0;
+  for (int c = 0; c < j.ncomp; ++c) {
+    const Comp& cc = j.comp[c];
+    bw[c] = j.mcux * cc.h;
+    base[c] = off;
+    off += (int64_t)bw[c] * j.mcuy * cc.v;
+    const int cw = (j.width * cc.h + j.hmax - 1) / j.hmax, ch = (j.height * cc.v + j.vmax - 1) / j.vmax;
+    nbx[c] = (cw + 7) / 8;
+    nby[c] = (ch + 7) / 8;
+  }
+  memset(nzm, 0, off * sizeof(uint64_t));
+  const uint8_t* p = j.scan;
+  const uint8_t* end = j.end;
+  while (p + 4 <= end) {
+    if (p[0] != 0xFF) {  // entropy data a scan did not consume (corrupt / padded): find the marker
+      ++p;
+      continue;
+    }
+    const int m = p[1];
+    if (m == 0xFF) { ++p; continue; }
+    if (m == 0x00 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) { p += 2; continue; }
+    if (m == 0xD9) break;  // EOI
+    p += 2;
+    const int L = (p[0] << 8) | p[1];
+    if (L < 2 || p + L > end) return MMF_EINVAL;
+    const uint8_t* sg = p + 2;
+    const int sl = L - 2;
+    if (m == 0xC4) {
+      int q = 0;
+      while (q < sl) {
+        if (q + 17 > sl) return MMF_EINVAL;
+        const int tc = sg[q] >> 4, th = sg[q] & 3;
+        int nv = 0;
+        for (int i = 0; i < 16; ++i) nv += sg[q + 1 + i];
+        if (nv > 256 || q + 17 + nv > sl) return MMF_EINVAL;
+        if (!build_huff(tc ? j.ac[th] : j.dc[th], sg + q + 1, sg + q + 17, nv)) return MMF_EINVAL;
+        q += 17 + nv;
+      }
+    } else if (m == 0xDD) {
+      if (sl < 2) return MMF_EINVAL;
+      j.restart = (sg[0] << 8) | sg[1];
+    } else if (m == 0xDB) {
+      return MMF_EUNSUPPORTED;  // a quantisation table redefined between scans: left to Pillow
+    } else if (m == 0xDA) {
+      if (sl < 1) return MMF_EINVAL;
+      const int ns = sg[0];
+      if (ns < 1 || ns > j.ncomp || sl < 4 + 2 * ns) return MMF_EINVAL;
+      int sc[3], td[3], ta[3];
+      for (int i = 0; i < ns; ++i) {
+        const int cid = sg[1 + 2 * i], tt = sg[2 + 2 * i];
+        sc[i] = -1;
+        for (int c = 0; c < j.ncomp; ++c)
+          if (j.comp[c].id == cid) sc[i] = c;
+        if (sc[i] < 0) return MMF_EINVAL;
+        td[i] = (tt >> 4) & 3;
+        ta[i] = tt & 3;
+      }
+      const int Ss = sg[1 + 2 * ns], Se = sg[2 + 2 * ns], Ah = sg[3 + 2 * ns] >> 4, Al = sg[3 + 2 * ns] & 15;
+      if (Ss > Se || Se > 63 || (Ss == 0 && Se != 0) || (Ss > 0 && ns != 1) || Al > 13) return MMF_EINVAL;
+      for (int i = 0; i < ns; ++i) {
+        if (Ss == 0 && Ah == 0 && !j.dc[td[i]].present) return MMF_EINVAL;
+        if (Ss > 0 && !j.ac[ta[i]].present) return MMF_EINVAL;
+      }
+      Bits b{p + L, end};
+      int pred[3] = {0, 0, 0};
+      int eobrun = 0;
+      const int ri = j.restart;
+      int64_t unit = 0;
+      const int p1 = 1 << Al, m1 = -(1 << Al);
+      const uint64_t band = (Se == 63 ? ~0ull : (1ull << (Se + 1)) - 1) & (~0ull << Ss);
+      // correction bits of the already-nonzero coefficients in `sel` (one bit each, in k order),
+      // read up to 16 at a time
+      auto refine = [&](int16_t* blk, uint64_t sel) {
+        while (sel) {
+          const int cnt = __builtin_popcountll(sel), take = cnt < 16 ? cnt : 16;
+          const uint32_t bits = (uint32_t)b.get(take);
+          for (int t = take - 1; t >= 0; --t) {
+            const int kk = __builtin_ctzll(sel);
+            sel &= sel - 1;
+            int16_t& c = blk[kZigzag[kk]];
+            if (((bits >> t) & 1) && (c & p1) == 0) c = (int16_t)(c >= 0 ? c + p1 : c + m1);
+          }
+        }
+      };
+      auto block = [&](int i, int64_t bi, int16_t* blk) {
+        if (Ss == 0) {
+          if (Ah == 0) {  // DC first
+            int t = decode_sym(b, j.dc[td[i]]);
+            if (t > 16) t = 16;
+            const int diff = t ? extend(b.get(t), t) : 0;
+            pred[i] += diff;
+            blk[0] = (int16_t)(pred[i] * (1 << Al));
+          } else if (get_bits(b, 1)) {  // DC refine
+            blk[0] = (int16_t)(blk[0] | p1);
+          }
+          return;
+        }
+        const Huff& ac = j.ac[ta[i]];
+        uint64_t& nz = nzm[bi];  // zigzag positions already nonzero (earlier AC scans)
+        if (Ah == 0) {  // AC first
+          if (eobrun > 0) {
+            --eobrun;
+            return;
+          }
+          for (int k = Ss; k <= Se; ++k) {
+            if (b.n < 16) b.fill();
+            const int32_t f = ac.acfast[b.peek(kLook)];
+            int v;
+            if (f) {
+              k += (f >> 8) & 15;
+              b.skip(f & 0xFF);
+              v = f >> 16;
+            } else {
+              const int rs = decode_sym(b, ac), r = rs >> 4, sz = rs & 15;
+              if (!sz) {
+                if (r == 15) {
+                  k += 15;
+                  continue;
+                }
+                eobrun = (1 << r) + get_bits(b, r) - 1;
+                break;
+              }
+              k += r;
+              v = extend(b.get(sz), sz);
+            }
+            if (k > 63) break;
+            blk[kZigzag[k]] = (int16_t)(v * (1 << Al));
+            nz |= 1ull << k;
+          }
+          return;
+        }
+        // AC refine (jdphuff.c decode_mcu_AC_refine) over bit masks: a run of r skips r still-zero
+        // coefficients and corrects every nonzero one passed over; the (r + 1)-th zero gets the
+        // newly nonzero value
+        int k = Ss;
+        if (eobrun == 0) {
+          for (; k <= Se; ++k) {
+            const int rs = decode_sym(b, ac);
+            const int r = rs >> 4, sz = rs & 15;
+            int v = 0;
+            if (sz) {
+              v = get_bits(b, 1) ? p1 : m1;
+            } else if (r != 15) {
+              eobrun = (1 << r) + get_bits(b, r);
+              break;
+            }
+            const uint64_t from = ~0ull << k;
+            uint64_t z = ~nz & band & from;
+            for (int t = 0; t < r && z; ++t) z &= z - 1;
+            const int tgt = z ? __builtin_ctzll(z) : Se + 1;
+            refine(blk, nz & band & from & (tgt >= 64 ? ~0ull : (1ull << tgt) - 1));
+            k = tgt;
+            if (v && k <= Se) {
+              blk[kZigzag[k]] = (int16_t)v;
+              nz |= 1ull << k;
+            }
+          }
+        }
+        if (eobrun > 0) {
+          if (k <= 63) refine(blk, nz & band & (~0ull << k));
+          --eobrun;
+        }
+      };
+      auto restart_check = [&]() {
+        if (ri && unit && unit % ri == 0) {
+          b.restart();
+          pred[0] = pred[1] = pred[2] = 0;
+          eobrun = 0;
+        }
+      };
+      if (ns > 1) {
+        for (int my = 0; my < j.mcuy; ++my)
+          for (int mx = 0; mx < j.mcux; ++mx, ++unit) {
+            restart_check();
+            for (int i = 0; i < ns; ++i) {
+              const Comp& c = j.comp[sc[i]];
+              for (int yy = 0; yy < c.v; ++yy)
+                for (int xx = 0; xx < c.h; ++xx)
+                {
+                  const int64_t bi = base[sc[i]] + (int64_t)(my * c.v + yy) * bw[sc[i]] + mx * c.h + xx;
+                  block(i, bi, coefs + bi * 64);
+                }
+            }
+          }
+      } else {
+        const int ci = sc[0];
+        for (int by = 0; by < nby[ci]; ++by)
+          for (int bx = 0; bx < nbx[ci]; ++bx, ++unit) {
+            restart_check();
+            const int64_t bi = base[ci] + (int64_t)by * bw[ci] + bx;
+            block(0, bi, coefs + bi * 64);
+          }
+      }
+      p = b.p;  // the bit reader stops at the next marker
+      continue;
+    }
+    p += L;
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* coefs, uint16_t* qt) {
@@ -459,6 +691,14 @@ extern "C" int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* co
   const int rc = parse(data, nbytes, j);
   if (rc) return rc;
   for (int c = 0; c < j.ncomp; ++c) memcpy(qt + 64 * c, j.qt[j.comp[c].tq], 64 * sizeof(uint16_t));
+  if (j.progressive) {
+    int64_t blocks = 0;
+    for (int c = 0; c < j.ncomp; ++c) blocks += (int64_t)j.mcux * j.comp[c].h * j.mcuy * j.comp[c].v;
+    memset(coefs, 0, blocks * 128);
+    thread_local std::vector<uint64_t> nzm;
+    if ((int64_t)nzm.size() < blocks) nzm.resize(blocks);
+    return decode_progressive(j, coefs, nzm.data());
+  }
   return walk_blocks(
       j, [&](Bits& b, int64_t gb, const Huff& dc, const Huff& ac, int& pred) { decode_block(b, dc, ac, pred, coefs + gb * 64); },
       [&](int64_t gb) { memset(coefs + gb * 64, 0, 128); });
@@ -481,6 +721,23 @@ extern "C" int mmf_jpeg_entropy_packed(const uint8_t* data, int64_t nbytes, uint
     return MMF_ERANGE;
   memset(out, 0, 8);  // record 0: the all-zero block (padding blocks point here)
   int64_t cur = 8;
+  if (j.progressive) {  // all scans into dense planes first, then one record per nonzero block
+    thread_local std::vector<int16_t> dense;
+    thread_local std::vector<uint64_t> nzm;
+    if ((int64_t)dense.size() < blocks * 64) dense.resize(blocks * 64);
+    if ((int64_t)nzm.size() < blocks) nzm.resize(blocks);
+    memset(dense.data(), 0, blocks * 128);
+    const int prc = decode_progressive(j, dense.data(), nzm.data());
+    if (prc) return prc;
+    for (int64_t b = 0; b < blocks; ++b) {
+      const int16_t* blk = dense.data() + b * 64;
+      const int sz = pack_block(blk, nzm[b] | (uint64_t)(blk[0] != 0), out + cur);
+      block_off[b] = sz ? (uint32_t)cur : 0;
+      cur += sz;
+    }
+    *used = cur;
+    return 0;
+  }
   walk_blocks(
       j,
       [&](Bits& b, int64_t gb, const Huff& dc, const Huff& ac, int& pred) {

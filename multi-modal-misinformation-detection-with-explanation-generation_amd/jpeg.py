@@ -8,7 +8,8 @@ the GIL); the quantised coefficients are packed sparse (per block a mask of the 
 positions + their values: ~0.35 MB for a 640x480 q90 photo instead of 0.92 MB of dense planes) into
 a pinned staging buffer, one H2D copy moves them, and the device reconstructs the pixels (csrc/jpeg.hip: islow IDCT, fancy chroma upsampling, YCbCr -> RGB,
 bit-exact with Pillow) as RGBX images that feed the Pillow-exact resampler (mmf_resize_pil).
-Files the C decoder does not take (progressive, CMYK, 4:4:0, ...) report MMF_EUNSUPPORTED and are
+Progressive files are decoded scan by scan into the same coefficients.  Files the C decoder does
+not take (CMYK, 4:4:0, lossless / arithmetic / 12-bit, ...) report MMF_EUNSUPPORTED and are
 decoded by Pillow on the host, as before.
 """
 from __future__ import annotations

@@ -1,7 +1,8 @@
 """JPEG test inputs shared by tests/test_jpeg_cpu.py and tests/test_gpu_jpeg.py: encoded in the test
 run by Pillow's encoder (deterministic), covering the decoder paths -- 4:2:0 / 4:2:2 / 4:4:4 /
 grayscale, odd sizes and 1x1, optimised Huffman tables, restart intervals (per blocks and per MCU
-rows), low and high quality -- plus files the device path must hand back to Pillow."""
+rows), low and high quality, progressive files -- plus files the device path must hand back to
+Pillow."""
 import io
 
 import numpy as np
@@ -46,15 +47,50 @@ SUPPORTED = [
 LARGE = [(640, 480, "RGB", dict(quality=90, subsampling=2)), (1023, 767, "RGB", dict(quality=80, subsampling=1))]
 
 
-def supported_jpegs(large=False):
-    cases = SUPPORTED + (LARGE if large else [])
+# progressive (SOF2): Pillow's scan script has DC first / refine and AC first / refine scans with
+# successive approximation, optimised tables per scan (DHT between scans)
+PROGRESSIVE = [(w, h, m, dict(kw, progressive=True)) for w, h, m, kw in (
+    (64, 48, "RGB", dict(quality=90, subsampling=2)),
+    (65, 49, "RGB", dict(quality=75, subsampling=2)),
+    (33, 17, "RGB", dict(quality=95, subsampling=1)),
+    (40, 40, "RGB", dict(quality=50, subsampling=0)),
+    (31, 23, "L", dict(quality=80)),
+    (1, 1, "RGB", dict(quality=90)),
+    (300, 200, "RGB", dict(quality=90, subsampling=2, restart_marker_blocks=7)),
+    (127, 129, "RGB", dict(quality=98, subsampling=0)),
+)]
+LARGE_PROGRESSIVE = [(640, 480, "RGB", dict(quality=90, subsampling=2, progressive=True))]
+
+
+def _cases(cases):
     return [(f"{w}x{h}-{m}-{kw}", encode(photo_like(w, h, seed=w * 31 + h), m, **kw)) for w, h, m, kw in cases]
+
+
+def supported_jpegs(large=False, progressive=False):
+    cases = SUPPORTED + (LARGE if large else [])
+    if progressive:
+        cases = cases + PROGRESSIVE + (LARGE_PROGRESSIVE if large else [])
+    return _cases(cases)
+
+
+def progressive_pairs():
+    """(name, progressive file, sequential file of the same pixels and settings): the quantised
+    coefficients of the two are the same (progression only changes the entropy coding)."""
+    out = []
+    for w, h, m, kw in PROGRESSIVE:
+        a = photo_like(w, h, seed=w * 31 + h)
+        seq = {k: v for k, v in kw.items() if k != "progressive"}
+        out.append((f"{w}x{h}-{m}-{kw}", encode(a, m, **kw), encode(a, m, **seq)))
+    return out
 
 
 def unsupported_files():
     """Files the device path declines (MMF_EUNSUPPORTED or not JPEG): Pillow decodes them."""
     a = photo_like(48, 40, seed=5)
-    out = [("progressive", encode(a, quality=90, progressive=True)),
+    seq = bytearray(encode(a, quality=90))
+    i = seq.index(b"\xff\xc0")
+    seq[i + 1] = 0xC3  # the same file relabelled lossless (SOF3)
+    out = [("lossless", bytes(seq)),
            ("cmyk", encode(a, "CMYK", quality=90))]
     b = io.BytesIO()
     Image.fromarray(a).save(b, "PNG")

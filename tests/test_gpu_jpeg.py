@@ -2,7 +2,7 @@
 pixels bit-exact with Pillow's decoder (the reference's Image.open(...).convert("RGB")) on every
 supported kind of file, and analyze_pairs over encoded files equal -- dict for dict -- to the same
 call with every image decoded by Pillow, including chunks that mix device-decoded JPEGs with files
-the device path declines (progressive, CMYK, PNG) and PIL images."""
+the device path declines (CMYK, lossless, PNG) and PIL images; progressive files included."""
 import io
 import os
 
@@ -35,7 +35,7 @@ def stager():
 
 def test_device_pixels_match_pillow(engine, stager):
     from mmf_amd import jpeg
-    cases = C.supported_jpegs(large=True)
+    cases = C.supported_jpegs(large=True, progressive=True)
     st = stager.stage([d for _, d in cases])
     assert st.index == list(range(len(cases)))
     got = jpeg.device_rgb(engine, stager, st)
@@ -50,7 +50,7 @@ def test_staging_slot_growth(engine):
     s = jpeg.JpegStager(workers=3)
     s.guess_bytes_per_block = 1
     try:
-        cases = C.supported_jpegs(large=True)
+        cases = C.supported_jpegs(large=True, progressive=True)
         for _ in range(2):  # second pass: the grown slots are reused
             st = s.stage([d for _, d in cases])
             got = jpeg.device_rgb(engine, s, st)
@@ -76,7 +76,7 @@ def test_windows_match_pillow_resampling(engine, stager):
     from PIL import Image
 
     from mmf_amd import io_utils, jpeg
-    cases = C.supported_jpegs(large=True)
+    cases = C.supported_jpegs(large=True, progressive=True)
     st = stager.stage([d for _, d in cases])
     eff, clp = jpeg.device_windows(engine, stager, st)
     for k, (name, d) in enumerate(cases):
@@ -104,7 +104,8 @@ def forensics(golden, golden_inputs, det_sd, clip_sd):
 
 def test_analyze_pairs_on_encoded_files(forensics, golden_inputs, tmp_path):
     """10 pairs in chunks of 4 (both pinned staging slots reused): JPEG bytes, a JPEG file path,
-    a progressive JPEG, a PNG and a PIL image, against the all-Pillow run of the same call."""
+    a progressive JPEG, a CMYK JPEG and a PNG (both declined: Pillow), a PIL image, against the
+    all-Pillow run of the same call."""
     from PIL import Image
     imgs = golden_inputs["imgs"]
     n = imgs.shape[0]
@@ -113,6 +114,8 @@ def test_analyze_pairs_on_encoded_files(forensics, golden_inputs, tmp_path):
         a = imgs[i % n]
         if i == 3:
             items.append(C.encode(a, quality=90, progressive=True))
+        elif i == 5:
+            items.append(C.encode(a, "CMYK", quality=90))
         elif i == 6:
             b = io.BytesIO()
             Image.fromarray(a).save(b, "PNG")

@@ -108,6 +108,28 @@ def test_packed_records_equal_dense_coefficients(name, data):
                                          qt2.ctypes.data, ctypes.byref(used)) == -34
 
 
+@pytest.mark.parametrize("name,prog,seq", C.progressive_pairs(), ids=[n for n, _, _ in C.progressive_pairs()])
+def test_progressive_coefficients_equal_sequential(name, prog, seq):
+    """Progressive (SOF2) decoding -- every scan of Pillow's successive-approximation script, DHT
+    between scans, restarts -- yields exactly the coefficients of the sequential file of the same
+    pixels (pinned above to the restatement and Pillow); the packed records carry them too."""
+    L = lib()
+    rc_p, info_p, co_p, qt_p = c_decode(L, prog)
+    rc_s, info_s, co_s, qt_s = c_decode(L, seq)
+    assert rc_p == 0 and rc_s == 0
+    np.testing.assert_array_equal(info_p, info_s)
+    np.testing.assert_array_equal(qt_p, qt_s)
+    np.testing.assert_array_equal(co_p, co_s)
+    blocks = int(info_p[11])
+    packed = np.zeros(int(L.mmf_jpeg_packed_bound(blocks)), np.uint8)
+    boff = np.zeros(blocks, np.uint32)
+    qt2 = np.zeros((3, 64), np.uint16)
+    used = ctypes.c_int64(0)
+    assert L.mmf_jpeg_entropy_packed(prog, len(prog), packed.ctypes.data, packed.size, boff.ctypes.data,
+                                     qt2.ctypes.data, ctypes.byref(used)) == 0
+    np.testing.assert_array_equal(unpack(packed, boff, blocks), co_s)
+
+
 def test_stage_packed_reserves_and_refuses_overflow():
     """mmf_jpeg_stage_packed (the staging call of mmf_amd/jpeg.py): records at the reserved offsets equal
     mmf_jpeg_entropy_packed's; an image that does not fit keeps its reservation and reports ERANGE."""
@@ -150,6 +172,8 @@ def test_unsupported_files_are_declined(name, data):
     assert rc == (-22 if name == "png" else -95)
     with pytest.raises((NotImplementedError, ValueError)):
         J.decode(data)
+    if name == "cmyk":  # files Pillow opens; the relabelled lossless one is not a real file
+        assert C.pillow_rgb(data).shape == (40, 48, 3)
 
 
 def test_truncated_and_corrupt_streams_do_not_crash():

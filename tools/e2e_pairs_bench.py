@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--json", default="")
+    ap.add_argument("--progressive", action="store_true", help="progressive JPEGs (Pillow's scan script)")
     a = ap.parse_args()
     from tokenizers import ByteLevelBPETokenizer
     from mmf_amd import io_utils
@@ -66,7 +67,7 @@ def main():
     rob = RobertaLike(bpe, [0], [2], 1, 510)
     clp = ClipLike(bpe, [49406], [49407], 49407, 75)
     texts = synth_texts(a.n, seed=4, words=40)[0]
-    jpegs = synth_jpegs(a.n)
+    jpegs = synth_jpegs(a.n, progressive=a.progressive)
     mf = MisinfoForensics(fusion_weights="", faiss_index_path="", synthetic_seed=0, roberta_tokenizer=rob,
                           clip_processor=clp, max_batch=a.n, verbose=False)
     g = np.random.default_rng(11)
@@ -131,7 +132,7 @@ def main():
            "pairs_per_s_pillow_decode": round(a.n / best["analyze_pairs_call_pillow_decode"], 1),
            "pairs_per_s_4_chunks_pillow_decode": round(4 * a.n / best["analyze_pairs_4_chunks_pillow_decode"], 1),
            "stage_ms": {k: round(1e3 * v, 2) for k, v in best.items()},
-           "note": "device JPEG decode (host entropy + device IDCT/upsample/colour) unless *_pillow_decode; synthetic 640x480 JPEGs, ~40-word texts, synthetic BPE tokenizers and weights; stages timed "
+           "note": "device JPEG decode (host entropy + device IDCT/upsample/colour) unless *_pillow_decode; synthetic 640x480 JPEGs" + (" (progressive)" if a.progressive else "") + ", ~40-word texts, synthetic BPE tokenizers and weights; stages timed "
                    "sequentially (analyze_pairs runs them in the same order)"}
     print(json.dumps(res), flush=True)
     if a.json:

@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mmf_amd import benchrun, io_utils  # noqa: E402
 
 
-def synth_jpegs(n, w=640, h=480, seed=3):
+def synth_jpegs(n, w=640, h=480, seed=3, progressive=False):
     from PIL import Image
     g = np.random.default_rng(seed)
     yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
@@ -35,7 +35,7 @@ def synth_jpegs(n, w=640, h=480, seed=3):
         a = np.stack([127 + 100 * np.sin(xx * f[c] + yy * f[(c + 1) % 3] + ph[c]) for c in range(3)], -1)
         a += g.normal(0, 8, size=a.shape)
         b = io.BytesIO()
-        Image.fromarray(np.clip(a, 0, 255).astype(np.uint8)).save(b, format="JPEG", quality=90)
+        Image.fromarray(np.clip(a, 0, 255).astype(np.uint8)).save(b, format="JPEG", quality=90, progressive=progressive)
         out.append(b.getvalue())
     return out
 

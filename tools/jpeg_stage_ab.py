@@ -18,9 +18,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=256)
 ap.add_argument("--workers", type=int, default=min(16, len(os.sched_getaffinity(0))))
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--progressive", action="store_true", help="progressive files (both legs)")
 a = ap.parse_args()
 L = hip.load()
-datas = [C.encode(C.photo_like(640, 480, seed=i % 16), quality=90, subsampling=2) for i in range(a.n)]
+datas = [C.encode(C.photo_like(640, 480, seed=i % 16), quality=90, subsampling=2, progressive=a.progressive)
+         for i in range(a.n)]
 info = np.zeros(16, np.int32)
 L.mmf_jpeg_header(datas[0], len(datas[0]), info.ctypes.data)
 blocks = int(info[11])
