@@ -42,8 +42,11 @@ struct Huff {
   int32_t acfast[1 << kLook];
 };
 
-bool build_huff(Huff& t, const uint8_t* bits, const uint8_t* vals, int nvals) {
+bool build_huff(Huff& t, const uint8_t* bits, const uint8_t* vals, int nvals, bool dc) {
   int code = 0, k = 0;
+  if (dc)  // jdhuff.c jpeg_make_d_derived_tbl: a DC symbol is a bit count, at most 15
+    for (int i = 0; i < nvals; ++i)
+      if (vals[i] > 15) return false;
   uint16_t huffcode[257];
   uint8_t huffsize[257];
   for (int l = 1; l <= 16; ++l)
@@ -169,7 +172,7 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
         int nv = 0;
         for (int i = 0; i < 16; ++i) nv += s[q + 1 + i];
         if (nv > 256 || q + 17 + nv > sl) return MMF_EINVAL;
-        if (!build_huff(tc ? j.ac[th] : j.dc[th], s + q + 1, s + q + 17, nv)) return MMF_EINVAL;
+        if (!build_huff(tc ? j.ac[th] : j.dc[th], s + q + 1, s + q + 17, nv, !tc)) return MMF_EINVAL;
         q += 17 + nv;
       }
     } else if (m == 0xDD) {
@@ -310,7 +313,7 @@ inline void decode_block(Bits& b, const Huff& dc, const Huff& ac, int& pred, int
     if (b.n < t) b.fill();
     diff = extend(b.get(t), t);
   }
-  pred += diff;
+  pred = (int)((uint32_t)pred + (uint32_t)diff);  // (wraps on corrupt data only)
   blk[0] = (int16_t)pred;
   for (int k = 1; k < 64; ++k) {
     if (b.n < 16) b.fill();
@@ -425,7 +428,7 @@ inline int decode_block_packed(Bits& b, const Huff& dc, const Huff& ac, int& pre
     if (b.n < t) b.fill();
     diff = extend(b.get(t), t);
   }
-  pred += diff;
+  pred = (int)((uint32_t)pred + (uint32_t)diff);  // (wraps on corrupt data only)
   if (pred) {
     mask = 1;
     val[n++] = (int16_t)pred;
@@ -517,7 +520,7 @@ int decode_progressive(Jpeg& j, int16_t* coefs, uint64_t* nzm) {
         int nv = 0;
         for (int i = 0; i < 16; ++i) nv += sg[q + 1 + i];
         if (nv > 256 || q + 17 + nv > sl) return MMF_EINVAL;
-        if (!build_huff(tc ? j.ac[th] : j.dc[th], sg + q + 1, sg + q + 17, nv)) return MMF_EINVAL;
+        if (!build_huff(tc ? j.ac[th] : j.dc[th], sg + q + 1, sg + q + 17, nv, !tc)) return MMF_EINVAL;
         q += 17 + nv;
       }
     } else if (m == 0xDD) {
@@ -572,8 +575,8 @@ int decode_progressive(Jpeg& j, int16_t* coefs, uint64_t* nzm) {
             int t = decode_sym(b, j.dc[td[i]]);
             if (t > 16) t = 16;
             const int diff = t ? extend(b.get(t), t) : 0;
-            pred[i] += diff;
-            blk[0] = (int16_t)(pred[i] * (1 << Al));
+            pred[i] = (int)((uint32_t)pred[i] + (uint32_t)diff);
+            blk[0] = (int16_t)((uint32_t)pred[i] << Al);
           } else if (get_bits(b, 1)) {  // DC refine
             blk[0] = (int16_t)(blk[0] | p1);
           }

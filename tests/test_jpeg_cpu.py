@@ -194,11 +194,13 @@ def test_truncated_and_corrupt_streams_do_not_crash():
         c_decode(L, bytes(bad))  # any rc; must not crash or write out of bounds
 
 
-def test_packed_staging_of_truncated_and_corrupt_streams():
+@pytest.mark.parametrize("which", ["sequential", "progressive"])
+def test_packed_staging_of_truncated_and_corrupt_streams(which):
     """The product's staging call on damaged scans: records stay inside the bound, every block offset
     points inside the written records (8-aligned), and the guard bytes after them are untouched."""
     L = lib()
-    d = CASES[9][1]  # 300x200 with restart markers
+    # 300x200 with restart markers
+    d = CASES[9][1] if which == "sequential" else [p for n, p, _ in C.progressive_pairs() if "300x200" in n][0]
     info = np.zeros(16, np.int32)
     assert L.mmf_jpeg_header(d, len(d), info.ctypes.data) == 0
     blocks = int(info[11])

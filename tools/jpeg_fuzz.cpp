@@ -1,0 +1,38 @@
+// Host-side fuzz of the JPEG entropy decoders (csrc/jpeg_host.cpp) under AddressSanitizer and
+// UndefinedBehaviorSanitizer (host code only; no GPU): random byte flips and truncations of the given
+// files through mmf_jpeg_header / mmf_jpeg_entropy / mmf_jpeg_entropy_packed, checking every block
+// offset lands inside the written records.
+//   g++ -O1 -g -fsanitize=address,undefined -std=c++17 -o /tmp/jpeg_fuzz \
+//       multi-modal-misinformation-detection-with-explanation-generation_amd/csrc/jpeg_host.cpp tools/jpeg_fuzz.cpp
+//   /tmp/jpeg_fuzz a.jpg b.jpg ...   (e.g. tests/jpeg_cases.py files, sequential and progressive)
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cstdint>
+#include <random>
+#include "../include/mmf_hip.h"
+int main(int argc, char** argv) {
+  std::mt19937 rng(1);
+  long ok = 0, runs = 0;
+  for (int a = 1; a < argc; ++a) {
+    FILE* f = fopen(argv[a], "rb"); std::vector<uint8_t> d(1 << 22); size_t n = fread(d.data(), 1, d.size(), f); fclose(f); d.resize(n);
+    for (int it = 0; it < 3000; ++it) {
+      std::vector<uint8_t> v = d;
+      int nf = 1 + rng() % 6;
+      for (int q = 0; q < nf; ++q) v[rng() % n] ^= (uint8_t)(1 + rng() % 255);
+      if (it % 5 == 0) v.resize(rng() % n + 1);
+      int32_t info[16];
+      if (mmf_jpeg_header(v.data(), v.size(), info)) continue;
+      ++runs;
+      std::vector<int16_t> co((size_t)info[11] * 64); uint16_t qt[192];
+      mmf_jpeg_entropy(v.data(), v.size(), co.data(), qt);
+      int64_t bound = mmf_jpeg_packed_bound(info[11]);
+      std::vector<uint8_t> out(bound); std::vector<uint32_t> boff(info[11]); int64_t used = 0;
+      if (mmf_jpeg_entropy_packed(v.data(), v.size(), out.data(), bound, boff.data(), qt, &used) == 0) {
+        ++ok;
+        for (int b = 0; b < info[11]; ++b) if (boff[b] >= used || boff[b] % 8) { printf("bad offset\n"); return 1; }
+      }
+    }
+  }
+  printf("runs %ld packed ok %ld\n", runs, ok);
+}
