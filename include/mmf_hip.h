@@ -118,8 +118,9 @@ int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, co
  * misinfo_forensics.py:255-258, decodes through Pillow's libjpeg-turbo).  Host: marker parsing and
  * Huffman entropy decoding (the serial part); device: dequantisation, islow IDCT, fancy chroma
  * upsampling and YCbCr -> RGB, pixels bit-exact with Pillow's decoder.  Supported: 8-bit baseline /
- * extended sequential Huffman JPEGs, one scan, grayscale or YCbCr 4:4:4 / 4:2:2 / 4:2:0; anything
- * else returns MMF_EUNSUPPORTED (decode that file on the host).
+ * extended sequential Huffman JPEGs with one scan, and progressive Huffman JPEGs (any scan script;
+ * quantisation tables fixed before the first scan), grayscale or YCbCr 4:4:4 / 4:2:2 / 4:2:0;
+ * anything else returns MMF_EUNSUPPORTED (decode that file on the host).
  *
  * mmf_jpeg_header: host-only, no handle.  info[MMF_JPEG_INFO_LEN] = {width, height, ncomp, hmax, vmax,
  * bw0, bh0, bw1, bh1, bw2, bh2, blocks, 0...} (bw_c x bh_c = component c's MCU-padded block grid;
@@ -128,7 +129,8 @@ int mmf_resize_pil(mmf_handle* h, const uint8_t* src, const int64_t* offsets, co
 int mmf_jpeg_header(const uint8_t* data, int64_t nbytes, int32_t* info);
 /* Host-only, thread-safe: quantised coefficients of every component as [bh_c][bw_c][64] int16
  * (natural order, components back to back) and the components' quantisation tables qt[c][64]
- * (natural order, uint16).  Replaces libjpeg's decode_mcu (jdhuff.c). */
+ * (natural order, uint16).  Replaces libjpeg's decode_mcu (jdhuff.c; progressive files: every scan
+ * accumulated as jdphuff.c does). */
 int mmf_jpeg_entropy(const uint8_t* data, int64_t nbytes, int16_t* coefs, uint16_t* qt);
 /* Host-only, thread-safe: the same coefficients packed for the H2D copy (~2.8x fewer bytes than the
  * dense planes on photos): one record per block -- uint64 mask of its nonzero ZIGZAG positions, then
