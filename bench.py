@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event-timed pass")
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs[1..3] lines")
     ap.add_argument("--no-per-sample", action="store_true", help="skip the B=1 / per-row API lines")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the text+JPEG analyze_pairs line")
     return ap.parse_args()
 
 
@@ -299,6 +300,11 @@ def main():
     per_sample = None
     if world == 1 and not a.no_per_sample:
         per_sample = per_sample_lines()
+    if world == 1 and not a.no_e2e:
+        benchrun.progress("text + JPEG line: analyze_pairs")
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+        import e2e_pairs_bench
+        per_sample = dict(per_sample or {}, text_jpeg_pairs=e2e_pairs_bench.bench_line())
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.cpu_seconds)

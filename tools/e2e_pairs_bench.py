@@ -52,6 +52,50 @@ class ClipLike(_BPE):
         return self._ids(self.bpe.encode_batch(list(text)), truncation, 77)
 
 
+def _forensics(n, progressive=False):
+    from tokenizers import ByteLevelBPETokenizer
+    from mmf_amd.api import MisinfoForensics
+    bpe = ByteLevelBPETokenizer()
+    bpe.train_from_iterator(synth_texts(4000, seed=9)[0], vocab_size=8000, min_frequency=2, show_progress=False)
+    rob = RobertaLike(bpe, [0], [2], 1, 510)
+    clp = ClipLike(bpe, [49406], [49407], 49407, 75)
+    texts = synth_texts(n, seed=4, words=40)[0]
+    jpegs = synth_jpegs(n, progressive=progressive)
+    mf = MisinfoForensics(fusion_weights="", faiss_index_path="", synthetic_seed=0, roberta_tokenizer=rob,
+                          clip_processor=clp, max_batch=n, verbose=False)
+    g = np.random.default_rng(11)
+    emb = g.standard_normal((2170, 512)).astype(np.float32)
+    mf.set_vault(emb, [{"title": t, "url": "u", "date": "d"} for t in synth_texts(2170, seed=12, words=12)[0]])
+    return mf, rob, texts, jpegs
+
+
+def bench_line(n=256, reps=3):
+    """bench.py's secondary line: analyze_pairs over n text + JPEG pairs (encoded bytes in host memory,
+    the reference's real input format), one call and a 4-chunk call, device JPEG decode vs Pillow."""
+    mf, _, texts, jpegs = _forensics(n)
+    best = {}
+    for chunks in (1, 4):
+        t4, j4 = texts * chunks, jpegs * chunks
+        for dj in (True, False):
+            mf.device_jpeg = dj
+            mf.analyze_pairs(t4, j4)  # warm
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                mf.analyze_pairs(t4, j4)
+                ts.append(time.perf_counter() - t0)
+            best[(chunks, dj)] = chunks * n / min(ts)
+    mf.engine.close()
+    return {"config": f"analyze_pairs over {n} text + JPEG pairs (synthetic 640x480 q90 4:2:0 JPEG bytes, "
+                      "~40-word texts, synthetic BPE tokenizers): decode + tokenise + resample + 5 signals + "
+                      "result dicts, host stages on the box's CPU share",
+            "value": round(best[(1, True)], 1), "unit": "pairs/s",
+            "pipelined_4_chunks": round(best[(4, True)], 1),
+            "pillow_decode": {"value": round(best[(1, False)], 1), "pipelined_4_chunks": round(best[(4, False)], 1)},
+            "note": "device JPEG path: host Huffman decoding into packed coefficients, IDCT / upsampling / colour "
+                    "and both resamplings on the GPU, pixels bit-exact with Pillow (tests/test_gpu_jpeg.py)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=256)
@@ -59,20 +103,8 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--progressive", action="store_true", help="progressive JPEGs (Pillow's scan script)")
     a = ap.parse_args()
-    from tokenizers import ByteLevelBPETokenizer
     from mmf_amd import io_utils
-    from mmf_amd.api import MisinfoForensics
-    bpe = ByteLevelBPETokenizer()
-    bpe.train_from_iterator(synth_texts(4000, seed=9)[0], vocab_size=8000, min_frequency=2, show_progress=False)
-    rob = RobertaLike(bpe, [0], [2], 1, 510)
-    clp = ClipLike(bpe, [49406], [49407], 49407, 75)
-    texts = synth_texts(a.n, seed=4, words=40)[0]
-    jpegs = synth_jpegs(a.n, progressive=a.progressive)
-    mf = MisinfoForensics(fusion_weights="", faiss_index_path="", synthetic_seed=0, roberta_tokenizer=rob,
-                          clip_processor=clp, max_batch=a.n, verbose=False)
-    g = np.random.default_rng(11)
-    emb = g.standard_normal((2170, 512)).astype(np.float32)
-    mf.set_vault(emb, [{"title": t, "url": "u", "date": "d"} for t in synth_texts(2170, seed=12, words=12)[0]])
+    mf, rob, texts, jpegs = _forensics(a.n, a.progressive)
     mf.analyze_pairs(texts, jpegs)  # warm (workspace growth, first launches)
     torch.cuda.synchronize()
 
