@@ -38,7 +38,7 @@ struct Huff {
   uint8_t huffval[256];
   uint16_t look[1 << kLook];  // (length << 8) | symbol, 0 = longer than kLook bits
   // AC fast path (libjpeg-turbo's idea): code + value bits within the lookahead ->
-  // (value << 16) | (run << 8) | total bits; 0 = take the symbol path
+  // (value << 16) | (run << 8) | total bits; 0 = take the symbol path; (1 << 15) | bits = end of block
   int32_t acfast[1 << kLook];
 };
 
@@ -88,6 +88,10 @@ bool build_huff(Huff& t, const uint8_t* bits, const uint8_t* vals, int nvals, bo
     const int e = t.look[lk];
     if (!e) continue;
     const int l = e >> 8, rs = e & 0xFF, r = rs >> 4, sz = rs & 15;
+    if (rs == 0) {  // end of block: flagged so the packed decoder ends the block without decode_sym
+      t.acfast[lk] = (1 << 15) | l;
+      continue;
+    }
     if (!sz || l + sz > kLook) continue;
     int v = (lk >> (kLook - l - sz)) & ((1 << sz) - 1);
     if (v < (1 << (sz - 1))) v -= (1 << sz) - 1;
@@ -319,8 +323,9 @@ inline void decode_block(Bits& b, const Huff& dc, const Huff& ac, int& pred, int
     if (b.n < 16) b.fill();
     const int32_t f = ac.acfast[b.peek(kLook)];
     if (f) {
-      k += (f >> 8) & 15;
       b.skip(f & 0xFF);
+      if (f & 0x8000) break;  // end of block
+      k += (f >> 8) & 15;
       blk[kZigzag[k]] = (int16_t)(f >> 16);
       continue;
     }
@@ -438,8 +443,9 @@ inline int decode_block_packed(Bits& b, const Huff& dc, const Huff& ac, int& pre
     const int32_t f = ac.acfast[b.peek(kLook)];
     int v;
     if (f) {
-      k += (f >> 8) & 15;
       b.skip(f & 0xFF);
+      if (f & 0x8000) break;  // end of block
+      k += (f >> 8) & 15;
       v = f >> 16;
     } else {
       const int rs = decode_sym(b, ac);
@@ -594,8 +600,9 @@ int decode_progressive(Jpeg& j, int16_t* coefs, uint64_t* nzm) {
             const int32_t f = ac.acfast[b.peek(kLook)];
             int v;
             if (f) {
-              k += (f >> 8) & 15;
               b.skip(f & 0xFF);
+              if (f & 0x8000) break;  // EOB0: a run of one block (this one), eobrun stays 0
+              k += (f >> 8) & 15;
               v = f >> 16;
             } else {
               const int rs = decode_sym(b, ac), r = rs >> 4, sz = rs & 15;
