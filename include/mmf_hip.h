@@ -147,6 +147,12 @@ int mmf_jpeg_entropy_packed(const uint8_t* data, int64_t nbytes, uint8_t* out, i
  * do not fit in dst_cap bytes: grow dst and place that image again (mmf_jpeg_entropy_packed). */
 int mmf_jpeg_stage_packed(const uint8_t* data, int64_t nbytes, uint8_t* dst, int64_t dst_cap, int64_t* cursor,
                           uint32_t* block_off, uint16_t* qt, int64_t* rec_off);
+/* Host-only: mmf_jpeg_stage_packed over n files on `nthreads` threads of its own (one C call per
+ * chunk: no per-file interpreter work); file k's block offsets go to block_off + block_base[k], its
+ * tables to qt + 192 k, its record offset to rec_off[k] and its status to rcs[k]. */
+int mmf_jpeg_stage_packed_batch(const uint8_t* const* datas, const int64_t* nbytes, int n, uint8_t* dst,
+                                int64_t dst_cap, int64_t* cursor, uint32_t* block_off, const int64_t* block_base,
+                                uint16_t* qt, int64_t* rec_off, int nthreads, int32_t* rcs);
 /* Device: B images' packed coefficients and tables -> uint8 RGBX pixels, bit-exact with Pillow's
  * decoder.  Every pointer is DEVICE memory: packed = the images' mmf_jpeg_entropy_packed records
  * (image i's at byte offset pk_off[i]), block_off uint32 = their block-offset tables concatenated

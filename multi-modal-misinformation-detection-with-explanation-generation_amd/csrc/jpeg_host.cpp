@@ -14,7 +14,9 @@
 // (row-major) order, c = 0, 1, 2 back to back; bw_c = mcux * h_c, bh_c = mcuy * v_c (the MCU-padded
 // block grid; blocks outside a single-component scan's extent stay zero, as in libjpeg).
 #include <cstdint>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/mmf_hip.h"
@@ -778,5 +780,25 @@ extern "C" int mmf_jpeg_stage_packed(const uint8_t* data, int64_t nbytes, uint8_
   *rec_off = off;
   if (off + used > dst_cap) return MMF_ERANGE;
   memcpy(dst + off, scratch.data(), used);
+  return 0;
+}
+
+extern "C" int mmf_jpeg_stage_packed_batch(const uint8_t* const* datas, const int64_t* nbytes, int n, uint8_t* dst,
+                                           int64_t dst_cap, int64_t* cursor, uint32_t* block_off,
+                                           const int64_t* block_base, uint16_t* qt, int64_t* rec_off, int nthreads,
+                                           int32_t* rcs) {
+  if (n < 0 || (n > 0 && (!datas || !nbytes || !dst || !cursor || !block_off || !block_base || !qt || !rec_off || !rcs)))
+    return MMF_EINVAL;
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (int k = next.fetch_add(1); k < n; k = next.fetch_add(1))
+      rcs[k] = mmf_jpeg_stage_packed(datas[k], nbytes[k], dst, dst_cap, cursor, block_off + block_base[k],
+                                     qt + 192 * (int64_t)k, rec_off + k);
+  };
+  const int nt = nthreads < 1 ? 1 : (nthreads > n ? n : nthreads);
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
   return 0;
 }

@@ -72,6 +72,8 @@ class JpegStager:
         self.copied = [None, None]  # torch.cuda.Event recorded after the H2D copy of each slot
         self.next_slot = 0
         self._pool = ThreadPoolExecutor(max_workers=self.workers)
+        # decode a chunk in one C call on the library's threads (MMF_JPEG_BATCH=0: per file on the pool)
+        self.batch_call = os.environ.get("MMF_JPEG_BATCH", "1") != "0"
 
     def close(self):
         self._pool.shutdown(wait=False)
@@ -129,11 +131,21 @@ class JpegStager:
         boff, qt, po = b + sec["block_off"], b + sec["qt"], pk_off.ctypes.data
         idx = st.index
 
-        def entropy(k):  # one C call per image (GIL released): decode, reserve room, copy
-            d = datas[idx[k]]
-            return lib.mmf_jpeg_stage_packed(d, len(d), dst, cap, cur, boff + int(coef_blocks[k]) * 4, qt + k * 384,
-                                             po + k * 8)
-        rcs = list(self._pool.map(entropy, range(n))) if n > 1 else [entropy(0)]
+        if self.batch_call:  # one C call for the chunk (GIL released; the library's own threads)
+            ds = [datas[i] for i in idx]
+            ptrs = (ctypes.c_char_p * n)(*ds)
+            lens = np.array([len(d) for d in ds], np.int64)
+            rcs_a = np.zeros(n, np.int32)
+            hip.check(lib.mmf_jpeg_stage_packed_batch(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, dst,
+                                                      cap, cur, boff, coef_blocks.ctypes.data, qt, po, self.workers,
+                                                      rcs_a.ctypes.data), "mmf_jpeg_stage_packed_batch")
+        else:  # one C call per file on the Python pool
+            def entropy(k):
+                d = datas[idx[k]]
+                return lib.mmf_jpeg_stage_packed(d, len(d), dst, cap, cur, boff + int(coef_blocks[k]) * 4,
+                                                 qt + k * 384, po + k * 8)
+            rcs_a = np.array(list(self._pool.map(entropy, range(n))) if n > 1 else [entropy(0)], np.int32)
+        rcs = rcs_a.tolist()
         overflow = [k for k, rc in enumerate(rcs) if rc == MMF_ERANGE]
         bad = [k for k, rc in enumerate(rcs) if rc not in (0, MMF_ERANGE)]
         if bad:  # (a header that parsed but a scan that did not: never seen; decode those on the host)

@@ -194,6 +194,46 @@ def test_truncated_and_corrupt_streams_do_not_crash():
         c_decode(L, bytes(bad))  # any rc; must not crash or write out of bounds
 
 
+def test_stage_packed_batch_equals_per_file_records():
+    """mmf_jpeg_stage_packed_batch (jpeg.py's chunk call, the library's own threads): every file's
+    records, block offsets and tables equal mmf_jpeg_entropy_packed's, at its reserved offset; a
+    file past the capacity reports ERANGE."""
+    L = lib()
+    files = [d for _, d in CASES] + [p for _, p, _ in C.progressive_pairs()]
+    infos = [c_decode(L, d)[1] for d in files]
+    blocks = np.array([int(i[11]) for i in infos], np.int64)
+    base = np.r_[0, np.cumsum(blocks)[:-1]].astype(np.int64)
+    n = len(files)
+    dst = np.zeros(1 << 22, np.uint8)
+    cursor = np.zeros(1, np.int64)
+    boff = np.zeros(int(blocks.sum()), np.uint32)
+    qt = np.zeros((n, 3, 64), np.uint16)
+    rec = np.zeros(n, np.int64)
+    rcs = np.full(n, 7, np.int32)
+    ptrs = (ctypes.c_char_p * n)(*files)
+    lens = np.array([len(d) for d in files], np.int64)
+    assert L.mmf_jpeg_stage_packed_batch(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, dst.ctypes.data,
+                                         dst.size, cursor.ctypes.data, boff.ctypes.data, base.ctypes.data,
+                                         qt.ctypes.data, rec.ctypes.data, 4, rcs.ctypes.data) == 0
+    assert not rcs.any()
+    for k, d in enumerate(files):
+        ref = np.zeros(int(L.mmf_jpeg_packed_bound(int(blocks[k]))), np.uint8)
+        b2 = np.zeros(int(blocks[k]), np.uint32)
+        q2 = np.zeros((3, 64), np.uint16)
+        used = ctypes.c_int64(0)
+        assert L.mmf_jpeg_entropy_packed(d, len(d), ref.ctypes.data, ref.size, b2.ctypes.data, q2.ctypes.data,
+                                         ctypes.byref(used)) == 0
+        np.testing.assert_array_equal(dst[rec[k]:rec[k] + used.value], ref[:used.value])
+        np.testing.assert_array_equal(boff[base[k]:base[k] + blocks[k]], b2)
+        np.testing.assert_array_equal(qt[k], q2)
+    cursor[0] = 0
+    small = 4096
+    assert L.mmf_jpeg_stage_packed_batch(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, dst.ctypes.data,
+                                         small, cursor.ctypes.data, boff.ctypes.data, base.ctypes.data,
+                                         qt.ctypes.data, rec.ctypes.data, 4, rcs.ctypes.data) == 0
+    assert set(rcs.tolist()) <= {0, -34} and (rcs == -34).any()
+
+
 @pytest.mark.parametrize("which", ["sequential", "progressive"])
 def test_packed_staging_of_truncated_and_corrupt_streams(which):
     """The product's staging call on damaged scans: records stay inside the bound, every block offset

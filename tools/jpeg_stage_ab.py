@@ -49,7 +49,19 @@ def f_packed(k):  # the product's staging call (jpeg.py): decode + reserve + cop
                                    rec_off.ctypes.data + k * 8)
 
 
-res = {"dense": [], "packed": []}
+ptrs = (ctypes.c_char_p * a.n)(*datas)
+lens = np.array([len(d) for d in datas], np.int64)
+bases = np.arange(a.n, dtype=np.int64) * blocks
+rcs = np.zeros(a.n, np.int32)
+
+
+def batch_call():
+    return L.mmf_jpeg_stage_packed_batch(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, a.n, stage.ctypes.data,
+                                         stage.size, cursor.ctypes.data, boff.ctypes.data, bases.ctypes.data,
+                                         qt.ctypes.data, rec_off.ctypes.data, a.workers, rcs.ctypes.data)
+
+
+res = {"dense": [], "packed": [], "packed_batch": []}
 for r in range(a.reps + 1):
     for name, f in (("dense", f_dense), ("packed", f_packed)):
         cursor[0] = 0
@@ -57,6 +69,11 @@ for r in range(a.reps + 1):
         assert not any(pool.map(f, range(a.n)))
         if r:
             res[name].append((time.perf_counter() - t) * 1e3)
+    cursor[0] = 0
+    t = time.perf_counter()
+    assert batch_call() == 0 and not rcs.any()
+    if r:
+        res["packed_batch"].append((time.perf_counter() - t) * 1e3)
 print(f"n={a.n} workers={a.workers} blocks/img={blocks} packed bytes/img={cursor[0] / a.n / 1e3:.0f} KB "
       f"dense {blocks * 128 / 1e3:.0f} KB")
 for k, v in res.items():
