@@ -147,6 +147,10 @@ int mmf_jpeg_entropy_packed(const uint8_t* data, int64_t nbytes, uint8_t* out, i
  * do not fit in dst_cap bytes: grow dst and place that image again (mmf_jpeg_entropy_packed). */
 int mmf_jpeg_stage_packed(const uint8_t* data, int64_t nbytes, uint8_t* dst, int64_t dst_cap, int64_t* cursor,
                           uint32_t* block_off, uint16_t* qt, int64_t* rec_off);
+/* Host-only: mmf_jpeg_header over n files (null datas[k] -> MMF_EINVAL) on up to `nthreads` threads;
+ * infos [n][MMF_JPEG_INFO_LEN], rcs[k] = file k's return code. */
+int mmf_jpeg_header_batch(const uint8_t* const* datas, const int64_t* nbytes, int n, int32_t* infos, int32_t* rcs,
+                          int nthreads);
 /* Host-only: mmf_jpeg_stage_packed over n files on `nthreads` threads of its own (one C call per
  * chunk: no per-file interpreter work); file k's block offsets go to block_off + block_base[k], its
  * tables to qt + 192 k, its record offset to rec_off[k] and its status to rcs[k]. */

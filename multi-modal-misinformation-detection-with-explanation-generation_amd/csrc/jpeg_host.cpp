@@ -802,3 +802,19 @@ extern "C" int mmf_jpeg_stage_packed_batch(const uint8_t* const* datas, const in
   for (auto& th : pool) th.join();
   return 0;
 }
+
+extern "C" int mmf_jpeg_header_batch(const uint8_t* const* datas, const int64_t* nbytes, int n, int32_t* infos,
+                                     int32_t* rcs, int nthreads) {
+  if (n < 0 || (n > 0 && (!datas || !nbytes || !infos || !rcs))) return MMF_EINVAL;
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (int k = next.fetch_add(1); k < n; k = next.fetch_add(1))
+      rcs[k] = datas[k] ? mmf_jpeg_header(datas[k], nbytes[k], infos + (int64_t)k * MMF_JPEG_INFO_LEN) : MMF_EINVAL;
+  };
+  const int nt = nthreads < 1 ? 1 : (nthreads > (n + 15) / 16 ? (n + 15) / 16 : nthreads);  // >= 16 files a thread
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  return 0;
+}

@@ -37,6 +37,7 @@ SIGNATURES = {
     "mmf_jpeg_packed_bound": (ctypes.c_int64, [ctypes.c_int32]),
     "mmf_jpeg_entropy_packed": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, _P]),
     "mmf_jpeg_stage_packed": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, _P, _P]),
+    "mmf_jpeg_header_batch": (_I, [_P, _P, _I, _P, _P, _I]),
     "mmf_jpeg_stage_packed_batch": (_I, [_P, _P, _I, _P, ctypes.c_int64, _P, _P, _P, _P, _P, _I, _P]),
     "mmf_jpeg_reconstruct": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "mmf_set_vault": (_I, [_P, _P, _I, _I]),

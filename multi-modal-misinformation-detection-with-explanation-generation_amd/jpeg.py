@@ -82,18 +82,20 @@ class JpegStager:
         st = Staged()
         lib = self.lib
 
-        def header(d):
-            if d is None:
-                return None
-            info = np.zeros(INFO_LEN, np.int32)
-            rc = lib.mmf_jpeg_header(d, len(d), info.ctypes.data)
-            return info if rc == 0 else None
-        infos = list(self._pool.map(header, datas)) if len(datas) > 1 else [header(d) for d in datas]
-        st.index = [i for i, inf in enumerate(infos) if inf is not None]
+        m = len(datas)
+        if m == 0:
+            return st
+        hptrs = (ctypes.c_char_p * m)(*datas)  # None -> NULL: declined
+        hlens = np.array([len(d) if d is not None else 0 for d in datas], np.int64)
+        allinf = np.zeros((m, INFO_LEN), np.int32)
+        hrc = np.zeros(m, np.int32)
+        hip.check(lib.mmf_jpeg_header_batch(ctypes.cast(hptrs, ctypes.c_void_p), hlens.ctypes.data, m,
+                                            allinf.ctypes.data, hrc.ctypes.data, self.workers), "mmf_jpeg_header_batch")
+        st.index = np.flatnonzero(hrc == 0).tolist()
         n = len(st.index)
         if n == 0:
             return st
-        inf = np.stack([infos[i] for i in st.index]).astype(np.int32)
+        inf = np.ascontiguousarray(allinf[st.index])
         blocks = inf[:, 11].astype(np.int64)
         pixels = inf[:, 0].astype(np.int64) * inf[:, 1]
         coef_blocks = np.zeros(n, np.int64)

@@ -194,6 +194,25 @@ def test_truncated_and_corrupt_streams_do_not_crash():
         c_decode(L, bytes(bad))  # any rc; must not crash or write out of bounds
 
 
+def test_header_batch_equals_per_file():
+    L = lib()
+    files = [d for _, d in CASES] + [d for _, d in C.unsupported_files()] + [None, b"", b"\xff\xd8"]
+    n = len(files)
+    ptrs = (ctypes.c_char_p * n)(*files)
+    lens = np.array([len(d) if d is not None else 0 for d in files], np.int64)
+    infos = np.full((n, 16), -7, np.int32)
+    rcs = np.full(n, 7, np.int32)
+    assert L.mmf_jpeg_header_batch(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, infos.ctypes.data,
+                                   rcs.ctypes.data, 3) == 0
+    for k, d in enumerate(files):
+        if d is None:
+            assert rcs[k] == -22
+            continue
+        info = np.zeros(16, np.int32)
+        assert rcs[k] == L.mmf_jpeg_header(d, len(d), info.ctypes.data)
+        np.testing.assert_array_equal(infos[k], info)
+
+
 def test_stage_packed_batch_equals_per_file_records():
     """mmf_jpeg_stage_packed_batch (jpeg.py's chunk call, the library's own threads): every file's
     records, block offsets and tables equal mmf_jpeg_entropy_packed's, at its reserved offset; a
