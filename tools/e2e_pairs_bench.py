@@ -2,7 +2,9 @@
 the reference's `analyze(text, image)` for a batch of real-format inputs, with the time split into
 its host and device stages.
 
-    python tools/e2e_pairs_bench.py [--n 256] [--reps 3] [--json out.json]
+    python tools/e2e_pairs_bench.py [--n 256] [--reps 3] [--progressive] [--json out.json]
+
+`bench_line()` is bench.py's `per_sample.text_jpeg_pairs` line (the same calls, fewer stage splits).
 
 Inputs: synthetic 640x480 JPEGs (tools/host_pipeline_bench.py) and ~40-word texts; tokenizers are
 byte-level BPEs trained on a synthetic corpus and wrapped with RoBERTa's / CLIP's special-token and
