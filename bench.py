@@ -5,6 +5,11 @@ batch 256 pairs per GPU, synthetic inputs, random-init weights of the reference 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+Both multi-GPU forms run the same ranks: started directly with --gpus N > 1 (no WORLD_SIZE in the
+environment), this process launches N rank processes itself (benchrun.launch_ranks: RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_* set as torchrun sets them, before anything touches the GPU),
+relays rank 0's JSON line and exits with the first failing rank's code.
+
 `value` follows SURVEY.md §8d: each step's inputs (int32 token ids + uint8 images, 38.96 MB per 256
 pairs) start in pinned HOST memory and cross PCIe inside the timed region (double-buffered H2D on a
 copy stream, engine.HostPipeline), and the result tensors come back D2H.  The HBM-resident rate
@@ -52,6 +57,9 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs[1..3] lines")
     ap.add_argument("--no-per-sample", action="store_true", help="skip the B=1 / per-row API lines")
     ap.add_argument("--no-e2e", action="store_true", help="skip the text+JPEG analyze_pairs line")
+    ap.add_argument("--cpu-standin", action="store_true",
+                    help="TEST ONLY: the rank launch, gloo barriers and max-over-ranks timing around a CPU "
+                         "stand-in step (no GPU, no HIP library); the JSON line says so in `data`")
     return ap.parse_args()
 
 
@@ -255,9 +263,62 @@ def per_sample_lines(n_lat: int = 200, n_rows: int = 64, warmup: int = 10):
                                                                  "behaviour, misinfo_forensics.py:395, 438)"}}}
 
 
+METRIC = "text+image pairs/sec through full analyze() 5-signal path, batch=256"
+WORKLOAD = ("Full MisinfoForensics.analyze() 5-signal pipeline incl. Truth-Vault lookup (BASELINE configs[4]), "
+            "text L=128, caption L=77, 224x224 images; inputs H2D and results D2H inside the timed region "
+            "(SURVEY.md §8d)")
+
+
+def result_line(a, world: int, B: int, dt: float, value: float, data: str, **extra) -> dict:
+    """The one JSON line rank 0 prints (the driver's contract)."""
+    res = {"metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": data,
+           "config": {"workload": WORKLOAD, "global_batch": world * B, "batch_per_gpu": B, "seq_len": 128,
+                      "parallelism": f"replicas x{world} (no data-path collective)"}}
+    cfg_extra = extra.pop("config_extra", None)
+    if cfg_extra:
+        res["config"].update(cfg_extra)
+    res.update(extra)
+    return res
+
+
+def standin_main(a, world: int, rank: int) -> None:
+    """--cpu-standin: everything bench.py does around the step -- the rank environment, gloo
+    barriers, exactly K timed steps, the max over ranks, the whole-job rate and the JSON line --
+    with a CPU stand-in step (a [B,768]x[768,768] matmul per pair batch) instead of the HIP path.
+    tests/test_multiproc_cpu.py runs `python bench.py --gpus 2 --cpu-standin` through it."""
+    fail = os.environ.get("MMF_STANDIN_FAIL_RANK", "")
+    if fail.isdigit() and int(fail) == rank:
+        raise SystemExit(f"rank {rank}: failing on request (MMF_STANDIN_FAIL_RANK)")
+    torch.set_num_threads(1)
+    dist = benchrun.init_dist(world, "gloo")
+    B = a.batch
+    g = torch.Generator().manual_seed(benchrun.input_seed(rank))
+    x, w = torch.randn(B, 768, generator=g), torch.randn(768, 768, generator=g)
+    dt = benchrun.timed_steps(lambda: torch.mm(x, w), a.steps, a.warmup, dist)
+    value = benchrun.whole_job_rate(world, B, a.steps, dt)
+    if rank == 0:
+        res = result_line(a, world, B, dt, value, "cpu stand-in step (test of the rank launch; not a measurement)",
+                          config_extra={"rank_launch": "bench.py" if os.environ.get("MMF_BENCH_PARENT") else
+                                        "external"})
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if benchrun.needs_launch(a.gpus):
+        # the driver's `python bench.py --gpus N`: become the parent of N ranks (never touches the GPU)
+        os.environ["MMF_BENCH_PARENT"] = "1"
+        cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(benchrun.launch_ranks(a.gpus, cmd, check_devices=not a.cpu_standin))
     world, rank, local = benchrun.rank_env()
+    if world != a.gpus:
+        benchrun.progress(f"note: --gpus {a.gpus} but the launcher started {world} rank(s); reporting {world}")
+    if a.cpu_standin:
+        return standin_main(a, world, rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = benchrun.init_dist(world, "nccl", dev)
@@ -309,21 +370,14 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.cpu_seconds)
     if rank == 0:
-        res = {"metric": "text+image pairs/sec through full analyze() 5-signal path, batch=256",
-               "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": a.steps,
-               "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
-               "data": "synthetic (seeded token ids, structured uint8 images, 2170-row vault); random-init weights",
-               "config": {"workload": "Full MisinfoForensics.analyze() 5-signal pipeline incl. Truth-Vault lookup "
-                                      "(BASELINE configs[4]), text L=128, caption L=77, 224x224 images; inputs H2D "
-                                      "and results D2H inside the timed region (SURVEY.md §8d)",
-                          "global_batch": world * B, "batch_per_gpu": B, "seq_len": 128,
-                          "parallelism": f"replicas x{world} (no data-path collective)",
-                          "h2d_bytes_per_step_per_gpu": h2d},
-               "hbm_resident": {"value": round(hbm, 2), "unit": "pairs/s", "ms_per_step": round(1000 * dt_hbm / a.steps, 3),
-                                "note": "same step with inputs already in HBM and results left on the device"},
-               "achieved_tflops_whole_path": round(value * GFLOP_PER_PAIR / 1e3, 1),
-               "roofline": roofline, "configs": configs, "per_sample": per_sample, "cpu_baseline": cpu}
+        res = result_line(
+            a, world, B, dt, value,
+            "synthetic (seeded token ids, structured uint8 images, 2170-row vault); random-init weights",
+            config_extra={"h2d_bytes_per_step_per_gpu": h2d},
+            hbm_resident={"value": round(hbm, 2), "unit": "pairs/s", "ms_per_step": round(1000 * dt_hbm / a.steps, 3),
+                          "note": "same step with inputs already in HBM and results left on the device"},
+            achieved_tflops_whole_path=round(value * GFLOP_PER_PAIR / 1e3, 1),
+            roofline=roofline, configs=configs, per_sample=per_sample, cpu_baseline=cpu)
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

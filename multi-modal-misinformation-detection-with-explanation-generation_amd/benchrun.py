@@ -2,8 +2,10 @@
 the CPU test suite exactly as it runs on an 8-GPU node (tests/test_multiproc_cpu.py::
 test_benchrun_gloo_world2 drives these functions over a gloo world of 2 with a CPU stand-in engine).
 
-One process per GPU (torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE and
-MASTER_*); the batch is sharded by rank with no collective on the data path:
+One process per GPU: torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE and
+MASTER_*, or `bench.py --gpus N` started directly becomes the parent of N rank processes itself
+(`launch_ranks`, before anything touches the GPU); the batch is sharded by rank with no collective
+on the data path:
 every rank times its own steps, the barrier brackets the timed region, and the whole-job time is
 the MAX over ranks (one all_reduce of one float) -- the only collective traffic.
 """
@@ -24,6 +26,71 @@ def rank_env() -> tuple:
     """(world, rank, local_rank) from the launcher's environment (1, 0, 0 when run directly)."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def needs_launch(n: int) -> bool:
+    """`bench.py --gpus N` started directly (no launcher environment) with N > 1: this process
+    becomes the parent of N rank processes instead of running a step itself."""
+    return n > 1 and "WORLD_SIZE" not in os.environ
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, cmd: list, check_devices: bool = True, poll_s: float = 0.2) -> int:
+    """Run `cmd` as N rank processes on this node, the way torch.distributed.run would: each child
+    gets RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = N and MASTER_ADDR / MASTER_PORT
+    (127.0.0.1, a free port).  The parent never touches the GPU (no HIP call, so no exec or fork
+    hazard after device initialisation; `torch.cuda.device_count()` does not initialise HIP on this
+    image); it relays rank 0's stdout (the JSON line) and returns the first non-zero child exit
+    code, terminating the other ranks, or 0 when every rank succeeded."""
+    import subprocess
+    import threading
+    if check_devices:
+        have = torch.cuda.device_count()
+        if have < n:
+            progress(f"--gpus {n}: only {have} HIP device(s) visible")
+            return 2
+    env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr))
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line.decode())
+            sys.stdout.flush()
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    rc = 0
+    live = set(range(n))
+    stop_at = None
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                progress(f"rank {r} exited with {c}: stopping the other ranks")
+                for q in live:
+                    procs[q].terminate()
+                stop_at = time.monotonic()
+        if stop_at is not None and time.monotonic() - stop_at > 30:
+            for q in live:  # a rank stuck in a collective ignores SIGTERM
+                procs[q].kill()
+        time.sleep(poll_s)
+    t.join(timeout=10)
+    return rc
 
 
 def input_seed(rank: int) -> int:

@@ -116,3 +116,43 @@ def test_benchrun_single_process():
     dt = benchrun.timed_steps(lambda: n.append(1), steps=3, warmup=1)
     assert len(n) == 4 and dt >= 0
     assert benchrun.usable_cpus() >= 1
+
+
+def _run_bench(args, env=None, timeout=180):
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MMF_BENCH_PARENT")}
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + args, env=e, cwd=repo,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """The driver's exact form, `python bench.py --gpus 2` (no launcher): bench.py starts the two
+    ranks itself and rank 0's line reports the whole job."""
+    rc, res, p = _run_bench(["--gpus", "2", "--steps", "4", "--warmup", "1", "--cpu-standin"])
+    assert rc == 0, p.stderr[-2000:]
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"].startswith("replicas x2")
+    assert res["config"]["rank_launch"] == "bench.py"
+    assert res["config"]["global_batch"] == 512 and res["scaling"] == "weak"
+    # value = all ranks' pairs / the max-over-ranks time
+    assert res["value"] == pytest.approx(2 * 256 * 4 / (res["ms_per_step"] * 4 / 1000), rel=2e-3)
+    assert sum(ln.startswith("{") for ln in p.stdout.splitlines()) == 1  # one JSON line
+
+
+def test_bench_gpus1_is_a_single_process():
+    rc, res, p = _run_bench(["--gpus", "1", "--steps", "2", "--warmup", "1", "--cpu-standin"])
+    assert rc == 0, p.stderr[-2000:]
+    assert res["n_gpus"] == 1 and res["config"]["parallelism"].startswith("replicas x1")
+    assert res["config"]["rank_launch"] == "external"  # no child processes were started
+
+
+def test_bench_failing_rank_fails_the_launch():
+    rc, res, p = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-standin"],
+                            env={"MMF_STANDIN_FAIL_RANK": "1"})
+    assert rc != 0 and res is None
+    assert "rank 1 exited" in p.stderr
