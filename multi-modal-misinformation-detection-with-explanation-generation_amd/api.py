@@ -236,6 +236,28 @@ def _load_pretrained_states(clip_model_dir: str):
     return det, clip
 
 
+CLIP_EOS_DEFAULT = 49407  # openai/clip-vit-base-patch32's text_config.eos_token_id
+
+
+def clip_eos_token_id(clip_model_dir: Optional[str]) -> int:
+    """The id the CLIP text tower pools at: `text_config.eos_token_id` of the CLIP config in
+    `clip_model_dir` -- the value transformers' CLIPTextTransformer keys its pooling on (the first
+    position holding it; the legacy id 2 means argmax(ids), handled by the device kernel too) --,
+    overridden by MMF_CLIP_EOS_TOKEN_ID, 49407 when no config is available offline."""
+    env = os.environ.get("MMF_CLIP_EOS_TOKEN_ID")
+    if env:
+        return int(env)
+    if clip_model_dir:
+        try:
+            from transformers import CLIPConfig
+            eos = CLIPConfig.from_pretrained(clip_model_dir, local_files_only=True).text_config.eos_token_id
+            if eos is not None:
+                return int(eos)
+        except Exception:  # noqa: BLE001  (no local config: the published model's id)
+            pass
+    return CLIP_EOS_DEFAULT
+
+
 def resolve_states(detector_state, clip_state, synthetic_seed: Optional[int], clip_model_dir: str,
                    loader=None):
     """Constructor weights: explicit states > synthetic seed > local pretrained files, each
@@ -370,9 +392,7 @@ class MisinfoForensics:
             self._load_individual_weights(ai_head_weights, misinfo_head_weights, efficientnet_weights, clip_weights)
         self.detector.eval()
 
-        eos = 49407
-        cfg = getattr(getattr(self.clip_processor, "tokenizer", None), "eos_token_id", None)
-        self.clip_eos_token_id = int(os.environ.get("MMF_CLIP_EOS_TOKEN_ID", eos))
+        self.clip_eos_token_id = clip_eos_token_id(clip_model_dir)
         self.engine = Engine(self.device.index or 0, None, clip_state, eos_token_id=self.clip_eos_token_id,
                              max_batch=max_batch, max_text_len=max_text_len)
         # fp32 EfficientNet activations: for towers whose logits reach O(100), where
@@ -784,7 +804,8 @@ class CLIPSimilarityEngine:
                 processor = CLIPProcessor.from_pretrained(model_name, local_files_only=True)
             self.processor = processor
             self.threshold = threshold
-            self.model = Engine(torch.device(self.device).index or 0, None, clip_state, max_batch=64)
+            self.model = Engine(torch.device(self.device).index or 0, None, clip_state, max_batch=64,
+                                eos_token_id=clip_eos_token_id(model_name))
             print(f"Model loaded successfully on {self.device}")
         except Exception as e:  # noqa: BLE001
             raise RuntimeError(f"Failed to load CLIP model: {str(e)}")

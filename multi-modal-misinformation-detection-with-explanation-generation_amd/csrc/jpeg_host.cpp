@@ -104,13 +104,14 @@ bool build_huff(Huff& t, const uint8_t* bits, const uint8_t* vals, int nvals, bo
 }
 
 struct Comp {
-  int id, h, v, tq, td, ta;
+  int id = 0, h = 0, v = 0, tq = 0, td = 0, ta = 0;
 };
 
 struct Jpeg {
   int width = 0, height = 0, ncomp = 0, restart = 0, adobe = -1;
+  bool jfif = false;
   Comp comp[4];
-  int nscan = 0, scomp[4];
+  int nscan = 0, scomp[4] = {0, 0, 0, 0};
   uint16_t qt[4][64];
   bool qt_present[4] = {false, false, false, false};
   Huff dc[4], ac[4];
@@ -184,6 +185,8 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
     } else if (m == 0xDD) {
       if (sl < 2) return MMF_EINVAL;
       j.restart = (s[0] << 8) | s[1];
+    } else if (m == 0xE0) {
+      if (sl >= 5 && memcmp(s, "JFIF", 5) == 0) j.jfif = true;
     } else if (m == 0xEE) {
       if (sl >= 12 && memcmp(s, "Adobe", 5) == 0) j.adobe = s[11];
     } else if (m == 0xDA) {
@@ -193,14 +196,19 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
         j.end = d + n;
         break;
       }
+      if (sl < 1 || sl < 4 + 2 * s[0]) return MMF_EINVAL;  // Ns, Ns x (Cs, Td/Ta), Ss, Se, Ah/Al
       j.nscan = s[0];
       if (j.nscan != j.ncomp) return MMF_EUNSUPPORTED;  // multi-scan sequential
+      bool seen[4] = {false, false, false, false};
       for (int i = 0; i < j.nscan; ++i) {
         const int cid = s[1 + 2 * i], tt = s[2 + 2 * i];
         int ci = -1;
         for (int c = 0; c < j.ncomp; ++c)
           if (j.comp[c].id == cid) ci = c;
-        if (ci < 0) return MMF_EINVAL;
+        // libjpeg's JERR_BAD_COMPONENT_ID: unknown or repeated ids (with Ns == Nf and no repeats, every
+        // frame component is in the scan, so every td / ta below is set)
+        if (ci < 0 || seen[ci]) return MMF_EINVAL;
+        seen[ci] = true;
         j.scomp[i] = ci;
         j.comp[ci].td = (tt >> 4) & 3;
         j.comp[ci].ta = tt & 3;
@@ -212,6 +220,20 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
     p += L;
   }
   if (!j.scan) return MMF_EINVAL;
+  // Pillow raises "image file is truncated" when the data ends before the EOI marker (its decoder
+  // asks for more bytes); such files go to Pillow so the error is the reference's.  Entropy-coded
+  // data stuffs every 0xFF data byte as FF 00, so FF D9 can only be a marker.
+  {
+    const uint8_t* q = j.scan;
+    bool eoi = false;
+    while (!eoi && q + 1 < j.end) {
+      q = (const uint8_t*)memchr(q, 0xFF, (size_t)(j.end - 1 - q));
+      if (!q) break;
+      eoi = q[1] == 0xD9;
+      ++q;
+    }
+    if (!eoi) return MMF_EUNSUPPORTED;
+  }
   for (int c = 0; c < j.ncomp; ++c) {
     if (!j.qt_present[j.comp[c].tq]) return MMF_EINVAL;
     if (!j.progressive && (!j.dc[j.comp[c].td].present || !j.ac[j.comp[c].ta].present)) return MMF_EINVAL;
@@ -220,6 +242,10 @@ int parse(const uint8_t* d, int64_t n, Jpeg& j) {
   }
   if (j.ncomp == 3) {
     if (j.adobe == 0) return MMF_EUNSUPPORTED;  // untransformed (RGB) JPEG
+    // libjpeg's default_decompress_parms: no JFIF and no Adobe marker, component ids 'R' 'G' 'B'
+    // -> an RGB file (decoded by Pillow)
+    if (!j.jfif && j.adobe < 0 && j.comp[0].id == 82 && j.comp[1].id == 71 && j.comp[2].id == 66)
+      return MMF_EUNSUPPORTED;
     // luma h, v in {1, 2}, chroma 1x1 (4:4:4, 4:2:2, 4:2:0; 4:4:0 decodes through Pillow)
     if (j.comp[0].h > 2 || j.comp[0].v > 2 || j.comp[1].h != 1 || j.comp[1].v != 1 || j.comp[2].h != 1 ||
         j.comp[2].v != 1 || (j.comp[0].h == 1 && j.comp[0].v == 2))

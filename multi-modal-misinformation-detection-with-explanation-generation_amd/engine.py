@@ -108,7 +108,8 @@ class Engine:
         arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
         ps = arrs[0].shape[2] if arrs else 3
         for a in arrs:
-            assert a.ndim == 3 and a.shape[2] == ps and ps in (3, 4), f"expected HxWx{ps} uint8, got {a.shape}"
+            if not (a.ndim == 3 and a.shape[2] == ps and ps in (3, 4)):
+                raise ValueError(f"expected HxWx{ps} uint8, got {a.shape}")
         sizes = [a.nbytes for a in arrs]
         offs = np.zeros(len(arrs), np.int64)
         if arrs:
@@ -144,8 +145,8 @@ class Engine:
 
     def _u8(self, x) -> torch.Tensor:
         t = torch.as_tensor(x)
-        assert t.dtype == torch.uint8 and t.dim() == 4 and tuple(t.shape[1:]) == (224, 224, 3), \
-            f"images must be uint8 [B,224,224,3], got {tuple(t.shape)} {t.dtype}"
+        if not (t.dtype == torch.uint8 and t.dim() == 4 and tuple(t.shape[1:]) == (224, 224, 3)):
+            raise ValueError(f"images must be uint8 [B,224,224,3], got {tuple(t.shape)} {t.dtype}")
         return t.to(self.device).contiguous()
 
     def _f32(self, *shape) -> torch.Tensor:
@@ -170,7 +171,8 @@ class Engine:
     def effnet_forward_f32(self, x):
         """Normalised fp32 NCHW input (detector.forward_image semantics)."""
         x = torch.as_tensor(x, dtype=torch.float32).to(self.device).contiguous()
-        assert x.dim() == 4 and tuple(x.shape[1:]) == (3, 224, 224), f"expected [B,3,224,224], got {tuple(x.shape)}"
+        if not (x.dim() == 4 and tuple(x.shape[1:]) == (3, 224, 224)):
+            raise ValueError(f"expected [B,3,224,224], got {tuple(x.shape)}")
         B = x.shape[0]
         lg, sc = self._f32(B, 2), self._f32(B)
         check(self.lib.mmf_effnet_forward_f32(self.h, ptr(x), B, ptr(lg), ptr(sc), stream_ptr()),

@@ -9,8 +9,10 @@ positions + their values: ~0.35 MB for a 640x480 q90 photo instead of 0.92 MB of
 a pinned staging buffer, one H2D copy moves them, and the device reconstructs the pixels (csrc/jpeg.hip: islow IDCT, fancy chroma upsampling, YCbCr -> RGB,
 bit-exact with Pillow) as RGBX images that feed the Pillow-exact resampler (mmf_resize_pil).
 Progressive files are decoded scan by scan into the same coefficients.  Files the C decoder does
-not take (CMYK, 4:4:0, lossless / arithmetic / 12-bit, ...) report MMF_EUNSUPPORTED and are
-decoded by Pillow on the host, as before.
+not take (CMYK, 4:4:0, lossless / arithmetic / 12-bit, RGB-id files, files whose data ends before
+the EOI marker, ...) report MMF_EUNSUPPORTED and are decoded by Pillow on the host, as before (so a
+truncated file raises Pillow's "image file is truncated", as in the reference); so are images past
+the device resampler's tap budget.
 """
 from __future__ import annotations
 
@@ -91,7 +93,13 @@ class JpegStager:
         hrc = np.zeros(m, np.int32)
         hip.check(lib.mmf_jpeg_header_batch(ctypes.cast(hptrs, ctypes.c_void_p), hlens.ctypes.data, m,
                                             allinf.ctypes.data, hrc.ctypes.data, self.workers), "mmf_jpeg_header_batch")
-        st.index = np.flatnonzero(hrc == 0).tolist()
+        ok = hrc == 0
+        # images past mmf_resize_pil's tap budget (shortest side above ~5264 px) are decoded and
+        # resampled by Pillow on the host (api._resize), like every other declined file
+        for i in np.flatnonzero(ok):
+            if not lib.mmf_resize_supported(int(allinf[i, 0]), int(allinf[i, 1])):
+                ok[i] = False
+        st.index = np.flatnonzero(ok).tolist()
         n = len(st.index)
         if n == 0:
             return st

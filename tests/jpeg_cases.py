@@ -98,5 +98,51 @@ def unsupported_files():
     return out
 
 
+def _segments(d: bytes):
+    """(marker, start, end) of each marker segment before the first SOS's entropy data."""
+    out, p = [], 2
+    while p + 4 <= len(d):
+        m = d[p + 1]
+        L = (d[p + 2] << 8) | d[p + 3]
+        out.append((m, p, p + 2 + L))
+        if m == 0xDA:
+            break
+        p += 2 + L
+    return out
+
+
+def rgb_component_ids() -> bytes:
+    """A 3-component file with no JFIF / Adobe marker whose component ids are 'R' 'G' 'B':
+    libjpeg (default_decompress_parms) decodes it as RGB, without the YCbCr transform."""
+    d = bytearray(encode(photo_like(40, 32, seed=9), quality=90, subsampling=0))
+    segs = _segments(bytes(d))
+    for m, a, b in segs:
+        if m in (0xC0, 0xDA):
+            ids = [a + 10 + 3 * i for i in range(3)] if m == 0xC0 else [a + 5 + 2 * i for i in range(3)]
+            for k, i in enumerate(ids):
+                d[i] = (82, 71, 66)[k]
+    app0 = [(a, b) for m, a, b in segs if m == 0xE0]
+    for a, b in reversed(app0):
+        del d[a:b]
+    return bytes(d)
+
+
+def duplicate_sos_ids() -> bytes:
+    """SOF ids 1, 2, 3 but SOS ids 1, 1, 1 (libjpeg: JERR_BAD_COMPONENT_ID)."""
+    d = bytearray(encode(photo_like(32, 24, seed=4), quality=90))
+    for m, a, b in _segments(bytes(d)):
+        if m == 0xDA:
+            for i in range(3):
+                d[a + 5 + 2 * i] = 1
+    return bytes(d)
+
+
+def short_sos_at_eof() -> bytes:
+    """A file ending in an SOS segment whose length field claims only the length itself (L = 2)."""
+    d = encode(photo_like(16, 16, seed=2), quality=90)
+    sos = [a for m, a, b in _segments(d) if m == 0xDA][0]
+    return d[:sos] + b"\xff\xda\x00\x02"
+
+
 def pillow_rgb(data: bytes) -> np.ndarray:
     return np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))

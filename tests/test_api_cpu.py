@@ -169,3 +169,17 @@ def test_fingerprint_sees_dtype_round_trip():
     with torch.no_grad():
         det.ai_head[0].bias.add_(1.0)  # in place: version counter
     assert det.stale_components() == ["text", "fusion"]
+
+
+def test_clip_eos_token_id_from_config(tmp_path, monkeypatch):
+    """The EOS id the CLIP text tower pools at comes from text_config.eos_token_id of the CLIP
+    config in clip_model_dir; env override first, 49407 without a config."""
+    from transformers import CLIPConfig
+    from mmf_amd.api import clip_eos_token_id
+    monkeypatch.delenv("MMF_CLIP_EOS_TOKEN_ID", raising=False)
+    CLIPConfig(text_config={"eos_token_id": 2}).save_pretrained(tmp_path)
+    assert clip_eos_token_id(str(tmp_path)) == 2
+    assert clip_eos_token_id(str(tmp_path / "missing")) == 49407
+    assert clip_eos_token_id(None) == 49407
+    monkeypatch.setenv("MMF_CLIP_EOS_TOKEN_ID", "123")
+    assert clip_eos_token_id(str(tmp_path)) == 123

@@ -71,6 +71,18 @@ def test_declined_files_are_left_to_pillow(engine, stager):
     np.testing.assert_array_equal(b, a)
 
 
+def test_oversized_jpeg_left_to_the_host_path(engine, stager):
+    """a JPEG whose shortest side is past mmf_resize_pil's tap budget is not staged for the
+    device (its windows would fail the whole chunk); the smaller file beside it is."""
+    big = C.encode(C.photo_like(5400, 5300, seed=1), quality=60)
+    info = np.zeros(16, np.int32)
+    assert engine.lib.mmf_jpeg_header(big, len(big), info.ctypes.data) == 0
+    assert not engine.resize_supported(5400, 5300)
+    good = C.supported_jpegs()[0][1]
+    st = stager.stage([big, good])
+    assert st.index == [1]
+
+
 def test_windows_match_pillow_resampling(engine, stager):
     """Device decode -> device resampling == Pillow decode -> Pillow resampling (io_utils)."""
     from PIL import Image
@@ -138,3 +150,24 @@ def test_analyze_pairs_on_encoded_files(forensics, golden_inputs, tmp_path):
         forensics.device_jpeg = True
     assert len(dev) == 10
     assert dev == host
+
+
+def test_analyze_pairs_oversized_and_truncated_jpegs(forensics, golden_inputs):
+    """An oversized JPEG (shortest side 5300 px > the device resampler's budget) goes through Pillow
+    decode + host resampling inside the same chunk, with dicts equal to the all-Pillow call; a
+    truncated JPEG raises Pillow's OSError, as the reference's Image.open(...).convert does."""
+    imgs = golden_inputs["imgs"]
+    big = C.encode(C.photo_like(5400, 5300, seed=1), quality=60)
+    items = [C.encode(imgs[0], quality=90), big, C.encode(imgs[1], quality=85)]
+    texts = ["sample text 0", "sample text 1", "sample text 1"]
+    forensics.device_jpeg = True
+    dev = forensics.analyze_pairs(texts, items)
+    forensics.device_jpeg = False
+    try:
+        host = forensics.analyze_pairs(texts, items)
+    finally:
+        forensics.device_jpeg = True
+    assert dev == host
+    cut = items[0][:len(items[0]) * 2 // 3]
+    with pytest.raises(OSError, match="truncated"):
+        forensics.analyze_pairs(texts[:2], [items[2], cut])

@@ -177,14 +177,20 @@ def test_unsupported_files_are_declined(name, data):
 
 
 def test_truncated_and_corrupt_streams_do_not_crash():
-    """Truncated scans decode with zeros past the end (as libjpeg: a warning, not an error); a
-    damaged header is rejected."""
+    """A file whose data ends before its EOI marker is declined (Pillow then raises "image file is
+    truncated", as the reference's Image.open(...).convert does); a scan cut short but followed by an
+    EOI decodes with zeros past the cut (libjpeg: a warning, not an error); a damaged header is
+    rejected."""
     L = lib()
     d = CASES[1][1]
     info = np.zeros(16, np.int32)
     assert L.mmf_jpeg_header(d[:40], 40, info.ctypes.data) != 0
     t = d[:len(d) * 2 // 3]
-    rc, info, co, _ = c_decode(L, t)
+    for cut in (t, d[:-2], d[:-1]):
+        assert L.mmf_jpeg_header(cut, len(cut), info.ctypes.data) == -95
+        with pytest.raises(OSError, match="truncated"):
+            C.pillow_rgb(cut)
+    rc, info, co, _ = c_decode(L, t + b"\xff\xd9")
     assert rc == 0 and co is not None
     rng = np.random.default_rng(3)
     for _ in range(20):
@@ -265,7 +271,7 @@ def test_packed_staging_of_truncated_and_corrupt_streams(which):
     blocks = int(info[11])
     bound = int(L.mmf_jpeg_packed_bound(blocks))
     rng = np.random.default_rng(7)
-    variants = [d[:len(d) * 2 // 3], d[:len(d) // 3]]
+    variants = [d[:len(d) * 2 // 3] + b"\xff\xd9", d[:len(d) // 3] + b"\xff\xd9"]
     for _ in range(30):
         bad = bytearray(d)
         for _ in range(3):
@@ -289,3 +295,34 @@ def test_packed_staging_of_truncated_and_corrupt_streams(which):
         for o in boff[::37]:  # each record's mask counts values that fit before the next offset bound
             n = bin(int(dst[o:o + 8].view(np.uint64)[0])).count("1")
             assert o + 8 + 2 * n <= used
+
+
+def test_malformed_scan_headers_are_rejected():
+    """repeated SOS component ids (their Huffman table slots would stay unset) and an SOS
+    segment shorter than its component list are EINVAL, with no read past the buffer."""
+    L = lib()
+    info = np.zeros(16, np.int32)
+    d = C.duplicate_sos_ids()
+    assert L.mmf_jpeg_header(d, len(d), info.ctypes.data) == -22
+    d = C.short_sos_at_eof()
+    buf = ctypes.create_string_buffer(d, len(d))  # exact-size copy
+    assert L.mmf_jpeg_header(buf, len(d), info.ctypes.data) == -22
+
+
+def test_rgb_component_ids_go_to_pillow():
+    """No JFIF / Adobe marker and ids 'R' 'G' 'B': libjpeg decodes without the YCbCr transform, so the
+    device path (which always converts) declines the file and Pillow decodes it."""
+    L = lib()
+    d = C.rgb_component_ids()
+    info = np.zeros(16, np.int32)
+    assert L.mmf_jpeg_header(d, len(d), info.ctypes.data) == -95
+    px = C.pillow_rgb(d)
+    assert px.shape == (32, 40, 3)
+    # the same bytes with ids 1 2 3 are YCbCr to libjpeg: different pixels, so the distinction matters
+    e = bytearray(d)
+    for m, a, b in C._segments(d):
+        if m in (0xC0, 0xDA):
+            for k in range(3):
+                e[a + (10 + 3 * k if m == 0xC0 else 5 + 2 * k)] = k + 1
+    assert L.mmf_jpeg_header(bytes(e), len(e), info.ctypes.data) == 0
+    assert not np.array_equal(C.pillow_rgb(bytes(e)), px)

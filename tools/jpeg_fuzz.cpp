@@ -7,6 +7,7 @@
 //   /tmp/jpeg_fuzz a.jpg b.jpg ...   (e.g. tests/jpeg_cases.py files, sequential and progressive)
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include <cstdint>
 #include <random>
@@ -20,18 +21,30 @@ int main(int argc, char** argv) {
       std::vector<uint8_t> v = d;
       int nf = 1 + rng() % 6;
       for (int q = 0; q < nf; ++q) v[rng() % n] ^= (uint8_t)(1 + rng() % 255);
-      if (it % 5 == 0) v.resize(rng() % n + 1);
+      if (it % 5 == 0) {  // truncation; half of them with an EOI appended so the header accepts them
+        const size_t m = rng() % n + 1;
+        std::vector<uint8_t> t(v.begin(), v.begin() + m);
+        if (it % 10 == 0) { t.push_back(0xFF); t.push_back(0xD9); }
+        v.swap(t);
+      }
+      // an exact-size heap copy: ASan sees any read past the caller's buffer (a vector keeps its
+      // old capacity after a shrink, which hid such reads)
+      uint8_t* buf = (uint8_t*)malloc(v.size());
+      memcpy(buf, v.data(), v.size());
+      v.assign(buf, buf + v.size());
       int32_t info[16];
-      if (mmf_jpeg_header(v.data(), v.size(), info)) continue;
+      const int hrc = mmf_jpeg_header(buf, v.size(), info);
+      if (hrc) { free(buf); continue; }
       ++runs;
       std::vector<int16_t> co((size_t)info[11] * 64); uint16_t qt[192];
-      mmf_jpeg_entropy(v.data(), v.size(), co.data(), qt);
+      mmf_jpeg_entropy(buf, v.size(), co.data(), qt);
       int64_t bound = mmf_jpeg_packed_bound(info[11]);
       std::vector<uint8_t> out(bound); std::vector<uint32_t> boff(info[11]); int64_t used = 0;
-      if (mmf_jpeg_entropy_packed(v.data(), v.size(), out.data(), bound, boff.data(), qt, &used) == 0) {
+      if (mmf_jpeg_entropy_packed(buf, v.size(), out.data(), bound, boff.data(), qt, &used) == 0) {
         ++ok;
         for (int b = 0; b < info[11]; ++b) if (boff[b] >= used || boff[b] % 8) { printf("bad offset\n"); return 1; }
       }
+      free(buf);
     }
   }
   printf("runs %ld packed ok %ld\n", runs, ok);
