@@ -954,7 +954,11 @@ static int glds_pick(const GemmArgs& a, bool with_128) {
 }
 
 int gemm_config(const GemmArgs& a) {
-  if (a.epi == 2) return 10;  // producers: 96-column partials (P = ceil(N / 96) <= kLnPMax)
+  // producers: 96-column partials (P = ceil(N / 96) <= kLnPMax); option ln_prod256: 256x256 tiles
+  // (64-column partials) where N is whole 256-column panels and N / 64 <= kLnPMax -- the CLIP text
+  // tower's N = 512, whose third 192-column tile is one-third empty.  Decided from N only, so a
+  // row's statistics (and so its result) do not depend on the batch it runs in.
+  if (a.epi == 2) return (a.prod256 && a.N % 256 == 0 && a.N / 64 <= kLnPMax) ? 11 : 10;
   const int f = forced_config(a);
   if (a.epi == 1) return (f == 10 || f == 11) ? f : glds_pick(a, false);
   if (f >= 0) return f;

@@ -25,6 +25,8 @@ struct GemmArgs {
   int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
   int ring;                      // 1 = plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
   int wide;                      // 1 = 256x384 tiles may be picked (gemm.hip glds_pick)
+  int prod256;                   // 1 = lazy-LN producers (epi 2) on 256x256 tiles where N's 64-column
+                                 //     partials fit (N % 256 == 0, N / 64 <= kLnPMax: CLIP text, N = 512)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials

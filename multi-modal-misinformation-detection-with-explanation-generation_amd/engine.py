@@ -41,6 +41,9 @@ class Engine:
         self.finalize()
         self.reserve(max_batch, max_text_len, max_clip_len)
         self.vault_n = 0
+        self.clip_stream_check = None
+        if clip_state is not None:
+            self.check_clip_streams()
 
     # ------------------------------------------------------------------ weights
     def load_state(self, state: Dict, prefix: str = "") -> None:
@@ -61,6 +64,42 @@ class Engine:
     @property
     def ready(self) -> int:
         return self.lib.mmf_ready(self.h)
+
+    # fp16 CLIP streams: largest tolerated L2 distance between an embedding computed with fp16 and
+    # with fp32 residual streams (unit vectors: |d cos| <= |da| + |db| stays under 1e-3 / 2)
+    CLIP_STREAM_TOL = 2.5e-4
+
+    def check_clip_streams(self, n: int = 8) -> dict:
+        """Load-time guard of the fp16 CLIP residual streams (option clip_res16).
+
+        The pre-LN stream is a running sum, so unlike RoBERTa's post-LN stream no LayerNorm
+        parameter bounds it: trained weights with outlier features can push it past fp16's range
+        (65504) or far enough up that its rounding matters.  A calibration forward measures it: both
+        CLIP towers on n seeded images / captions with fp16 streams and again with fp32 streams; if
+        either embedding is non-finite or moves by more than CLIP_STREAM_TOL (L2) the fp32 streams
+        stay selected.  Returns (and keeps as `clip_stream_check`) the measured distances."""
+        from . import synthetic as syn
+        if self.get_option("clip_res16") != 1:
+            return self.clip_stream_check or {}
+        n = max(1, min(n, self.max_batch))
+        imgs = torch.from_numpy(syn.images(n, 4099)).to(self.device)
+        ids, mask = syn.clip_ids(n, min(77, self.max_clip_len), 4099)
+
+        def embed():
+            e = self.clip_image(imgs)
+            t = self.clip_text(ids, mask)
+            return e.double(), t.double()
+        e16, t16 = embed()
+        self.set_option("clip_res16", 0)
+        e32, t32 = embed()
+        finite = bool(torch.isfinite(e16).all() and torch.isfinite(t16).all())
+        de = float((e16 - e32).norm(dim=1).max()) if finite else float("inf")
+        dt = float((t16 - t32).norm(dim=1).max()) if finite else float("inf")
+        ok = finite and max(de, dt) <= self.CLIP_STREAM_TOL
+        if ok:
+            self.set_option("clip_res16", 1)
+        self.clip_stream_check = {"image_l2": de, "text_l2": dt, "fp16_streams": ok, "rows": n}
+        return self.clip_stream_check
 
     # ------------------------------------------------------------------ options / accounting
     def set_option(self, name: str, value: int) -> None:

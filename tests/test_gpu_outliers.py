@@ -84,7 +84,7 @@ def test_outlier_streams_full_size_vs_oracle():
     Bf = 256
     eng = Engine(0, det, clip, max_batch=Bf)
     # default options: CLIP streams fp16; RoBERTa's layout chosen at load time from the LayerNorm
-    # parameters (|beta| + 4 |gamma| = 900+ here -> the split hi + lo stream)
+    # parameters (|beta| + sqrt(767) |gamma| = 900+ here -> the split hi + lo stream)
     assert eng.get_option("text_hilo") == -1 and eng.get_option("clip_res16") == 1
     assert eng.get_option("text_hilo_effective") == 1
     rid, rm = syn.roberta_ids(Bf, 128, 1234)
@@ -130,4 +130,134 @@ def test_plain_draw_keeps_the_fp16_stream(det_sd, clip_sd):
     from mmf_amd.engine import Engine
     eng = Engine(0, det_sd, clip_sd, max_batch=8)
     assert eng.get_option("text_hilo_effective") == 0
+    eng.close()
+
+
+DOM_CH = 301  # the dominating RoBERTa channel of the gamma draw
+
+
+def dominating_gamma_state(det, gamma_out=3.5, kappa=3.5, emb_scale=30.0, seed_level=60.0):
+    """VERDICT r3 item 2's draw: beta ~ 0 in every LayerNorm and a large gamma (`gamma_out`) in ONE
+    channel that dominates the LayerNorm statistics -- the case the round-3 bound (|beta| + 4 |gamma|)
+    missed.  The word embeddings carry a constant `seed_level` in the channel (normal channels scaled
+    to std 0.6), so the embedding LayerNorm's xhat there is near its sqrt(767) ceiling, and every
+    later LayerNorm sees the channel dominating again: the post-LN stream settles at ~82 (gamma 3.5)
+    / ~151 (gamma 7) in that channel in every layer (tools-free check: the test reads it from the
+    oracle).  As in trained models the normal channels' gamma carries the compensating scale (`kappa`,
+    here equal to gamma_out, which keeps them alive: rows differ by O(1)) and the weight columns
+    reading the channel are x0.01.  max |beta| + 4 |gamma| stays at 17 / 33, under the 64 threshold:
+    the round-3 guard picked the fp16-only stream for it."""
+    det = {k: np.array(v, copy=True) for k, v in det.items()}
+    c = DOM_CH
+    nm = np.ones(768, bool)
+    nm[c] = False
+    det["roberta.embeddings.word_embeddings.weight"][:, nm] *= emb_scale
+    det["roberta.embeddings.word_embeddings.weight"][:, c] += seed_level
+    for ln in ["roberta.embeddings.LayerNorm"] + [f"roberta.encoder.layer.{i}.{n}" for i in range(12)
+                                                  for n in ("attention.output.LayerNorm", "output.LayerNorm")]:
+        det[ln + ".weight"][nm] *= kappa
+        det[ln + ".weight"][c] = gamma_out
+        det[ln + ".bias"][:] = np.clip(det[ln + ".bias"], -0.02, 0.02)  # beta ~ 0
+    for i in range(12):
+        p = f"roberta.encoder.layer.{i}."
+        for w in ("attention.self.query", "attention.self.key", "attention.self.value", "intermediate.dense"):
+            det[p + w + ".weight"][:, c] *= 0.01
+    for h in ("ai_head", "misinfo_head"):
+        det[f"{h}.0.weight"][:, c] *= 0.01
+    return det
+
+
+def _ln_bound(det, xhat):
+    return max(float((np.abs(det[k[:-6] + "bias"]) + xhat * np.abs(v)).max())
+               for k, v in det.items() if k.startswith("roberta") and k.endswith("LayerNorm.weight"))
+
+
+@pytest.mark.parametrize("gamma_out", [3.5, 7.0])
+def test_dominating_gamma_channel_selects_split_stream(det_sd, clip_sd, gamma_out):
+    """The sound bound |beta| + sqrt(767) |gamma| selects the split hi + lo stream on a draw whose
+    post-LN stream is ~82 / ~151 in one dominating channel with beta ~ 0 (the round-3 bound, 17 / 33,
+    did not), and the full-size scores and probabilities stay within 1e-3 of the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    from oracle import models as M
+    from oracle.pipeline import batched_scores
+    det = dominating_gamma_state(det_sd, gamma_out, kappa=gamma_out)
+    assert _ln_bound(det, 4.0) < 64.0 < _ln_bound(det, np.sqrt(767.0))
+    Bf = 256
+    eng = Engine(0, det, clip_sd, max_batch=Bf)
+    assert eng.get_option("text_hilo_effective") == 1
+    rid, rm = syn.roberta_ids(Bf, 128, 1234)
+    cid, cm = syn.clip_ids(Bf, 77, 1234)
+    imgs = syn.images(Bf, 1234)
+    vault = syn.vault(2170, 512, 77)
+    eng.set_vault(vault)
+    out = eng.analyze_batch(rid, rm, cid, cm, imgs)
+    torch.cuda.synchronize()
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    with torch.no_grad():
+        ref = batched_scores(det, clip_sd, rid, rm, cid, cm, imgs, vault)
+        sd = M.to_torch(det)
+        cls = M.roberta_forward(sd, torch.as_tensor(rid[:4]).long(), torch.as_tensor(rm[:4]).long())[:, 0]
+    lvl = float(cls[:, DOM_CH].abs().min())
+    rest = cls[:, [c for c in range(768) if c != DOM_CH]]
+    print(f"dominating channel draw (gamma {gamma_out}): stream level {lvl:.1f}, rest std {float(rest.std()):.2f}")
+    assert 70.0 < lvl < 200.0 and lvl > 4.0 * gamma_out * 4  # the draw does what it claims
+    assert float(rest.std()) > 0.3 and float((cls[0] - cls[1]).abs().max()) > 0.1
+    d = np.abs(got["scores"] - ref["scores"]).max(0)
+    eng.set_option("text_hilo", 0)
+    o16 = eng.analyze_batch(rid, rm, cid, cm, imgs)["scores"].cpu().numpy()
+    eng.set_option("text_hilo", -1)
+    print(f"  split stream: ai {d[0]:.2e} misinfo {d[1]:.2e}; fp16-only stream: ai "
+          f"{np.abs(o16[:, 0] - ref['scores'][:, 0]).max():.2e} misinfo {np.abs(o16[:, 1] - ref['scores'][:, 1]).max():.2e}")
+    np.testing.assert_allclose(got["scores"], ref["scores"], atol=1e-3)
+    np.testing.assert_allclose(got["probs"], ref["probs"], atol=1e-3)
+    eng.close()
+
+
+def test_clip_stream_overflow_selects_fp32_streams(det_sd, clip_sd):
+    """CLIP's pre-LN streams have no parameter bound, so the engine measures them at load
+    (Engine.check_clip_streams).  A draw whose text-tower stream passes fp16's range (FFN-2 biases
+    of +7000 per layer in 2 channels: ~8e4 by the last layer) must fall back to fp32 streams and
+    match the oracle; the plain draw keeps the fp16 streams."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    from oracle.pipeline import batched_scores
+    plain = Engine(0, det_sd, clip_sd, max_batch=8)
+    chk = plain.clip_stream_check
+    print(f"plain draw: {chk}")
+    assert chk["fp16_streams"] and plain.get_option("clip_res16") == 1
+    plain.close()
+    clip = {k: np.array(v, copy=True) for k, v in clip_sd.items()}
+    c, H, step = list(TXT_CH), 512, 7000.0
+    nm = np.ones(H, bool)
+    nm[c] = False
+    for i in range(12):
+        p = f"text_model.encoder.layers.{i}."
+        clip[p + "mlp.fc2.bias"][c] += step
+        g = max(1.0, step * i * np.sqrt(len(c) / H))
+        for ln in ("layer_norm1", "layer_norm2"):
+            clip[p + ln + ".weight"][nm] *= g
+            clip[p + ln + ".weight"][c] = 0.05
+    clip["text_model.final_layer_norm.weight"][nm] *= step * 12 * np.sqrt(len(c) / H)
+    clip["text_model.final_layer_norm.weight"][c] = 0.05
+    Bf = 64
+    eng = Engine(0, det_sd, clip, max_batch=Bf)
+    chk = eng.clip_stream_check
+    print(f"overflow draw: {chk}")
+    assert not chk["fp16_streams"] and eng.get_option("clip_res16") == 0
+    rid, rm = syn.roberta_ids(Bf, 128, 77)
+    cid, cm = syn.clip_ids(Bf, 77, 77)
+    imgs = syn.images(Bf, 77)
+    vault = syn.vault(2170, 512, 77)
+    eng.set_vault(vault)
+    got = {k: v.cpu().numpy() for k, v in eng.analyze_batch(rid, rm, cid, cm, imgs).items()}
+    with torch.no_grad():
+        ref = batched_scores(det_sd, clip, rid, rm, cid, cm, imgs, vault)
+    assert np.isfinite(got["scores"]).all()
+    np.testing.assert_allclose(got["scores"], ref["scores"], atol=1e-3)
+    np.testing.assert_allclose(got["probs"], ref["probs"], atol=1e-3)
     eng.close()

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("variants", nargs="+")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--what", choices=("step", "clip", "text"), default="step",
+                    help="step: analyze_batch; clip: mmf_clip_consistency (configs[3]); text: configs[1]")
     a = ap.parse_args()
     import bench
     import mmf_amd.weights as W
@@ -35,8 +37,22 @@ def main():
         for k in names:
             eng.set_option(k, v.get(k, base[k]))
 
-    def step():
-        eng.analyze_batch(t["rid"], t["rm"], t["cid"], t["cm"], t["img"], out=out)
+    if a.what == "clip":
+        out = {"img_emb": torch.empty(B, 512, device=eng.device), "txt_emb": torch.empty(B, 512, device=eng.device),
+               "sim": torch.empty(B, device=eng.device)}
+
+        def step():
+            eng.clip_consistency(t["img"], t["cid"], t["cm"], out=out)
+    elif a.what == "text":
+        from mmf_amd.hip import check, ptr, stream_ptr
+        out = {k: torch.empty(B, 2, device=eng.device) for k in ("ai", "mi", "sc")}
+
+        def step():
+            check(eng.lib.mmf_text_forward(eng.h, ptr(t["rid"]), ptr(t["rm"]), B, 128, ptr(out["ai"]),
+                                           ptr(out["mi"]), ptr(out["sc"]), stream_ptr()))
+    else:
+        def step():
+            eng.analyze_batch(t["rid"], t["rm"], t["cid"], t["cm"], t["img"], out=out)
 
     ref = None
     for v in variants:
@@ -49,7 +65,8 @@ def main():
             ref = o
         else:
             same = all(torch.equal(o[k], ref[k]) for k in o)
-            print(f"{v}: outputs identical to {variants[0]}: {same}", flush=True)
+            dmax = max(float((o[k].double() - ref[k].double()).abs().max()) for k in o)
+            print(f"{v}: outputs identical to {variants[0]}: {same} (max |d| {dmax:.2e})", flush=True)
     times = [[] for _ in variants]
     for _ in range(a.rounds):
         for i, v in enumerate(variants):
