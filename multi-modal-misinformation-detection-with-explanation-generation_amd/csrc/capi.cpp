@@ -138,6 +138,7 @@ struct Options {
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
+  int cu_split = 0;     // > 0: EfficientNet on that many CUs, the encoders on the rest (CU-masked streams; A/B)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -151,6 +152,7 @@ const OptName kOptNames[] = {
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
+    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -233,6 +235,12 @@ struct mmf_handle {
   // fork/join streams of mmf_analyze_batch (text, effnet, clip-text towers beside the caller's)
   hipStream_t tower[3] = {nullptr, nullptr, nullptr};
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
+  // option cu_split = n > 0: CU-masked tower streams -- EfficientNet on n CUs, the three encoders
+  // (text, CLIP text, ViT) on the other CUs (mtower: text, effnet, clip-text, vit)
+  hipStream_t mtower[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t mjoin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int mtower_split = 0, ncu = 0;
+  int grid_cap = 0;  // persistent-GEMM grid cap of the tower being enqueued (0 = all CUs)
   // mmf_resize_pil workspaces (grow-only, group AG_RESIZE)
   struct ResizeWs {
     ResizeJob* jobs = nullptr;
@@ -249,6 +257,10 @@ struct mmf_handle {
     for (int i = 0; i < 3; ++i) {
       if (tower[i]) (void)hipStreamDestroy(tower[i]);
       if (join_ev[i]) (void)hipEventDestroy(join_ev[i]);
+    }
+    for (int i = 0; i < 4; ++i) {
+      if (mtower[i]) (void)hipStreamDestroy(mtower[i]);
+      if (mjoin_ev[i]) (void)hipEventDestroy(mjoin_ev[i]);
     }
     if (fork_ev) (void)hipEventDestroy(fork_ev);
   }
@@ -662,6 +674,7 @@ GemmArgs with_ws(GemmArgs g, float* ws, size_t elems) {
 
 int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   apply_options(h->opt, &g);
+  g.max_grid = h->grid_cap;
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
   ProfScope ps(h, s, (gemm_config(g) * kGemmEpis + g.epi) * kGemmActs + g.act, 2.0 * M * N * K,
@@ -1141,6 +1154,53 @@ int ensure_towers(mmf_handle* h) {
   return 0;
 }
 
+// CU-masked tower streams (option cu_split = n): EfficientNet's stream may run on n CUs, the three
+// encoder streams on the remaining ones, so the latency-bound EfficientNet kernels keep a fixed CU
+// slice for the whole step instead of queueing behind the encoders' persistent GEMMs (which then
+// size their grids to the encoders' CUs).  Mask bit i is CU i; the driver interleaves the bits
+// over the 8 XCDs (bit i -> XCD i % 8), so a run of low bits is an even share of every XCD.
+int ensure_masked_towers(mmf_handle* h, int n) {
+  if (h->mtower_split == n && h->mtower[0]) return 0;
+  if (!h->ncu) HIPCHK(hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+  if (n <= 0 || n >= h->ncu) return fail(MMF_EINVAL, "cu_split %d outside 1..%d", n, h->ncu - 1);
+  for (int i = 0; i < 4; ++i) {
+    if (h->mtower[i]) HIPCHK(hipStreamDestroy(h->mtower[i]));
+    h->mtower[i] = nullptr;
+    if (!h->mjoin_ev[i]) HIPCHK(hipEventCreateWithFlags(&h->mjoin_ev[i], hipEventDisableTiming));
+  }
+  if (!h->fork_ev) HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+  const int words = (h->ncu + 31) / 32;
+  std::vector<uint32_t> eff(words, 0u), enc(words, 0u);
+  for (int c = 0; c < h->ncu; ++c) (c < n ? eff : enc)[c >> 5] |= 1u << (c & 31);
+  for (int i = 0; i < 4; ++i)
+    HIPCHK(hipExtStreamCreateWithCUMask(&h->mtower[i], (uint32_t)h->ncu, i == 1 ? eff.data() : enc.data()));
+  h->mtower_split = n;
+  return 0;
+}
+
+// after the towers joined: CLIP cosine, vault top-5, fusion (mmf_analyze_batch's last part)
+int analyze_tail(mmf_handle* h, int B, float* scores5, float* text_sim, float* probs2, int32_t* verdict, float* conf,
+                 int32_t* rule, float* top_sims, int32_t* top_idx, hipStream_t s) {
+  Workspace& w = h->ws;
+  HIPCHK(launch_rowdot(w.v_emb, w.t_emb, scores5 + 3, 5, B, 512, s));
+  if (h->ready & 32) {
+    ProfScope ps(h, s, PK_VAULT, 2.0 * B * h->vault_n * 512, (double)h->vault_n * 512 * 4 + (double)B * h->vault_n * 8);
+    HIPCHK(launch_vault_sims(w.v_emb, h->vault, w.s_sims, B, h->vault_n, 512, s));
+    HIPCHK(launch_vault_topk(w.s_sims, B, h->vault_n, 5, 0.85f, top_sims, top_idx, scores5 + 4, 5, w.t_emb,
+                             h->vault_title, 512, text_sim, s));
+  } else {
+    HIPCHK(launch_fill_strided(scores5 + 4, 5, B, 0.f, s));
+    if (text_sim) HIPCHK(hipMemsetAsync(text_sim, 0, (size_t)B * 4, s));
+    if (top_sims) HIPCHK(hipMemsetAsync(top_sims, 0, (size_t)B * 5 * 4, s));
+    if (top_idx) HIPCHK(hipMemsetAsync(top_idx, 0xff, (size_t)B * 5 * 4, s));
+  }
+  ProfScope ps(h, s, PK_FUSION, 2.0 * B * (5 * 64 + 64 * 32 + 32 * 2), (double)B * (5 + 2 + 3) * 4);
+  HIPCHK(launch_fusion(scores5, h->f_w0, h->f_b0, h->f_w3, h->f_b3, h->f_w5, h->f_b5, probs2, verdict, conf, rule, B,
+                       s));
+  return 0;
+}
+
+
 int ensure_sims(mmf_handle* h) {
   if (!h->vault_n || !h->cap_b) return 0;
   if (h->ws.s_cap_n >= h->vault_n) return 0;
@@ -1486,6 +1546,26 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   Workspace& w = h->ws;
   // the per-kernel profiling pass runs the towers sequentially so event intervals are clean
   const int concurrent = h->opt.concurrent && !h->prof;
+  if (concurrent && h->opt.cu_split > 0) {
+    // CU-split fork: four masked streams; the caller's stream only forks and joins
+    CHK(ensure_masked_towers(h, h->opt.cu_split));
+    HIPCHK(hipEventRecord(h->fork_ev, s));
+    for (int i = 0; i < 4; ++i) HIPCHK(hipStreamWaitEvent(h->mtower[i], h->fork_ev, 0));
+    const int enc = h->ncu - h->opt.cu_split;
+    h->grid_cap = enc;
+    int rc = run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, h->mtower[0]);
+    if (!rc) rc = run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, h->mtower[2]);
+    if (!rc) rc = run_clip_image(h, img_clip, B, w.v_emb, h->mtower[3]);
+    h->grid_cap = h->opt.cu_split;
+    if (!rc) rc = run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, h->mtower[1]);
+    h->grid_cap = 0;
+    CHK(rc);
+    for (int i = 0; i < 4; ++i) {
+      HIPCHK(hipEventRecord(h->mjoin_ev[i], h->mtower[i]));
+      HIPCHK(hipStreamWaitEvent(s, h->mjoin_ev[i], 0));
+    }
+    return analyze_tail(h, B, scores5, text_sim, probs2, verdict, conf, rule, top_sims, top_idx, s);
+  }
   if (concurrent) CHK(ensure_towers(h));
   // fork: the four towers only share read-only inputs and write disjoint workspaces/outputs
   hipStream_t st_text = s, st_eff = s, st_ctxt = s;
@@ -1506,22 +1586,7 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
       HIPCHK(hipStreamWaitEvent(s, h->join_ev[i], 0));
     }
   }
-  HIPCHK(launch_rowdot(w.v_emb, w.t_emb, scores5 + 3, 5, B, 512, s));
-  if (h->ready & 32) {
-    ProfScope ps(h, s, PK_VAULT, 2.0 * B * h->vault_n * 512, (double)h->vault_n * 512 * 4 + (double)B * h->vault_n * 8);
-    HIPCHK(launch_vault_sims(w.v_emb, h->vault, w.s_sims, B, h->vault_n, 512, s));
-    HIPCHK(launch_vault_topk(w.s_sims, B, h->vault_n, 5, 0.85f, top_sims, top_idx, scores5 + 4, 5, w.t_emb,
-                             h->vault_title, 512, text_sim, s));
-  } else {
-    HIPCHK(launch_fill_strided(scores5 + 4, 5, B, 0.f, s));
-    if (text_sim) HIPCHK(hipMemsetAsync(text_sim, 0, (size_t)B * 4, s));
-    if (top_sims) HIPCHK(hipMemsetAsync(top_sims, 0, (size_t)B * 5 * 4, s));
-    if (top_idx) HIPCHK(hipMemsetAsync(top_idx, 0xff, (size_t)B * 5 * 4, s));
-  }
-  ProfScope ps(h, s, PK_FUSION, 2.0 * B * (5 * 64 + 64 * 32 + 32 * 2), (double)B * (5 + 2 + 3) * 4);
-  HIPCHK(launch_fusion(scores5, h->f_w0, h->f_b0, h->f_w3, h->f_b3, h->f_w5, h->f_b5, probs2, verdict, conf, rule, B,
-                       s));
-  return 0;
+  return analyze_tail(h, B, scores5, text_sim, probs2, verdict, conf, rule, top_sims, top_idx, s);
 }
 
 int mmf_profile_begin(mmf_handle* h) {

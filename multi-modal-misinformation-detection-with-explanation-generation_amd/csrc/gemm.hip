@@ -766,7 +766,8 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
   const int per_cu = (BM == 128) ? 2 : 1;  // co-resident workgroups per CU (LDS / VGPR budget)
-  const int grid = tiles < 256 * per_cu ? tiles : 256 * per_cu;
+  const int cap = (a.max_grid > 0 && a.max_grid < 256 ? a.max_grid : 256) * per_cu;
+  const int grid = tiles < cap ? tiles : cap;
   const dim3 blk(64 * WGM * WGN);
   const int gm = a.group_m;  // tile-order option (handle option "gemm_group_m"; 0 = row-major)
 #define MMF_GLDS_CASE(ACT)                                                                                  \
@@ -797,7 +798,8 @@ template <int BM, int BN, int WGM, int WGN>
 hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
-  const int grid = tiles < 256 ? tiles : 256;
+  const int cap = a.max_grid > 0 && a.max_grid < 256 ? a.max_grid : 256;
+  const int grid = tiles < cap ? tiles : cap;
   const dim3 blk(64 * WGM * WGN);
   const int gm = a.group_m;
 #define MMF_EPI_CASE(EPI, ACT)                                                                                 \

@@ -25,6 +25,8 @@ struct GemmArgs {
   int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
   int ring;                      // 1 = plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
   int wide;                      // 1 = 256x384 tiles may be picked (gemm.hip glds_pick)
+  int max_grid;                  // > 0: persistent GEMM grids capped at this many workgroups (the CUs of a
+                                 //     CU-masked tower stream, option cu_split); 0 = 256
   int prod256;                   // 1 = lazy-LN producers (epi 2) on 256x256 tiles where N's 64-column
                                  //     partials fit (N % 256 == 0, N / 64 <= kLnPMax: CLIP text, N = 512)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null

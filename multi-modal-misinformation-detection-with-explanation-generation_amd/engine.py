@@ -65,8 +65,9 @@ class Engine:
     def ready(self) -> int:
         return self.lib.mmf_ready(self.h)
 
-    # fp16 CLIP streams: largest tolerated L2 distance between an embedding computed with fp16 and
-    # with fp32 residual streams (unit vectors: |d cos| <= |da| + |db| stays under 1e-3 / 2)
+    # fp16 CLIP streams: largest tolerated change of an image-text cosine (the quantity clip_similarity
+    # and the vault scores are made of) between fp16 and fp32 residual streams -- a quarter of the
+    # north-star 1e-3
     CLIP_STREAM_TOL = 2.5e-4
 
     def check_clip_streams(self, n: int = 8) -> dict:
@@ -76,8 +77,9 @@ class Engine:
         parameter bounds it: trained weights with outlier features can push it past fp16's range
         (65504) or far enough up that its rounding matters.  A calibration forward measures it: both
         CLIP towers on n seeded images / captions with fp16 streams and again with fp32 streams; if
-        either embedding is non-finite or moves by more than CLIP_STREAM_TOL (L2) the fp32 streams
-        stay selected.  Returns (and keeps as `clip_stream_check`) the measured distances."""
+        an embedding is non-finite or any of the n x n image-text cosines moves by more than
+        CLIP_STREAM_TOL, the fp32 streams stay selected.  Returns (and keeps as `clip_stream_check`)
+        the measured change."""
         from . import synthetic as syn
         if self.get_option("clip_res16") != 1:
             return self.clip_stream_check or {}
@@ -85,20 +87,20 @@ class Engine:
         imgs = torch.from_numpy(syn.images(n, 4099)).to(self.device)
         ids, mask = syn.clip_ids(n, min(77, self.max_clip_len), 4099)
 
-        def embed():
-            e = self.clip_image(imgs)
-            t = self.clip_text(ids, mask)
-            return e.double(), t.double()
-        e16, t16 = embed()
+        def cosines():
+            e = self.clip_image(imgs).double()
+            t = self.clip_text(ids, mask).double()
+            return e, t, e @ t.T  # unit rows: cosines
+        e16, t16, c16 = cosines()
         self.set_option("clip_res16", 0)
-        e32, t32 = embed()
+        e32, t32, c32 = cosines()
         finite = bool(torch.isfinite(e16).all() and torch.isfinite(t16).all())
-        de = float((e16 - e32).norm(dim=1).max()) if finite else float("inf")
-        dt = float((t16 - t32).norm(dim=1).max()) if finite else float("inf")
-        ok = finite and max(de, dt) <= self.CLIP_STREAM_TOL
+        dcos = float((c16 - c32).abs().max()) if finite else float("inf")
+        demb = float(max((e16 - e32).abs().max(), (t16 - t32).abs().max())) if finite else float("inf")
+        ok = finite and dcos <= self.CLIP_STREAM_TOL
         if ok:
             self.set_option("clip_res16", 1)
-        self.clip_stream_check = {"image_l2": de, "text_l2": dt, "fp16_streams": ok, "rows": n}
+        self.clip_stream_check = {"max_dcos": dcos, "max_demb": demb, "fp16_streams": ok, "rows": n}
         return self.clip_stream_check
 
     # ------------------------------------------------------------------ options / accounting
