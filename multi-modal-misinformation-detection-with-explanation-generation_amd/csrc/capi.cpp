@@ -139,6 +139,8 @@ struct Options {
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
   int cu_split = 0;     // > 0: EfficientNet on that many CUs, the encoders on the rest (CU-masked streams; A/B)
+  int cu_split_layout = 0;  // which mask bits: 0 = the n lowest, 1 = n / 8 from each 32-bit word (one per XCD
+                            // if the driver maps bit words to XCDs), 2 = bits i with i % 8 < ... (see ensure_masked_towers)
 };
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
@@ -152,7 +154,7 @@ const OptName kOptNames[] = {
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
-    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},
+    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -239,7 +241,7 @@ struct mmf_handle {
   // (text, CLIP text, ViT) on the other CUs (mtower: text, effnet, clip-text, vit)
   hipStream_t mtower[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t mjoin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  int mtower_split = 0, ncu = 0;
+  int mtower_split = 0, mtower_layout = 0, ncu = 0;
   int grid_cap = 0;  // persistent-GEMM grid cap of the tower being enqueued (0 = all CUs)
   // mmf_resize_pil workspaces (grow-only, group AG_RESIZE)
   struct ResizeWs {
@@ -1160,7 +1162,8 @@ int ensure_towers(mmf_handle* h) {
 // size their grids to the encoders' CUs).  Mask bit i is CU i; the driver interleaves the bits
 // over the 8 XCDs (bit i -> XCD i % 8), so a run of low bits is an even share of every XCD.
 int ensure_masked_towers(mmf_handle* h, int n) {
-  if (h->mtower_split == n && h->mtower[0]) return 0;
+  const int layout = h->opt.cu_split_layout;
+  if (h->mtower_split == n && h->mtower_layout == layout && h->mtower[0]) return 0;
   if (!h->ncu) HIPCHK(hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device));
   if (n <= 0 || n >= h->ncu) return fail(MMF_EINVAL, "cu_split %d outside 1..%d", n, h->ncu - 1);
   for (int i = 0; i < 4; ++i) {
@@ -1171,10 +1174,19 @@ int ensure_masked_towers(mmf_handle* h, int n) {
   if (!h->fork_ev) HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
   const int words = (h->ncu + 31) / 32;
   std::vector<uint32_t> eff(words, 0u), enc(words, 0u);
-  for (int c = 0; c < h->ncu; ++c) (c < n ? eff : enc)[c >> 5] |= 1u << (c & 31);
+  // layout 0: bits [0, n); 1: the first n / 32 * ... of every 32-bit word (n / (ncu / 32) per word);
+  // 2: every (ncu / n)-th bit
+  const int words32 = h->ncu / 32;
+  for (int c = 0; c < h->ncu; ++c) {
+    bool e = c < n;
+    if (layout == 1) e = (c & 31) < n / (words32 ? words32 : 1);
+    if (layout == 2) e = (c % (h->ncu / n)) == 0 && c / (h->ncu / n) < n;
+    (e ? eff : enc)[c >> 5] |= 1u << (c & 31);
+  }
   for (int i = 0; i < 4; ++i)
     HIPCHK(hipExtStreamCreateWithCUMask(&h->mtower[i], (uint32_t)h->ncu, i == 1 ? eff.data() : enc.data()));
   h->mtower_split = n;
+  h->mtower_layout = layout;
   return 0;
 }
 

@@ -66,9 +66,9 @@ class Engine:
         return self.lib.mmf_ready(self.h)
 
     # fp16 CLIP streams: largest tolerated change of an image-text cosine (the quantity clip_similarity
-    # and the vault scores are made of) between fp16 and fp32 residual streams -- a quarter of the
-    # north-star 1e-3
-    CLIP_STREAM_TOL = 2.5e-4
+    # and the vault scores are made of) between fp16 and fp32 residual streams -- half of the
+    # north-star 1e-3 (the ordinary synthetic draw measures 2.3e-4, an outlier-feature draw 1.3e-4)
+    CLIP_STREAM_TOL = 5e-4
 
     def check_clip_streams(self, n: int = 8) -> dict:
         """Load-time guard of the fp16 CLIP residual streams (option clip_res16).

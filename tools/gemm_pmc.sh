@@ -25,6 +25,6 @@ run_passes() {  # $1 = sub-dir, rest = command
     timeout -s KILL 150 rocprofv3 --pmc $P -f csv -d $D/p$i -o run -- "$@" > $D/p$i.log 2>&1 || { echo "pass $i failed rc=$?" >> $D/passes.log; return 1; }
   done
 }
-run_passes iso python3 $R/tools/gemm_bench.py --configs auto --iters 10 --shapes rob_qkv,rob_o,rob_fc1,rob_fc2,vit_fc2,sq4096 && \
-run_passes step python3 $R/bench.py --steps 3 --warmup 2 --no-configs --no-per-sample --no-cpu-baseline --no-profile
+[ "${STEP_ONLY:-0}" = 1 ] || run_passes iso python3 $R/tools/gemm_bench.py --configs auto --iters 10 --shapes rob_qkv,rob_o,rob_fc1,rob_fc2,vit_fc2,sq4096 && \
+run_passes step python3 $R/bench.py --steps 3 --warmup 2 --no-configs --no-per-sample --no-cpu-baseline --no-profile --no-e2e
 echo done >> $OUT/passes.log
