@@ -328,6 +328,10 @@ MMF_DEV void tile_coords(int t, int tilesM, int tilesN, int gm, int& tm, int& tn
 // the second K-step and combined into (mean, rstd) per row at the top of the third.
 constexpr int kLnPMax = 8;  // partials per row a reader accepts
 
+#ifndef MMF_GLDS_BUF
+#define MMF_GLDS_BUF 1  // descriptor LDS-DMA fills for full panels (0: 64-bit-address fills everywhere; A/B builds)
+#endif
+
 // DBG (measurement builds, forced configs 15 / 16 only; outputs garbage): 1 = LDS-DMA + barriers only,
 // 2 = fragment reads + MFMAs + barriers only
 template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0>
@@ -381,9 +385,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
   int t = wgid;
   if (t >= tiles) return;
   if ((g.prio == 1 && wave >= NW / 2) || (g.prio == 2 && wave < NW / 2)) __builtin_amdgcn_s_setprio(1);
-  // WIDE: descriptor fills (glds_tile_buf; the launcher checks the 32-bit byte extents)
-  const rsrc_t ra = make_rsrc(g.A, WIDE ? (uint32_t)M * (uint32_t)g.lda * 2u : 0u);
-  const rsrc_t rw = make_rsrc(g.W, WIDE ? (uint32_t)N * (uint32_t)g.ldw * 2u : 0u);
+  // descriptor fills (glds_tile_buf) for every full row / column panel whose operand's byte extent
+  // fits 32 bits (WIDE: checked by the launcher): the per-lane source offset is one loop-invariant
+  // VGPR and the panel base rides in the scalar soffset, so a K-step's DMA issue costs no VALU
+  // (glds_tile: a clamped row and a 64-bit address per piece, ~6 VALU each, every K-step)
+  const bool bufA = WIDE || (MMF_GLDS_BUF && (size_t)M * g.lda * 2 < ((size_t)1 << 32));
+  const bool bufW = WIDE || (MMF_GLDS_BUF && (size_t)N * g.ldw * 2 < ((size_t)1 << 32));
+  const rsrc_t ra = make_rsrc(g.A, bufA ? (uint32_t)((size_t)M * g.lda * 2) : 0u);
+  const rsrc_t rw = make_rsrc(g.W, bufW ? (uint32_t)((size_t)N * g.ldw * 2) : 0u);
   const uint32_t lchunk = (uint32_t)(((lane & 7) ^ (lane >> 3)) * 16);
   const uint32_t aoff = (uint32_t)(lane >> 3) * (uint32_t)g.lda * 2u + lchunk;
   const uint32_t woff = (uint32_t)(lane >> 3) * (uint32_t)g.ldw * 2u + lchunk;
@@ -401,8 +410,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g
       glds_tile_buf<BN, NW>(rw, (uint32_t)g.ldw * 2u, tn_ * BN, kt * BK, woff, nb + BM * BK, wave);
       return;
     }
-    glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
-    glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
+    if (bufA && tm_ * BM + BM <= M) glds_tile_buf<BM, NW>(ra, (uint32_t)g.lda * 2u, tm_ * BM, kt * BK, aoff, nb, wave);
+    else glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
+    if (bufW && tn_ * BN + BN <= N)
+      glds_tile_buf<BN, NW>(rw, (uint32_t)g.ldw * 2u, tn_ * BN, kt * BK, woff, nb + BM * BK, wave);
+    else glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
   };
   // lazy-LN epilogue operands of tile (m0_, n0_) -> LDS (issued in the second K-step: every wave
   // has left the previous tile's epilogue by then; the K-step barriers' vmcnt(0) covers them)
