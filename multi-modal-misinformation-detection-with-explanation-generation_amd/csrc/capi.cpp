@@ -132,7 +132,8 @@ struct Options {
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
   int dw_v2 = 0;        // depthwise phases with one channel group per wave, weights in SGPRs (effnet.hip)
   int gemm_ring = 0;    // plain fp16-output encoder GEMMs on the loader / consumer kernel (gemm_ring.hip)
-  int pw32_mfma = 1;    // fp32 tower's 1x1 convs on the fp32-input MFMA (1) or the fp32-FMA VALU kernel (0)
+  int pw32_mfma = 2;    // fp32 tower's 1x1 convs on the fp32-input MFMA (2: loads 3 K-chunks ahead, 1: one ahead)
+                        // or the fp32-FMA VALU kernel (0) -- every mode bit-identical
   int gemm_wide = 0;    // 256x384 tiles where they save a persistent round (gemm.hip glds_pick; step A/B: a tie)
   int dw_persist = 0;   // persistent depthwise kernels with the next tile's loads in flight (effnet.hip; A/B: slower)
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)

@@ -94,10 +94,17 @@ constexpr int QB = 64, QK = 16;
 // 16-lane ds_read_b128 groups conflict-free (the 64-B-row swizzle of gemm_ring.hip)
 MMF_DEV int q_off(int row, int g) { return row * QK + ((g ^ (((row >> 3) & 1) << 1)) << 2); }
 
+// D = global-load prefetch depth in K chunks: chunk c is requested D - 1 chunks before the one that
+// stores it to LDS (D = 2: during the previous chunk's MFMAs only, the round-3 kernel).  The launches
+// with few workgroups per CU (M = B * 7^2 or 14^2 rows, K = 480 ... 1152) cannot hide a global load
+// behind one 16-deep chunk; D = 4 keeps three chunks of loads in flight (8 more VGPRs per chunk of
+// depth).  The operation sequence, and so every result bit, is the same for every D.
+template <int D>
 __global__ __launch_bounds__(256) void pw32m_kernel(const float* __restrict__ A, const float* __restrict__ Wt,
                                                     const float* __restrict__ bias, const float* __restrict__ ascale,
                                                     int rows_per_image, const float* __restrict__ res,
                                                     float* __restrict__ C, int M, int N, int K, int act) {
+  static_assert(D >= 2, "the stored chunk is at least one chunk ahead");
   __shared__ __attribute__((aligned(16))) float As[2][QB * QK];
   __shared__ __attribute__((aligned(16))) float Ws[2][QB * QK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -133,30 +140,39 @@ __global__ __launch_bounds__(256) void pw32m_kernel(const float* __restrict__ A,
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float4 a, w;
-  gload(0, a, w);
-  lstore(0, a, w);
+  // register slots: chunk c lives in slot c % D from its request until it is stored to LDS
+  float4 ra[D], rw[D];
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) gload(d * QK, ra[d], rw[d]);
+  lstore(0, ra[0], rw[0]);
   __syncthreads();
-  int buf = 0;
-  for (int k0 = 0; k0 < K; k0 += QK) {
-    const bool more = k0 + QK < K;
-    if (more) gload(k0 + QK, a, w);
-    float4 wf[2], xf[2];
+  const int nch = (K + QK - 1) / QK;
+  // chunk c = c0 + d with d compile-time (slot indices static); c0 steps by D
+  for (int c0 = 0; c0 < nch; c0 += D) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) wf[i] = *reinterpret_cast<const float4*>(&Ws[buf][q_off(wn * 32 + i * 16 + fr, fg)]);
+    for (int d = 0; d < D; ++d) {
+      const int c = c0 + d;
+      if (c >= nch) break;
+      const int buf = c & 1;
+      // request chunk c + D - 1 into the slot chunk c - 1 occupied (stored to LDS a chunk ago)
+      if (c + D - 1 < nch) gload((c + D - 1) * QK, ra[(d + D - 1) % D], rw[(d + D - 1) % D]);
+      float4 wf[2], xf[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) xf[j] = *reinterpret_cast<const float4*>(&As[buf][q_off(wm * 32 + j * 16 + fr, fg)]);
-    const float wfs[2][4] = {{wf[0].x, wf[0].y, wf[0].z, wf[0].w}, {wf[1].x, wf[1].y, wf[1].z, wf[1].w}};
-    const float xfs[2][4] = {{xf[0].x, xf[0].y, xf[0].z, xf[0].w}, {xf[1].x, xf[1].y, xf[1].z, xf[1].w}};
+      for (int i = 0; i < 2; ++i) wf[i] = *reinterpret_cast<const float4*>(&Ws[buf][q_off(wn * 32 + i * 16 + fr, fg)]);
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
+      for (int j = 0; j < 2; ++j) xf[j] = *reinterpret_cast<const float4*>(&As[buf][q_off(wm * 32 + j * 16 + fr, fg)]);
+      const float wfs[2][4] = {{wf[0].x, wf[0].y, wf[0].z, wf[0].w}, {wf[1].x, wf[1].y, wf[1].z, wf[1].w}};
+      const float xfs[2][4] = {{xf[0].x, xf[0].y, xf[0].z, xf[0].w}, {xf[1].x, xf[1].y, xf[1].z, xf[1].w}};
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int st = 0; st < 4; ++st)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wfs[i][st], xfs[j][st], acc[i][j], 0, 0, 0);
-    if (more) lstore(buf ^ 1, a, w);
-    __syncthreads();
-    buf ^= 1;
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wfs[i][st], xfs[j][st], acc[i][j], 0, 0, 0);
+      if (c + 1 < nch) lstore(buf ^ 1, ra[(d + 1) % D], rw[(d + 1) % D]);
+      __syncthreads();
+    }
   }
   // lane: C[m][n .. n + 3] of each 16 x 16 block (operands swapped)
 #pragma unroll
@@ -312,8 +328,15 @@ hipError_t launch_pw32(const float* A, const float* W, const float* bias, const 
       (act != ACT_NONE && act != ACT_SILU))
     return hipErrorInvalidValue;
   if (mfma) {
+    // mfma = 1: loads one chunk ahead (round 3); 2: three chunks ahead where K has >= 4 chunks and
+    // the grid leaves < 4 workgroups per CU (the 7^2-stage projects, K = 672 / 1152: 134 -> 107 and
+    // 199 -> 160 us per launch); launches with more workgroups hide the latency by occupancy and
+    // measured 1.3-1.7x SLOWER with the deeper prefetch (its 16 more VGPRs)
     const dim3 grid((M + QB - 1) / QB, (N + QB - 1) / QB);
-    hipLaunchKernelGGL(pw32m_kernel, grid, dim3(256), 0, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act);
+    if (mfma >= 2 && K >= 4 * QK && (long)grid.x * grid.y < 4 * 256)
+      hipLaunchKernelGGL(pw32m_kernel<4>, grid, dim3(256), 0, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act);
+    else
+      hipLaunchKernelGGL(pw32m_kernel<2>, grid, dim3(256), 0, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act);
     return hipGetLastError();
   }
   const dim3 grid((M + PB - 1) / PB, (N + PB - 1) / PB);

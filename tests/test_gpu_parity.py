@@ -64,7 +64,8 @@ def test_effnet_fp32_tower_vs_golden(engine, golden, golden_inputs):
 
 
 def test_fp32_tower_mfma_pointwise_bit_identical(det_sd, clip_sd):
-    """The fp32 tower's 1x1 convolutions on the fp32-input MFMA (option pw32_mfma = 1, default:
+    """The fp32 tower's 1x1 convolutions on the fp32-input MFMA (option pw32_mfma = 1: loads one
+    K-chunk ahead; 2, default since round 4: three chunks ahead where K allows --
     v_mfma_f32_16x16x4_f32 is a k-ordered fp32 fmaf chain) against the fp32-FMA VALU kernel
     (pw32_mfma = 0): every logit bit-identical, on the ill-conditioned He draw the mode exists for."""
     import mmf_amd.synthetic as syn
@@ -76,11 +77,12 @@ def test_fp32_tower_mfma_pointwise_bit_identical(det_sd, clip_sd):
         imgs = syn.images(64, 29)
         eng.set_option("pw32_mfma", 0)
         lg0, _ = eng.effnet_forward(imgs)
-        eng.set_option("pw32_mfma", 1)
-        lg1, _ = eng.effnet_forward(imgs)
-        torch.cuda.synchronize()
-        assert torch.isfinite(lg1).all()
-        assert torch.equal(lg0, lg1), (lg0 - lg1).abs().max().item()
+        for mode in (1, 2):
+            eng.set_option("pw32_mfma", mode)
+            lg1, _ = eng.effnet_forward(imgs)
+            torch.cuda.synchronize()
+            assert torch.isfinite(lg1).all()
+            assert torch.equal(lg0, lg1), (mode, (lg0 - lg1).abs().max().item())
     finally:
         eng.close()
 
