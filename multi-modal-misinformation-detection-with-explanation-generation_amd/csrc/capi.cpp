@@ -139,6 +139,8 @@ struct Options {
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
+  int fuse_expand32 = 0;  // fp32 tower: expand + depthwise fused for the <= 40-channel inputs (bit-identical;
+                          // measured 11.82 -> 13.79 ms per 512 images: kept off)
   int cu_split = 0;     // > 0: EfficientNet on that many CUs, the encoders on the rest (CU-masked streams; A/B)
   int cu_split_layout = 0;  // which mask bits: 0 = the n lowest, 1 = n / 8 from each 32-bit word (one per XCD
                             // if the driver maps bit words to XCDs), 2 = bits i with i % 8 < ... (see ensure_masked_towers)
@@ -155,7 +157,7 @@ const OptName kOptNames[] = {
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
-    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -1026,13 +1028,23 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
   for (const EffBlock& b : h->e_blocks) {
     const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
     const float* src = cur;
-    if (b.expand != 1) {
+    bool fused = false;
+    if (b.expand != 1 && h->opt.fuse_expand32) {
+      ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k + 2.0 * B * H * W * b.cin * b.cexp,
+                   4.0 * B * ((double)H * W * b.cin + (double)Ho * Wo * b.cexp));
+      const hipError_t e = launch_expand_dw32(cur, b.e.w32, b.e.b, b.wd_t, b.bd, e32_dw, B, H, W, b.cin, b.cexp, b.k,
+                                              b.stride, s);
+      if (e != hipErrorNotSupported) HIPCHK(e);
+      fused = e == hipSuccess;
+    }
+    if (fused) {
+    } else if (b.expand != 1) {
       ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * b.cin * b.cexp, 4.0 * B * H * W * (b.cin + b.cexp));
       HIPCHK(launch_pw32(cur, b.e.w32, b.e.b, nullptr, 1, nullptr, e32_exp, B * H * W, b.cexp, b.cin, 3 /* SiLU */, s,
                              h->opt.pw32_mfma));
       src = e32_exp;
     }
-    {
+    if (!fused) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k, 4.0 * B * b.cexp * ((double)H * W + Ho * Wo));
       HIPCHK(launch_dw32(src, b.wd_t, b.bd, e32_dw, B, H, W, b.cexp, b.k, b.stride, s));
     }

@@ -194,6 +194,8 @@ hipError_t launch_pw32(const float* A, const float* W, const float* bias, const 
 hipError_t launch_dw32(const float* in, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                        int k, int stride, hipStream_t s);
 // part[b][j][c] = sum over pixel chunk j of nchunks (the SE's pool partials)
+hipError_t launch_expand_dw32(const float* in, const float* we, const float* be, const float* wd, const float* bd,
+                              float* out, int B, int H, int W, int cin, int cexp, int k, int stride, hipStream_t s);
 hipError_t launch_sum32(const float* x, int B, int HW, int C, int nchunks, float* part, hipStream_t s);
 hipError_t launch_gap32(const float* x, int HW, int C, const float* w, const float* b, float* logits, float* score,
                         int score_stride, int B, hipStream_t s);

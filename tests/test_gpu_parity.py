@@ -87,6 +87,30 @@ def test_fp32_tower_mfma_pointwise_bit_identical(det_sd, clip_sd):
         eng.close()
 
 
+def test_fp32_tower_fused_fronts_bit_identical(det_sd, clip_sd):
+    """The fp32 tower's fused expand + depthwise fronts (option fuse_expand32 = 1, round 4, off by
+    default -- slower, DESIGN.md §4: stages 2.1 - 4.1, the expanded tensor kept in LDS) against the
+    separate pw32m + dw32 launches:
+    every logit bit-identical, on the ill-conditioned He draw (a reordered sum would show there), at
+    a batch whose tiles include ragged edges (56 / 8, 28 / 7 and 14 / 7 tiles, halos past the image)."""
+    import mmf_amd.synthetic as syn
+    import mmf_amd.weights as W
+    from mmf_amd.engine import Engine
+    eng = Engine(0, W.synthetic_detector_state(0, effnet_gain=2 ** 0.5), None, max_batch=48)
+    try:
+        eng.set_option("effnet_fp32", 1)
+        imgs = syn.images(48, 31)
+        eng.set_option("fuse_expand32", 0)
+        lg0, _ = eng.effnet_forward(imgs)
+        eng.set_option("fuse_expand32", 1)
+        lg1, _ = eng.effnet_forward(imgs)
+        torch.cuda.synchronize()
+        assert torch.isfinite(lg1).all()
+        assert torch.equal(lg0, lg1), (lg0 - lg1).abs().max().item()
+    finally:
+        eng.close()
+
+
 def test_clip_embeddings(engine, golden, golden_inputs):
     ie = engine.clip_image(golden_inputs["imgs"]).cpu().numpy()
     te = engine.clip_text(golden["clip_ids"], golden["clip_mask"]).cpu().numpy()
