@@ -139,6 +139,7 @@ struct Options {
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
+  int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
   int fuse_expand32 = 0;  // fp32 tower: expand + depthwise fused for the <= 40-channel inputs (bit-identical;
                           // measured 11.82 -> 13.79 ms per 512 images: kept off)
   int cu_split = 0;     // > 0: EfficientNet on that many CUs, the encoders on the rest (CU-masked streams; A/B)
@@ -157,7 +158,8 @@ const OptName kOptNames[] = {
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
-    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
+    {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -1601,10 +1603,13 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
     st_eff = h->tower[1];
     st_ctxt = h->tower[2];
   }
-  CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
-  CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
-  CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
-  CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
+  // diag_skip (diagnostic only, never set by the API or bench.py): towers left out to measure each
+  // tower's marginal cost in the concurrent step (bit 1 text, 2 EfficientNet, 4 CLIP text, 8 ViT)
+  const int skip = h->opt.diag_skip;
+  if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
+  if (!(skip & 4)) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
+  if (!(skip & 2)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
+  if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
   if (concurrent) {
     for (int i = 0; i < 3; ++i) {
       HIPCHK(hipEventRecord(h->join_ev[i], h->tower[i]));
