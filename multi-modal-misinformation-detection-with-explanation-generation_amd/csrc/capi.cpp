@@ -139,6 +139,7 @@ struct Options {
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
+  int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
   int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
   int fuse_expand32 = 0;  // fp32 tower: expand + depthwise fused for the <= 40-channel inputs (bit-identical;
                           // measured 11.82 -> 13.79 ms per 512 images: kept off)
@@ -159,7 +160,7 @@ const OptName kOptNames[] = {
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
-    {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -778,14 +779,38 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   }
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = h->r_layers[i];
-    // (M <= 512, a single text or a few: split-K through the workspace, gemm_splitk_factor)
-    GemmArgs g = with_ws(gemm_args(w.r_xb, 768, Ly.qkv, M), w.sk_text, w.sk_elems);
-    g.c16 = w.r_qkv;
-    CHK(gemm(h, g, s));
-    CHK(attn(h, w.r_qkv, 2304, mask, w.r_ctx, 768, B, L, 12, 0, s));
     // last layer: only the CLS row feeds the heads (misinfo_forensics.py:95), so the rows below
     // run on B compact CLS rows (strided A / residual reads) instead of B*L rows
     const bool last = (i == 11);
+    GemmArgs g;
+    if (last && h->opt.last_q1) {
+      // ... and of its attention only the CLS queries are needed: K and V of every row (the fused
+      // weight's rows 768..2303: 3 whole persistent rounds at M = 32768 instead of 4.5), Q of the
+      // B CLS rows (skinny, split-K), one query per (sequence, head) (attention_q1_kernel) written
+      // to the CLS rows of r_ctx
+      Lin16 kv = Ly.qkv;
+      kv.w += (size_t)768 * 768;
+      kv.b += 768;
+      kv.out = 1536;
+      g = with_ws(gemm_args(w.r_xb, 768, kv, M), w.sk_text, w.sk_elems);
+      g.c16 = w.r_qkv + 768;
+      g.ldc = 2304;
+      CHK(gemm(h, g, s));
+      Lin16 qq = Ly.qkv;
+      qq.out = 768;
+      f16_t* qcls = w.r_h;  // free until the FFN-1 below
+      g = with_ws(gemm_args(w.r_xb, L * 768, qq, B), w.sk_text, w.sk_elems);
+      g.c16 = qcls;
+      CHK(gemm(h, g, s));
+      ProfScope ps(h, s, PK_ATTN, 4.0 * B * 12 * (double)L * 64, (double)B * L * 768 * 2 * 2);
+      HIPCHK(launch_attention_q1(qcls, 768, w.r_qkv, 2304, 768, 1536, mask, nullptr, w.r_ctx, L * 768, B, L, 12, s));
+    } else {
+      // (M <= 512, a single text or a few: split-K through the workspace, gemm_splitk_factor)
+      g = with_ws(gemm_args(w.r_xb, 768, Ly.qkv, M), w.sk_text, w.sk_elems);
+      g.c16 = w.r_qkv;
+      CHK(gemm(h, g, s));
+      CHK(attn(h, w.r_qkv, 2304, mask, w.r_ctx, 768, B, L, 12, 0, s));
+    }
     if (!last) {
       // out-proj and FFN-2 write their fp16 branch output y; the residual add happens in fp32
       // inside add+LN (y lives in r_h, free until FFN-1, then in r_ctx, free after out-proj)
@@ -860,13 +885,50 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
   int sti = 0;
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = layers[i];
-    GemmArgs g = lazy ? ln_consumer(x16, H, Ly.qkv_f, Ly.qkv_u, cur, M)
-                      : with_ws(gemm_args(xb, H, Ly.qkv, M), skws, sk_elems);
-    g.c16 = qkv;
-    CHK(gemm(h, g, s));
-    CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
+    GemmArgs g;
+    if (i == 11 && h->opt.last_q1) {
+      // only the pooled rows' queries are needed in the last layer: their stream rows -> xc (fp32,
+      // also the residual below), LN1 -> Q (skinny GEMM on the unfolded weights), K and V of every
+      // row (the fused weight's rows H..3H; lazy consumer or materialised), one query per
+      // (sequence, head) straight into the compact ctxc
+      HIPCHK(launch_gather_rows2(nullptr, x16 ? nullptr : x, x16, last_rows, L, H, nullptr, xc, B, s));
+      f16_t* xq = hid;                   // hid ([M][I] fp16) is free until FFN-1
+      f16_t* qc = hid + (size_t)B * H;
+      CHK(lnorm(h, xc, H, Ly.ln1, nullptr, 0, xq, H, B, H, s));
+      Lin16 qq = Ly.qkv;
+      qq.out = H;
+      g = with_ws(gemm_args(xq, H, qq, B), skws, sk_elems);
+      g.c16 = qc;
+      CHK(gemm(h, g, s));
+      if (lazy) {
+        Lin16 kvf = Ly.qkv_f;
+        kvf.w += (size_t)H * H;
+        kvf.b += H;  // (c and u are padded by 256 past 3H: the 256-column DMA stays in bounds)
+        kvf.out = 2 * H;
+        g = ln_consumer(x16, H, kvf, Ly.qkv_u + H, cur, M);
+      } else {
+        Lin16 kv = Ly.qkv;
+        kv.w += (size_t)H * H;
+        kv.b += H;
+        kv.out = 2 * H;
+        g = with_ws(gemm_args(xb, H, kv, M), skws, sk_elems);
+      }
+      g.c16 = qkv + H;
+      g.ldc = 3 * H;
+      CHK(gemm(h, g, s));
+      {
+        ProfScope ps(h, s, PK_ATTN, 4.0 * B * heads * (double)L * 64, (double)B * L * H * 2 * 2);
+        HIPCHK(launch_attention_q1(qc, H, qkv, 3 * H, H, 2 * H, mask, causal ? last_rows : nullptr, ctxc, H, B, L,
+                                   heads, s));
+      }
+    } else {
+      g = lazy ? ln_consumer(x16, H, Ly.qkv_f, Ly.qkv_u, cur, M) : with_ws(gemm_args(xb, H, Ly.qkv, M), skws, sk_elems);
+      g.c16 = qkv;
+      CHK(gemm(h, g, s));
+      CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
+    }
     if (i == 11) {
-      HIPCHK(launch_gather_rows2(ctx, x16 ? nullptr : x, x16, last_rows, L, H, ctxc, xc, B, s));
+      if (!h->opt.last_q1) HIPCHK(launch_gather_rows2(ctx, x16 ? nullptr : x, x16, last_rows, L, H, ctxc, xc, B, s));
       g = with_ws(gemm_args(ctxc, H, Ly.o, B), skws, sk_elems);
       g.res32 = xc;
       g.c32 = xc;

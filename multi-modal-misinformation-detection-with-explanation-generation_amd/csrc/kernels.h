@@ -76,6 +76,11 @@ hipError_t launch_add_ln(const f16_t* x, int ldx, const f16_t* y, int ldy, const
 
 // Fused multi-head attention, head_dim 64, L <= 128: qkv fp16 [B*L][ldqkv] with q at col h*64,
 // k at D + h*64, v at 2D + h*64 (D = H*64); mask int32 [B][L] (1 keep) or null; out fp16 [B*L][ldo].
+// one query per sequence over the sequence's keys (the compact last encoder layer): q [B][ldq], out row b
+// at out + b * ldo; qpos (nullable) = the query's position per sequence for a causal mask
+hipError_t launch_attention_q1(const f16_t* q, int ldq, const f16_t* qkv, int ld, int koff, int voff,
+                               const int32_t* mask, const int32_t* qpos, f16_t* out, int ldo, int B, int L, int H,
+                               hipStream_t s);
 hipError_t launch_attention(const f16_t* qkv, int ldqkv, const int32_t* mask, f16_t* out, int ldo, int B,
                             int L, int H, int causal, hipStream_t s);
 
@@ -108,8 +113,8 @@ hipError_t launch_eos_index(const int32_t* ids, int32_t* out, int B, int L, int 
 // gather rows: out fp16 [B][C] = LN(x[row_index(b)]) where row_index = b*L + (idx ? idx[b] : 0)
 hipError_t launch_gather_ln(const float* x, const int32_t* idx, int L, const float* g, const float* b, float eps,
                             f16_t* out, float* out32, int B, int C, hipStream_t s);
-// compact copies of rows b*L + (idx ? idx[b] : 0) of a fp16 and an fp32 (a32, or fp16 a32h: exactly
-// one non-null) [.,C] buffer; o32 is fp32 either way
+// compact copies of rows b*L + (idx ? idx[b] : 0) of a fp16 (a16, nullable: then o16 is not written) and
+// an fp32 (a32, or fp16 a32h: exactly one non-null) [.,C] buffer; o32 is fp32 either way
 hipError_t launch_gather_rows2(const f16_t* a16, const float* a32, const f16_t* a32h, const int32_t* idx, int L,
                                int C, f16_t* o16, float* o32, int B, hipStream_t s);
 // L2-normalise rows of fp32 [B][C] in place (C multiple of 64)

@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void gather_rows2_kernel(const f16_t* a16, con
   if (bi >= B) return;
   const size_t row = (size_t)bi * L + (idx ? idx[bi] : 0);
   for (int c = threadIdx.x * 4; c < C; c += 256 * 4) {
-    *reinterpret_cast<uint2*>(o16 + (size_t)bi * C + c) = *reinterpret_cast<const uint2*>(a16 + row * C + c);
+    if (a16) *reinterpret_cast<uint2*>(o16 + (size_t)bi * C + c) = *reinterpret_cast<const uint2*>(a16 + row * C + c);
     if constexpr (std::is_same_v<XT, float>) {
       *reinterpret_cast<float4*>(o32 + (size_t)bi * C + c) = *reinterpret_cast<const float4*>(a32 + row * C + c);
     } else {
