@@ -60,6 +60,15 @@ def launch_ranks(n: int, cmd: list, check_devices: bool = True, poll_s: float = 
     env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n),
                 LOCAL_WORLD_SIZE=str(n))
     procs = []
+    import signal
+
+    def stop_children(signum, _frame):  # the launcher itself stopped (e.g. a driver timeout): no orphans
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        sys.exit(128 + signum)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, stop_children)
     for r in range(n):
         env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr))

@@ -327,9 +327,9 @@ __global__ __launch_bounds__(256) void attention_long_kernel(const f16_t* __rest
 // is consumed after it, so the other queries of that layer are dead work).  One wave per (sequence,
 // head): lanes over keys for the scores (fp32 dot products of 64 dims, ascending), wave max / sum,
 // then lanes over the 64 head dims for O = sum_j p_j v_j (keys ascending, fp32), stored fp16.
-// q: [B][ldq] (head h at h * 64); K / V: the QKV rows of the sequence (row b * L + j, columns
+// q: [B][ldq] fp32 (head h at h * 64); K / V: the QKV rows of the sequence (row b * L + j, columns
 // koff + h * 64 / voff + h * 64); a masked key (mask 0, or past qpos[b] when causal) is excluded.
-__global__ __launch_bounds__(256) void attention_q1_kernel(const f16_t* __restrict__ q, int ldq,
+__global__ __launch_bounds__(256) void attention_q1_kernel(const float* __restrict__ q, int ldq,
                                                            const f16_t* __restrict__ qkv, int ld, int koff, int voff,
                                                            const int32_t* __restrict__ mask,
                                                            const int32_t* __restrict__ qpos, f16_t* __restrict__ out,
@@ -339,18 +339,16 @@ __global__ __launch_bounds__(256) void attention_q1_kernel(const f16_t* __restri
   const int wid = blockIdx.x * 4 + wave;
   if (wid >= B * H) return;  // wave-uniform
   const int bi = wid / H, h = wid - bi * H;
-  float qf[64];
+  float qf[64];  // the query in fp32 (the skinny Q GEMM's fp32 output: no fp16 rounding of q)
   {
-    const uint4* qp = reinterpret_cast<const uint4*>(q + (size_t)bi * ldq + h * 64);
+    const float4* qp = reinterpret_cast<const float4*>(q + (size_t)bi * ldq + h * 64);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const uint4 v = qp[c];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        qf[c * 8 + e * 2] = lo_h(w[e]);
-        qf[c * 8 + e * 2 + 1] = hi_h(w[e]);
-      }
+    for (int c = 0; c < 16; ++c) {
+      const float4 v = qp[c];
+      qf[c * 4] = v.x;
+      qf[c * 4 + 1] = v.y;
+      qf[c * 4 + 2] = v.z;
+      qf[c * 4 + 3] = v.w;
     }
   }
   const int last = qpos ? qpos[bi] : L - 1;  // causal: keys <= the query position
@@ -392,16 +390,16 @@ __global__ __launch_bounds__(256) void attention_q1_kernel(const f16_t* __restri
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const f16_t* vp = qkv + (size_t)bi * L * ld + voff + h * 64 + lane;
   float o = 0.f;
-  for (int j = 0; j <= last && j < L; ++j) o = fmaf(ps[wave][j], (float)vp[(size_t)j * ld], o);
-  out[(size_t)bi * ldo + h * 64 + lane] = (f16_t)(sum > 0.f ? o / sum : 0.f);
+  for (int j = 0; j <= last && j < L; ++j) o = fmaf(ps[wave][j], h2f(vp[(size_t)j * ld]), o);
+  out[(size_t)bi * ldo + h * 64 + lane] = f2h(sum > 0.f ? o / sum : 0.f);
 }
 
 }  // namespace
 
-hipError_t launch_attention_q1(const f16_t* q, int ldq, const f16_t* qkv, int ld, int koff, int voff,
+hipError_t launch_attention_q1(const float* q, int ldq, const f16_t* qkv, int ld, int koff, int voff,
                                const int32_t* mask, const int32_t* qpos, f16_t* out, int ldo, int B, int L, int H,
                                hipStream_t s) {
-  if (L <= 0 || L > LLONG || (ldq & 7) || (ld & 7) || (koff & 7) || (voff & 7)) return hipErrorInvalidValue;
+  if (L <= 0 || L > LLONG || (ldq & 3) || (ld & 7) || (koff & 7) || (voff & 7)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(attention_q1_kernel, dim3((B * H + 3) / 4), dim3(256), 0, s, q, ldq, qkv, ld, koff, voff, mask,
                      qpos, out, ldo, B, L, H);
   return hipGetLastError();

@@ -796,12 +796,21 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       g.c16 = w.r_qkv + 768;
       g.ldc = 2304;
       CHK(gemm(h, g, s));
+      // Q of the CLS rows in fp32 (r_y is free until hilo_rows below); with the split stream the
+      // lo word is added by a second skinny GEMM (q = Wq hi + bq + Wq lo: the ~22-bit row)
       Lin16 qq = Ly.qkv;
       qq.out = 768;
-      f16_t* qcls = w.r_h;  // free until the FFN-1 below
+      float* qcls = w.r_y;
       g = with_ws(gemm_args(w.r_xb, L * 768, qq, B), w.sk_text, w.sk_elems);
-      g.c16 = qcls;
+      g.c32 = qcls;
       CHK(gemm(h, g, s));
+      if (rlo) {
+        g = with_ws(gemm_args(reinterpret_cast<const f16_t*>(rlo), L * 768, qq, B), w.sk_text, w.sk_elems);
+        g.bias = nullptr;
+        g.res32 = qcls;
+        g.c32 = qcls;
+        CHK(gemm(h, g, s));
+      }
       ProfScope ps(h, s, PK_ATTN, 4.0 * B * 12 * (double)L * 64, (double)B * L * 768 * 2 * 2);
       HIPCHK(launch_attention_q1(qcls, 768, w.r_qkv, 2304, 768, 1536, mask, nullptr, w.r_ctx, L * 768, B, L, 12, s));
     } else {
@@ -893,12 +902,12 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
       // (sequence, head) straight into the compact ctxc
       HIPCHK(launch_gather_rows2(nullptr, x16 ? nullptr : x, x16, last_rows, L, H, nullptr, xc, B, s));
       f16_t* xq = hid;                   // hid ([M][I] fp16) is free until FFN-1
-      f16_t* qc = hid + (size_t)B * H;
+      float* qc = reinterpret_cast<float*>(hid + (size_t)B * H);  // fp32 queries
       CHK(lnorm(h, xc, H, Ly.ln1, nullptr, 0, xq, H, B, H, s));
       Lin16 qq = Ly.qkv;
       qq.out = H;
       g = with_ws(gemm_args(xq, H, qq, B), skws, sk_elems);
-      g.c16 = qc;
+      g.c32 = qc;
       CHK(gemm(h, g, s));
       if (lazy) {
         Lin16 kvf = Ly.qkv_f;

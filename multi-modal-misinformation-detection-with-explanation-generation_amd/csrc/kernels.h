@@ -76,9 +76,9 @@ hipError_t launch_add_ln(const f16_t* x, int ldx, const f16_t* y, int ldy, const
 
 // Fused multi-head attention, head_dim 64, L <= 128: qkv fp16 [B*L][ldqkv] with q at col h*64,
 // k at D + h*64, v at 2D + h*64 (D = H*64); mask int32 [B][L] (1 keep) or null; out fp16 [B*L][ldo].
-// one query per sequence over the sequence's keys (the compact last encoder layer): q [B][ldq], out row b
-// at out + b * ldo; qpos (nullable) = the query's position per sequence for a causal mask
-hipError_t launch_attention_q1(const f16_t* q, int ldq, const f16_t* qkv, int ld, int koff, int voff,
+// one query per sequence over the sequence's keys (the compact last encoder layer): q [B][ldq] fp32, out
+// row b at out + b * ldo; qpos (nullable) = the query's position per sequence for a causal mask
+hipError_t launch_attention_q1(const float* q, int ldq, const f16_t* qkv, int ld, int koff, int voff,
                                const int32_t* mask, const int32_t* qpos, f16_t* out, int ldo, int B, int L, int H,
                                hipStream_t s);
 hipError_t launch_attention(const f16_t* qkv, int ldqkv, const int32_t* mask, f16_t* out, int ldo, int B,

@@ -338,7 +338,22 @@ def test_splitk_compact_layers_match_unsplit(engine, golden):
     a, b = outs
     np.testing.assert_allclose(a["scores"], b["scores"], atol=2e-4)
     np.testing.assert_allclose(a["probs"], b["probs"], atol=2e-4)
-    np.testing.assert_array_equal(a["top_idx"], b["top_idx"])
+    np.testing.assert_allclose(a["top_sims"], b["top_sims"], atol=2e-4)
+    # the top-5 orders agree except where the summation order under test reorders near-equal
+    # similarities (the golden vault plants scaled copies of random-init image embeddings, which all
+    # point in nearly one direction): a position may differ only between entries whose similarities
+    # are within 2e-4 in both runs
+    for r in range(B):
+        ia, ib = a["top_idx"][r], b["top_idx"][r]
+        if np.array_equal(ia, ib):
+            continue
+        sa = dict(zip(ia.tolist(), a["top_sims"][r].tolist()))
+        sb = dict(zip(ib.tolist(), b["top_sims"][r].tolist()))
+        for k in np.flatnonzero(ia != ib):
+            assert abs(a["top_sims"][r][k] - b["top_sims"][r][k]) < 2e-4, (r, ia, ib)
+            assert abs(sa[int(ia[k])] - a["top_sims"][r][k]) < 1e-12
+            if int(ib[k]) in sa:
+                assert abs(sa[int(ib[k])] - sb[int(ib[k])]) < 2e-4
 
 
 def test_effnet_config3_batch512(det_sd, clip_sd):
