@@ -783,7 +783,9 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
     // run on B compact CLS rows (strided A / residual reads) instead of B*L rows
     const bool last = (i == 11);
     GemmArgs g;
-    if (last && h->opt.last_q1) {
+    // (split-stream mode -- outlier-feature checkpoints, which sit at the parity bar: DESIGN §4 --
+    // keeps the full last-layer attention, whose roundings were measured there)
+    if (last && h->opt.last_q1 && !rlo) {
       // ... and of its attention only the CLS queries are needed: K and V of every row (the fused
       // weight's rows 768..2303: 3 whole persistent rounds at M = 32768 instead of 4.5), Q of the
       // B CLS rows (skinny, split-K), one query per (sequence, head) (attention_q1_kernel) written
