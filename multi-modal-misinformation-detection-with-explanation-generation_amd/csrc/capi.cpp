@@ -1272,7 +1272,7 @@ int ensure_masked_towers(mmf_handle* h, int n) {
     (e ? eff : enc)[c >> 5] |= 1u << (c & 31);
   }
   for (int i = 0; i < 4; ++i)
-    HIPCHK(hipExtStreamCreateWithCUMask(&h->mtower[i], (uint32_t)h->ncu, i == 1 ? eff.data() : enc.data()));
+    HIPCHK(hipExtStreamCreateWithCUMask(&h->mtower[i], (uint32_t)words, i == 1 ? eff.data() : enc.data()));  // size in 32-bit words
   h->mtower_split = n;
   h->mtower_layout = layout;
   return 0;
