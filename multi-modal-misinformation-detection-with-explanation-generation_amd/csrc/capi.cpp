@@ -140,6 +140,8 @@ struct Options {
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
+                        // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
+                        // GEMMs round to as many rounds as QKV: measured slower, off)
   int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
   int fuse_expand32 = 0;  // fp32 tower: expand + depthwise fused for the <= 40-channel inputs (bit-identical;
                           // measured 11.82 -> 13.79 ms per 512 images: kept off)
@@ -785,7 +787,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
     GemmArgs g;
     // (split-stream mode -- outlier-feature checkpoints, which sit at the parity bar: DESIGN §4 --
     // keeps the full last-layer attention, whose roundings were measured there)
-    if (last && h->opt.last_q1 && !rlo) {
+    if (last && (h->opt.last_q1 & 1) && !rlo) {
       // ... and of its attention only the CLS queries are needed: K and V of every row (the fused
       // weight's rows 768..2303: 3 whole persistent rounds at M = 32768 instead of 4.5), Q of the
       // B CLS rows (skinny, split-K), one query per (sequence, head) (attention_q1_kernel) written
@@ -897,7 +899,7 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = layers[i];
     GemmArgs g;
-    if (i == 11 && h->opt.last_q1) {
+    if (i == 11 && (h->opt.last_q1 & 2)) {
       // only the pooled rows' queries are needed in the last layer: their stream rows -> xc (fp32,
       // also the residual below), LN1 -> Q (skinny GEMM on the unfolded weights), K and V of every
       // row (the fused weight's rows H..3H; lazy consumer or materialised), one query per
@@ -939,7 +941,7 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
       CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
     }
     if (i == 11) {
-      if (!h->opt.last_q1) HIPCHK(launch_gather_rows2(ctx, x16 ? nullptr : x, x16, last_rows, L, H, ctxc, xc, B, s));
+      if (!(h->opt.last_q1 & 2)) HIPCHK(launch_gather_rows2(ctx, x16 ? nullptr : x, x16, last_rows, L, H, ctxc, xc, B, s));
       g = with_ws(gemm_args(ctxc, H, Ly.o, B), skws, sk_elems);
       g.res32 = xc;
       g.c32 = xc;

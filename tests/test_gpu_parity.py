@@ -111,6 +111,34 @@ def test_fp32_tower_fused_fronts_bit_identical(det_sd, clip_sd):
         eng.close()
 
 
+@pytest.mark.parametrize("B", [3, 37])
+def test_compact_last_layer_queries(engine, B):
+    """Option last_q1 (round 4): the last encoder layer computes K / V for every row but Q and the
+    attention only for the pooled rows (RoBERTa CLS: bit 1, default; CLIP CLS / EOS: bit 2), one
+    query per (sequence, head).  The 5 scores and probabilities of every combination agree with the
+    full last layer at the north-star tolerance; B = 3 runs the materialised-LN small-batch CLIP path,
+    B = 37 the lazy-LN one; ragged texts / captions exercise the key masks and the causal EOS query."""
+    import mmf_amd.synthetic as syn
+    rid, rm = syn.roberta_ids(B, 128, 41, [128, 90, 7, 33])
+    cid, cm = syn.clip_ids(B, 77, 41, [77, 30, 5, 12])
+    imgs = syn.images(B, 41)
+    outs = {}
+    try:
+        for v in (0, 1, 3):
+            engine.set_option("last_q1", v)
+            o = engine.analyze_batch(rid, rm, cid, cm, imgs)
+            torch.cuda.synchronize()
+            outs[v] = {k: t.cpu().numpy() for k, t in o.items()}
+    finally:
+        engine.set_option("last_q1", 1)
+    for v in (1, 3):
+        assert np.isfinite(outs[v]["scores"]).all()
+        np.testing.assert_allclose(outs[v]["scores"], outs[0]["scores"], atol=2e-4)
+        np.testing.assert_allclose(outs[v]["probs"], outs[0]["probs"], atol=2e-4)
+    # bit 1 leaves the CLIP towers untouched: their signals are bit-identical
+    np.testing.assert_array_equal(outs[1]["scores"][:, 2:], outs[0]["scores"][:, 2:])
+
+
 def test_clip_embeddings(engine, golden, golden_inputs):
     ie = engine.clip_image(golden_inputs["imgs"]).cpu().numpy()
     te = engine.clip_text(golden["clip_ids"], golden["clip_mask"]).cpu().numpy()
