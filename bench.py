@@ -313,21 +313,29 @@ def main():
         # the driver's `python bench.py --gpus N`: become the parent of N ranks (never touches the GPU)
         os.environ["MMF_BENCH_PARENT"] = "1"
         cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
-        sys.exit(benchrun.launch_ranks(a.gpus, cmd, check_devices=not a.cpu_standin))
+        sys.exit(benchrun.launch_ranks(a.gpus, cmd, check_devices=not (a.cpu_standin or
+                                                                        os.environ.get("MMF_BENCH_SHARE_GPU") == "1")))
     world, rank, local = benchrun.rank_env()
     if world != a.gpus:
         benchrun.progress(f"note: --gpus {a.gpus} but the launcher started {world} rank(s); reporting {world}")
     if a.cpu_standin:
         return standin_main(a, world, rank)
+    # MMF_BENCH_SHARE_GPU=1 (rehearsal only, never a measurement): N ranks share the visible GPUs
+    # round-robin and time over gloo -- the whole multi-rank path (launch, per-rank engines and
+    # inputs, barriers, max-over-ranks) on a box with fewer GPUs than ranks
+    share = os.environ.get("MMF_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = benchrun.init_dist(world, "nccl", dev)
+    dist = benchrun.init_dist(world, "gloo" if share else "nccl", dev)
+    tdev = None if share else dev  # device of the max-over-ranks reduction (gloo: host)
 
     import mmf_amd.weights as W
     from mmf_amd.engine import Engine
 
     B = a.batch
-    benchrun.progress(f"rank {rank}/{world}: building the engine")
+    benchrun.progress(f"rank {rank}/{world}: building the engine on cuda:{local}")
     det = W.synthetic_detector_state(0)
     eng = Engine(local, det, W.synthetic_clip_state(0), max_batch=B)
     t = build_inputs(eng, B, rank)
@@ -337,7 +345,7 @@ def main():
     # headline: inputs from pinned host memory every step, results back to the host
     host = {k: v.cpu().pin_memory() for k, v in t.items()}
     pipe = eng.host_pipeline(B, host["rid"].shape[1], host["cid"].shape[1])
-    dt = benchrun.timed_steps(lambda: pipe.submit(host), a.steps, a.warmup, dist, sync, dev)
+    dt = benchrun.timed_steps(lambda: pipe.submit(host), a.steps, a.warmup, dist, sync, tdev)
     value = benchrun.whole_job_rate(world, B, a.steps, dt)
     h2d = sum(v.numel() * v.element_size() for v in host.values())
 
@@ -347,7 +355,7 @@ def main():
 
     def step():
         eng.analyze_batch(t["rid"], t["rm"], t["cid"], t["cm"], t["img"], out=out)
-    dt_hbm = benchrun.timed_steps(step, a.steps, a.warmup, dist, sync, dev)
+    dt_hbm = benchrun.timed_steps(step, a.steps, a.warmup, dist, sync, tdev)
     hbm = benchrun.whole_job_rate(world, B, a.steps, dt_hbm)
 
     roofline = None
@@ -373,7 +381,10 @@ def main():
         res = result_line(
             a, world, B, dt, value,
             "synthetic (seeded token ids, structured uint8 images, 2170-row vault); random-init weights",
-            config_extra={"h2d_bytes_per_step_per_gpu": h2d},
+            config_extra=dict({"h2d_bytes_per_step_per_gpu": h2d},
+                              **({"rehearsal": f"{world} ranks sharing {torch.cuda.device_count()} GPU(s) over gloo "
+                                                "(MMF_BENCH_SHARE_GPU=1): a functional check, not a measurement"}
+                                 if share else {})),
             hbm_resident={"value": round(hbm, 2), "unit": "pairs/s", "ms_per_step": round(1000 * dt_hbm / a.steps, 3),
                           "note": "same step with inputs already in HBM and results left on the device"},
             achieved_tflops_whole_path=round(value * GFLOP_PER_PAIR / 1e3, 1),
