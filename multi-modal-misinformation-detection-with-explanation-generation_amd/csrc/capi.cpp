@@ -135,6 +135,7 @@ struct Options {
   int pw32_mfma = 2;    // fp32 tower's 1x1 convs on the fp32-input MFMA (2: loads 3 K-chunks ahead, 1: one ahead)
                         // or the fp32-FMA VALU kernel (0) -- every mode bit-identical
   int gemm_wide = 0;    // 256x384 tiles where they save a persistent round (gemm.hip glds_pick; step A/B: a tie)
+  int gemm_w4 = 0;      // 192-column GEMM picks on the 4-wave 256x192 tiles (config 21; A/B)
   int dw_persist = 0;   // persistent depthwise kernels with the next tile's loads in flight (effnet.hip; A/B: slower)
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
@@ -159,6 +160,7 @@ const OptName kOptNames[] = {
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
     {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},            {"gemm_ring", &Options::gemm_ring, "MMF_GEMM_RING"},
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
+    {"gemm_w4", &Options::gemm_w4, "MMF_GEMM_W4"},
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
@@ -183,6 +185,7 @@ void apply_options(const Options& o, GemmArgs* g) {
   g->prio = o.gemm_prio;
   g->ring = o.gemm_ring;
   g->wide = o.gemm_wide;
+  g->w4 = o.gemm_w4;
   g->prod256 = o.ln_prod256;
 }
 
@@ -302,7 +305,7 @@ int free_group(mmf_handle* h, int group) {
 // each, so the numbers line up with a rocprofv3 kernel trace of the same run.
 constexpr int kGemmActs = 5, kGemmEpis = 3;
 enum ProfKind {
-  PK_GEMM0 = 0, PK_GEMM_LAST = 13 * kGemmEpis * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
+  PK_GEMM0 = 0, PK_GEMM_LAST = kGemmConfigs * kGemmEpis * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
   PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_PW32, PK_COUNT
 };
 const char* prof_kind_name(int k) {
@@ -1712,6 +1715,7 @@ int mmf_profile_end(mmf_handle* h, int max_kinds, int* counts, double* ms, doubl
   }
   if (!h->prof_recs.empty()) HIPCHK(hipEventSynchronize(h->ev_pool[h->prof_recs.back().ev + 1]));
   for (const auto& r : h->prof_recs) {
+    if (r.kind < 0 || r.kind >= PK_COUNT) continue;
     float t = 0.f;
     HIPCHK(hipEventElapsedTime(&t, h->ev_pool[r.ev], h->ev_pool[r.ev + 1]));
     counts[r.kind] += 1;

@@ -335,7 +335,7 @@ constexpr int kLnPMax = 8;  // partials per row a reader accepts
 // DBG (measurement builds, forced configs 15 / 16 only; outputs garbage): 1 = LDS-DMA + barriers only,
 // 2 = fragment reads + MFMAs + barriers only
 template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0>
-__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
+__global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 : 2) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
                                                                      int gm) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
   // K-slab of the NEXT tile is DMA'd into the free LDS stage during the current tile's last
@@ -935,7 +935,7 @@ static int forced_config(const GemmArgs& a) {
   if (c == 9 && !pw_applicable(a)) return -1;
   if (((c >= 12 && c <= 14) || c >= 17) && !gemm_ring_ok(a)) return -1;
   if (c == 20 && !wide_ok(a)) return -1;
-  return (c >= 0 && c <= 20) ? c : -1;
+  return (c >= 0 && c <= 21) ? c : -1;
 }
 
 // persistent 256-row LDS-DMA tiles: the column tile that minimises whole "rounds" of 256 CUs x
@@ -945,7 +945,7 @@ static int glds_pick(const GemmArgs& a, bool with_128) {
   // option gemm_ring, 192-column tiles that gemm_lc_kernel can serve run it instead, config 17)
   const long tm = (a.M + 255) / 256;
   const bool lc = a.ring && gemm_ring_ok(a);
-  const int bns[3] = {256, 192, 128}, cfg[3] = {11, lc ? 17 : 10, 5};
+  const int bns[3] = {256, 192, 128}, cfg[3] = {11, lc ? 17 : (a.w4 ? 21 : 10), 5};
   // measured per-flop efficiency (tools/gemm_bench.py; the loader / consumer kernel 0.95)
   const double eff[3] = {1.0, lc ? 0.95 : 0.88, 0.80};
   int best = 11;
@@ -1014,8 +1014,8 @@ const char* gemm_config_name(int c) {
                                 "pw_conv", "gemm_glds_pipe2<256,192,4,2>", "gemm_glds_pipe2<256,256,2,4>",
                                 "gemm_ring<256,192,4,2>", "gemm_ring_dma_only", "gemm_ring_compute_only",
                                 "gemm_glds_dma_only", "gemm_glds_compute_only", "gemm_lc<256,192,8+4>", "gemm_lc_dma_only",
-                                "gemm_lc_compute_only", "gemm_glds<256,384,2,4>"};
-  return (c >= 0 && c < 21) ? names[c] : "gemm_f16<?>";
+                                "gemm_lc_compute_only", "gemm_glds<256,384,2,4>", "gemm_glds_pipe2<256,192,2,2>"};
+  return (c >= 0 && c < kGemmConfigs) ? names[c] : "gemm_f16<?>";
 }
 
 hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
@@ -1049,6 +1049,7 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
     case 10: return run_glds<256, 192, 4, 2, true>(a, s);
     case 11: return run_glds<256, 256, 2, 4, true>(a, s);
     case 20: return run_glds<256, 384, 2, 4>(a, s);
+    case 21: return run_glds<256, 192, 2, 2, true>(a, s);  // 4 waves, 128x96 wave tiles (A/B)
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

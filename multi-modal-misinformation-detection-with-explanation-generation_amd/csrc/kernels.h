@@ -25,6 +25,7 @@ struct GemmArgs {
   int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
   int ring;                      // 1 = plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
   int wide;                      // 1 = 256x384 tiles may be picked (gemm.hip glds_pick)
+  int w4;                        // 1 = 192-column picks run the 4-wave tiles (config 21; A/B)
   int max_grid;                  // > 0: persistent GEMM grids capped at this many workgroups (the CUs of a
                                  //     CU-masked tower stream, option cu_split); 0 = 256
   int prod256;                   // 1 = lazy-LN producers (epi 2) on 256x256 tiles where N's 64-column
@@ -55,6 +56,7 @@ bool gemm_ring_ok(const GemmArgs& a);
 hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s, int dbg = 0);
 hipError_t launch_gemm_lc(const GemmArgs& a, hipStream_t s, int dbg = 0);  // loader / consumer waves (same conditions)
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
+constexpr int kGemmConfigs = 22;  // tile instantiations gemm_config can return (0 .. 21)
 const char* gemm_config_name(int c);
 // streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable
 bool pw_applicable(const GemmArgs& a);

@@ -1,5 +1,6 @@
 """The 256x384 LDS-DMA tiles of csrc/gemm.hip (config 20: descriptor fills, 192 accumulator
-registers per lane) against the production 256x256 / 256x192 kernels and a torch fp32 reference of
+registers per lane) and the 4-wave 256x192 tiles (config 21: one wave per SIMD, 128x96 wave tiles,
+accumulators in AGPRs) against the production 256x256 / 256x192 kernels and a torch fp32 reference of
 the same op (C = act(A W^T + b) [+ res], fp16 in / out, fp32 accumulation).
 
 Every tile shape accumulates each output element in the same order (32-deep MFMA chunks,
@@ -29,8 +30,9 @@ def _run(lib, hip, A, W, bias, res, M, N, K, act, cfg):
     return C
 
 
+@pytest.mark.parametrize("cfg", [20, 21])
 @pytest.mark.parametrize("M,N,K,act,resid", SHAPES)
-def test_wide_tiles_match_production_bitwise(M, N, K, act, resid):
+def test_wide_tiles_match_production_bitwise(M, N, K, act, resid, cfg):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import mmf_amd.hip as hip
@@ -41,7 +43,7 @@ def test_wide_tiles_match_production_bitwise(M, N, K, act, resid):
     bias = torch.randn(N, device="cuda", generator=g)
     res = torch.randn(M, N, device="cuda", generator=g).to(torch.float16) if resid else None
     try:
-        wide = _run(lib, hip, A, W, bias, res, M, N, K, act, 20)
+        wide = _run(lib, hip, A, W, bias, res, M, N, K, act, cfg)
         # (the half-step-pipelined 256x256 / 256x192 kernels need >= 3 K-steps of 64)
         base = {c: _run(lib, hip, A, W, bias, res, M, N, K, act, c) for c in ((11, 10) if K >= 192 else (4, 6))}
     finally:
