@@ -69,7 +69,13 @@ struct Lin16 {
 struct LNp { float* g = nullptr; float* b = nullptr; };
 // qkv_f / fc1_f (CLIP): the QKV and FFN-1 projections with their input LayerNorm folded in (lazy
 // LN, gemm.hip): w' = fp16(w diag(gamma)), bias c = b + w beta, u = rows of w' summed (fp16 values)
-struct EncLayer { Lin16 qkv, o, fc1, fc2; LNp ln1, ln2; Lin16 qkv_f, fc1_f; float *qkv_u = nullptr, *fc1_u = nullptr; };
+struct EncLayer {
+  Lin16 qkv, o, fc1, fc2;
+  LNp ln1, ln2;
+  Lin16 qkv_f, fc1_f;
+  float *qkv_u = nullptr, *fc1_u = nullptr;
+  Lin16 qkv_h;  // RoBERTa: the fused QKV with rows interleaved per head, [q_h; k_h; v_h] (gemm.hip epi 3)
+};
 
 struct EffBlock {
   int expand, k, stride, cin, cout, cexp, csq, residual;
@@ -140,6 +146,7 @@ struct Options {
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
+  int qkv_attn = 1;     // RoBERTa L = 128: attention in the QKV GEMM's epilogue (gemm.hip epi 3)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
                         // GEMMs round to as many rounds as QKV: measured slower, off)
@@ -164,7 +171,7 @@ const OptName kOptNames[] = {
     {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
-    {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -303,7 +310,7 @@ int free_group(mmf_handle* h, int group) {
 // ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
 // GEMM launches are profiled per (tile instantiation, epilogue, activation) -- one kernel symbol
 // each, so the numbers line up with a rocprofv3 kernel trace of the same run.
-constexpr int kGemmActs = 5, kGemmEpis = 3;
+constexpr int kGemmActs = 5, kGemmEpis = 4;
 enum ProfKind {
   PK_GEMM0 = 0, PK_GEMM_LAST = kGemmConfigs * kGemmEpis * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
   PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_PW32, PK_COUNT
@@ -438,9 +445,10 @@ int fold_ln_named(mmf_handle* h, Lin16* dst, float** u, const std::string& lin, 
   GET(be, ln + ".bias", in);
   return fold_ln_lin(h, dst, u, w->f, b->f, out, in, g->f, be->f);
 }
-// fused QKV: rows [q; k; v] of [3*H][H] + bias; with ln (non-empty) also the LN-folded copy
+// fused QKV: rows [q; k; v] of [3*H][H] + bias; with ln (non-empty) also the LN-folded copy; with
+// heads also the per-head interleaved copy qkv_h (row 192 h + 64 part + d = row H part + 64 h + d)
 int load_qkv(mmf_handle* h, EncLayer* L, const std::string& q, const std::string& k, const std::string& v, int H,
-             const std::string& ln) {
+             const std::string& ln, bool heads = false) {
   Lin16* l = &L->qkv;
   std::vector<float> w((size_t)3 * H * H), b((size_t)3 * H);
   const std::string names[3] = {q, k, v};
@@ -454,6 +462,20 @@ int load_qkv(mmf_handle* h, EncLayer* L, const std::string& q, const std::string
   CHK(up_f32_padded(h, &l->b, b));
   l->out = 3 * H;
   l->in = H;
+  if (heads) {
+    std::vector<float> wh(w.size()), bh(b.size());
+    for (int hd = 0; hd < H / 64; ++hd)
+      for (int part = 0; part < 3; ++part)
+        for (int d = 0; d < 64; ++d) {
+          const size_t src = (size_t)part * H + hd * 64 + d, dst = (size_t)hd * 192 + part * 64 + d;
+          std::memcpy(wh.data() + dst * H, w.data() + src * H, sizeof(float) * H);
+          bh[dst] = b[src];
+        }
+    CHK(up_f16(h, &L->qkv_h.w, wh));
+    CHK(up_f32_padded(h, &L->qkv_h.b, bh));
+    L->qkv_h.out = 3 * H;
+    L->qkv_h.in = H;
+  }
   if (ln.empty()) return 0;
   GET(g, ln + ".weight", H);
   GET(be, ln + ".bias", H);
@@ -525,7 +547,8 @@ int finalize_text(mmf_handle* h) {
   for (int i = 0; i < 12; ++i) {
     const std::string l = p + "encoder.layer." + std::to_string(i) + ".";
     EncLayer& L = h->r_layers[i];
-    CHK(load_qkv(h, &L, l + "attention.self.query", l + "attention.self.key", l + "attention.self.value", 768, ""));
+    CHK(load_qkv(h, &L, l + "attention.self.query", l + "attention.self.key", l + "attention.self.value", 768, "",
+                 true));
     CHK(load_lin(h, &L.o, l + "attention.output.dense", 768, 768, true));
     CHK(load_ln(h, &L.ln1, l + "attention.output.LayerNorm", 768));
     CHK(load_lin(h, &L.fc1, l + "intermediate.dense", 3072, 768, true));
@@ -690,8 +713,11 @@ int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   g.max_grid = h->grid_cap;
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
-  ProfScope ps(h, s, (gemm_config(g) * kGemmEpis + g.epi) * kGemmActs + g.act, 2.0 * M * N * K,
-               2.0 * (M * K + N * K) + M * N * out_b);
+  // epi 3 also runs the attention of its rows (4 L^2 64 flops per sequence and head, L = 128) and
+  // writes ctx (N / 3 columns) instead of qkv
+  const double att = g.epi == 3 ? 4.0 * (M / 128) * (N / 192) * 128.0 * 128.0 * 64.0 : 0.0;
+  ProfScope ps(h, s, (gemm_config(g) * kGemmEpis + g.epi) * kGemmActs + g.act, 2.0 * M * N * K + att,
+               2.0 * (M * K + N * K) + M * (g.epi == 3 ? N / 3 : N) * out_b);
   HIPCHK(launch_gemm(g, s));
   return 0;
 }
@@ -820,6 +846,15 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       }
       ProfScope ps(h, s, PK_ATTN, 4.0 * B * 12 * (double)L * 64, (double)B * L * 768 * 2 * 2);
       HIPCHK(launch_attention_q1(qcls, 768, w.r_qkv, 2304, 768, 1536, mask, nullptr, w.r_ctx, L * 768, B, L, 12, s));
+    } else if (h->opt.qkv_attn && L == 128 && M > 512) {
+      // the attention of each (two sequences, head) tile inside the QKV GEMM's epilogue: ctx is
+      // written directly (bit-identical to the two launches below, tests/test_gpu_parity.py)
+      g = gemm_args(w.r_xb, 768, Ly.qkv_h, M);
+      g.epi = 3;
+      g.amask = mask;
+      g.c16 = w.r_ctx;
+      g.ldc = 768;
+      CHK(gemm(h, g, s));
     } else {
       // (M <= 512, a single text or a few: split-K through the workspace, gemm_splitk_factor)
       g = with_ws(gemm_args(w.r_xb, 768, Ly.qkv, M), w.sk_text, w.sk_elems);

@@ -263,6 +263,8 @@ __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
 // Two LDS stages: the next K-tile's DMA is in flight while the current one feeds the MFMAs.
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 template <int ROWS, int NW>
 MMF_DEV void glds_tile(const f16_t* __restrict__ G, int ld, int row0, int rowmax, int k0, f16_t* tile, int wave,
@@ -328,6 +330,120 @@ MMF_DEV void tile_coords(int t, int tilesM, int tilesN, int gm, int& tm, int& tn
 // the second K-step and combined into (mean, rstd) per row at the top of the third.
 constexpr int kLnPMax = 8;  // partials per row a reader accepts
 
+// Attention epilogue (EPI 3; RoBERTa layers with L = 128, option qkv_attn).  The tile is 256 rows =
+// two whole sequences x 192 columns = q | k | v of head tn (the QKV weight's rows interleaved per
+// head on the host).  Its values, rounded to fp16 exactly as the plain epilogue stores them, go to
+// LDS rows [key][64] in attention.hip's swizzle; then each of the 8 waves runs attention_kernel's
+// arithmetic (S^T = K Q^T, exp2-domain masked softmax, O^T = V^T P^T with V^T by transposed LDS
+// reads) for two 16-query tiles of one sequence and stores its ctx rows -- so ctx is bit-identical to
+// the QKV GEMM + attention_kernel<128> pair, without qkv's HBM round trip or the second launch.
+// win: 96 KB of LDS -- q of sequence s at win + 8192 s, k at win + 16384 + 16384 s, v 8192 after it.
+template <int MI, int NI>
+MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], const float4 (&bias_r)[NI], f16_t* win,
+                                float* kbias, int m0, int head, int M, int wm, int wn, int wave, int tid, int fr,
+                                int fg) {
+  constexpr int TM = MI * 16, TN = NI * 16;
+  f16_t* qs = win;
+  f16_t* kvs = win + 16384;
+#pragma unroll
+  for (int j = 0; j < MI; ++j) {
+    const int row = wm * TM + j * 16 + fr, sq = row >> 7, key = row & 127;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int c = wn * TN + i * 16 + fg * 4, part = c >> 6, d = c & 63;
+      const float4 bi = bias_r[i];
+      const uint2 pk = make_uint2(pack2h(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y),
+                                  pack2h(acc[i][j][2] + bi.z, acc[i][j][3] + bi.w));
+      f16_t* dst = part == 0 ? qs + sq * 8192 : kvs + sq * 16384 + (part - 1) * 8192;
+      *reinterpret_cast<uint2*>(dst + swz(key, d >> 3) + (d & 7)) = pk;
+    }
+  }
+  if (tid < 256) {  // key bias of the two sequences (rows past M: masked, their queries not stored)
+    const bool keep = m0 + tid < M && (!g.amask || g.amask[(size_t)m0 + tid] != 0);
+    kbias[tid] = keep ? 0.f : -INFINITY;
+  }
+  __syncthreads();
+  const int sq = wave >> 2, wq = wave & 3;
+  if (m0 + sq * 128 < M) {
+    const f16_t* Ks = kvs + sq * 16384;
+    const f16_t* Vs = Ks + 8192;
+    const f16_t* Qs = qs + sq * 8192;
+    const float* kb = kbias + sq * 128;
+    constexpr int NKT = 8;
+#pragma unroll 1
+    for (int it = 0; it < 2; ++it) {
+      const int qt = wq + 4 * it, qq = qt * 16 + fr;
+      f16x8 qf[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) qf[ks] = as_f16x8(*reinterpret_cast<const uint4*>(Qs + swz(qq, ks * 4 + fg)));
+      f32x4 sc[NKT];
+#pragma unroll
+      for (int j = 0; j < NKT; ++j) {
+        sc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const f16x8 kf = as_f16x8(*reinterpret_cast<const uint4*>(Ks + swz(j * 16 + fr, ks * 4 + fg)));
+          sc[j] = mfma16x16x32(kf, qf[ks], sc[j]);
+        }
+      }
+      constexpr float kScaleLog2e = 0.125f * 1.44269504088896341f;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NKT; ++j) {
+        const float4 kbv = *reinterpret_cast<const float4*>(kb + j * 16 + fg * 4);
+        const float kbr[4] = {kbv.x, kbv.y, kbv.z, kbv.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = fmaf(sc[j][r], kScaleLog2e, kbr[r]);
+          sc[j][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (mx == -INFINITY) mx = 0.f;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < NKT; ++j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(sc[j][r] - mx);
+          sc[j][r] = e;
+          sum += e;
+        }
+      }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+      f32x4 o[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kq = 0; kq < NKT / 2; ++kq) {
+        const uint4 pk = make_uint4(pack2h(sc[2 * kq][0], sc[2 * kq][1]), pack2h(sc[2 * kq][2], sc[2 * kq][3]),
+                                    pack2h(sc[2 * kq + 1][0], sc[2 * kq + 1][1]),
+                                    pack2h(sc[2 * kq + 1][2], sc[2 * kq + 1][3]));
+        const f16x8 pf = as_f16x8(pk);
+        const int key0 = kq * 32 + fg * 4 + (fr >> 2), p = fr & 3;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int c = dt * 2 + (p >> 1), e = (p & 1) * 4;
+          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + swz(key0, c) + e));
+          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + swz(key0 + 16, c) + e));
+          const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+          o[dt] = mfma16x16x32(as_f16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
+        }
+      }
+      f16_t* dst = g.c16 + (size_t)(m0 + sq * 128 + qq) * g.ldc + head * 64 + fg * 4;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *reinterpret_cast<uint2*>(dst + dt * 16) =
+            make_uint2(pack2h(o[dt][0] * inv, o[dt][1] * inv), pack2h(o[dt][2] * inv, o[dt][3] * inv));
+    }
+  }
+  __syncthreads();  // the window is the next tile's second-slab stage
+}
+
 #ifndef MMF_GLDS_BUF
 #define MMF_GLDS_BUF 1  // descriptor LDS-DMA fills for full panels (0: 64-bit-address fills everywhere; A/B builds)
 #endif
@@ -347,19 +463,25 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int STAGE = (BM + BN) * BK;
   static_assert(NW == 8 || NW == 4, "4 or 8 waves");
+  // EPI 3 (attention epilogue, RoBERTa QKV): a 40 KB gap between the two stages, so that the stage
+  // the last K-step freed plus the gap hold q (32 KB) and k | v (64 KB) of the tile's two sequences
+  constexpr bool ATT = EPI == 3;
+  static_assert(!ATT || (BM == 256 && BN == 192 && WGM == 4 && WGN == 2 && PIPE2), "attention epilogue: 256x192");
+  constexpr int XGAP = ATT ? 20480 : 0;  // f16 elements
+  constexpr int SOFF = STAGE + XGAP;     // stage 1's offset
   // 256x384 tiles (two stages = all 160 KB of LDS; 192 accumulator registers per lane): the bias
   // columns are fetched after the K loop and the residual rows without look-ahead, so that neither
   // is live beside the accumulators
   constexpr bool WIDE = BN == 384;
   static_assert(!WIDE || (EPI == 0 && !PIPE2), "256x384 tiles: plain epilogues, one-step K loop");
-  __shared__ __attribute__((aligned(16))) f16_t lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) f16_t lds[2 * STAGE + XGAP];
   constexpr bool ROWST = EPI == 1;  // reads row statistics
   static_assert(EPI == 0 || BM == 256, "lazy-LN epilogues assume 256-row tiles");
   __shared__ __attribute__((aligned(16))) float2 lds_rows[ROWST ? BM * kLnPMax : 2];
   // column vectors of a consumer tile: u | bias (bias through LDS frees the 4*NI bias registers the
   // plain path holds across the K loop)
   constexpr int kBiasCol = 256;
-  __shared__ __attribute__((aligned(16))) float lds_cols[ROWST ? 512 : 4];
+  __shared__ __attribute__((aligned(16))) float lds_cols[(ROWST || ATT) ? 512 : 4];  // (ATT: key mask bias)
   __shared__ __attribute__((aligned(16))) float2 lds_stat[ROWST ? BM : 2];  // (mean, rstd) per tile row
 
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -400,7 +522,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
     if constexpr (DBG == 2) return;
     int tm_, tn_;
     tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);
-    f16_t* nb = lds + buf * STAGE;
+    f16_t* nb = lds + buf * SOFF;
     if constexpr (WIDE) {
       if (tm_ * BM + BM <= M) {  // (N % 384 == 0: every column panel is full)
         glds_tile_buf<BM, NW>(ra, (uint32_t)g.lda * 2u, tm_ * BM, kt * BK, aoff, nb, wave);
@@ -517,7 +639,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
       }
       if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
       else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
-      const f16_t* Xs = lds + cur * STAGE;
+      const f16_t* Xs = lds + cur * SOFF;
       const f16_t* Ws = Xs + BM * BK;
       if constexpr (DBG == 1) {
       } else if constexpr (PIPE2) {
@@ -632,6 +754,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
     // fetched at tile start and residual rows are loaded one fragment row AHEAD of the stores (one
     // vmcnt counter covers loads and stores in issue order).
     // lazy LN: (mean, rstd) of fragment row j -> lds_stat[wm * TM + j * 16 + fr] (computed at kt = 2)
+    if constexpr (ATT) {
+      attention_epilogue(g, acc, bias_r, lds + ((cur ^ 1) ? SOFF + STAGE - 49152 : 0), lds_cols, m0, tn, M, wm, wn,
+                         wave, tid, fr, fg);
+      continue;
+    }
     if constexpr (EPI == 2) {
       // producer: out = acc + bias + residual, stored fp16 (in place over the residual is allowed:
       // each element is read before it is written, by one lane), then this wave's partial
@@ -828,6 +955,12 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   } else if (a.epi == 2) {
     MMF_EPI_CASE(2, ACT_NONE);
+  } else if (a.epi == 3) {
+    if constexpr (BN == 192) {
+      MMF_EPI_CASE(3, ACT_NONE);
+    } else {
+      return hipErrorInvalidValue;
+    }
   } else {
     return hipErrorInvalidValue;
   }
@@ -973,6 +1106,7 @@ int gemm_config(const GemmArgs& a) {
   // tower's N = 512, whose third 192-column tile is one-third empty.  Decided from N only, so a
   // row's statistics (and so its result) do not depend on the batch it runs in.
   if (a.epi == 2) return (a.prod256 && a.N % 256 == 0 && a.N / 64 <= kLnPMax) ? 11 : 10;
+  if (a.epi == 3) return 10;
   const int f = forced_config(a);
   if (a.epi == 1) return (f == 10 || f == 11) ? f : glds_pick(a, false);
   if (f >= 0) return f;
@@ -1004,6 +1138,9 @@ static bool epi_ok(const GemmArgs& a) {
     return a.ln_in && a.ln_u && a.bias && a.c16 && !a.c32 && !a.res16 && !a.res32 && a.ln_in_P >= 1 && a.ln_in_P <= kLnPMax &&
            a.ln_in_tn > 0 && (long)a.ln_in_P * a.ln_in_tn >= a.K;
   if (a.epi == 2) return a.c16 && !a.c32 && a.res16 && !a.res32 && a.ln_out && (a.N + 95) / 96 <= kLnPMax;
+  if (a.epi == 3)  // whole 128-row sequences, whole heads (192 = q | k | v columns of one head)
+    return a.c16 && !a.c32 && !a.res16 && !a.res32 && a.bias && a.act == ACT_NONE && a.N % 192 == 0 &&
+           a.M % 128 == 0 && a.ldc >= a.N / 3;
   return false;
 }
 

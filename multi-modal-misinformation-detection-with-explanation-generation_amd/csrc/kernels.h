@@ -43,6 +43,11 @@ struct GemmArgs {
   const float* ln_u;             // epi 1: [N] sum_k W[n][k] (padded to N + 256)
   float2* ln_out;                // epi 2: partials of the output rows, [rows][ceil(N / tn_out)]
   float ln_eps;
+  // epi 3 (RoBERTa, L = 128, option qkv_attn): W / bias are the fused QKV with rows interleaved per
+  // head ([q_h; k_h; v_h] = 192 rows for head h), so a 256 x 192 tile holds q, k and v of one head
+  // for two whole sequences; the epilogue runs their attention and writes ctx [M][ldc] (c16, head h
+  // at columns 64 h) instead of qkv.  amask: key-padding mask int32 [M / 128][128] (1 keep) or null
+  const int32_t* amask;
 };
 // epi 2: the column-block width (= P partials per row of ceil(N / tn)) launch_gemm will use
 int gemm_ln_tn(const GemmArgs& a);

@@ -408,3 +408,27 @@ def test_effnet_config3_batch512(det_sd, clip_sd):
         ref = torch.softmax(M.effnet_forward(sd, M.effnet_preprocess(torch.as_tensor(imgs[rows]))), 1)[:, 1].numpy()
     np.testing.assert_allclose(sc[rows], ref, atol=TOL)
     eng.close()
+
+
+@pytest.mark.parametrize("last_q1", [0, 1])
+@pytest.mark.parametrize("B,lengths", [(256, None), (37, [128, 97, 40, 5, 128, 64, 2])])
+def test_qkv_attention_epilogue_bit_identical(det_sd, B, lengths, last_q1):
+    """RoBERTa at L = 128: the attention run inside the QKV GEMM's epilogue (gemm.hip EPI 3, option
+    qkv_attn, head-interleaved QKV weight rows) against the QKV GEMM + attention_kernel<128> pair --
+    bit-identical heads, with padded keys, an odd batch (the last tile holds one sequence) and the
+    last layer both compact (last_q1) and full."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    eng = Engine(0, det_sd, None, max_batch=256)
+    ids, mask = syn.roberta_ids(B, 128, 11, lengths)
+    eng.set_option("last_q1", last_q1)
+    outs = {}
+    for qa in (0, 1):
+        eng.set_option("qkv_attn", qa)
+        res = eng.text_forward(ids, mask)
+        torch.cuda.synchronize()
+        outs[qa] = [t.clone() for t in res]
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()

@@ -37,7 +37,8 @@ def test_profile_kinds_cover_every_tile_option(det_sd, opts):
     # the B CLS rows; its K/V GEMM covers every row, its Q the CLS rows)
     flops = sum(r["flops_per_launch"] * r["launches_per_step"] for r in gemm)
     H, I, M = 768, 3072, B * L
-    full = 2.0 * M * H * (3 * H + H + 2 * I)
+    att = 4.0 * B * 12 * L * L * 64  # the QKV kind runs the attention in its epilogue (option qkv_attn)
+    full = 2.0 * M * H * (3 * H + H + 2 * I) + att
     q1 = 2.0 * M * H * 2 * H + 2.0 * B * H * (H + H + 2 * I)  # compact queries (option last_q1)
-    q_all = 2.0 * M * H * 3 * H + 2.0 * B * H * (H + 2 * I)   # split-stream checkpoints: full QKV
+    q_all = 2.0 * M * H * 3 * H + att + 2.0 * B * H * (H + 2 * I)  # split-stream checkpoints: full QKV
     assert any(flops == pytest.approx(11 * full + last, rel=0.02) for last in (q1, q_all)), flops
