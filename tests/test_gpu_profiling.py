@@ -11,7 +11,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("opts", [{}, {"gemm_wide": 1}, {"gemm_w4": 1}, {"gemm_wide": 1, "gemm_w4": 1}])
+# (the 256x384 tiles serve RoBERTa's plain QKV GEMM, which option qkv_attn replaces by the attention epilogue)
+@pytest.mark.parametrize("opts", [{}, {"gemm_wide": 1, "qkv_attn": 0}, {"gemm_w4": 1},
+                                  {"gemm_wide": 1, "gemm_w4": 1, "qkv_attn": 0}])
 def test_profile_kinds_cover_every_tile_option(det_sd, opts):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -37,7 +39,7 @@ def test_profile_kinds_cover_every_tile_option(det_sd, opts):
     # the B CLS rows; its K/V GEMM covers every row, its Q the CLS rows)
     flops = sum(r["flops_per_launch"] * r["launches_per_step"] for r in gemm)
     H, I, M = 768, 3072, B * L
-    att = 4.0 * B * 12 * L * L * 64  # the QKV kind runs the attention in its epilogue (option qkv_attn)
+    att = 4.0 * B * 12 * L * L * 64 if opts.get("qkv_attn", 1) else 0.0  # attention in the QKV epilogue
     full = 2.0 * M * H * (3 * H + H + 2 * I) + att
     q1 = 2.0 * M * H * 2 * H + 2.0 * B * H * (H + H + 2 * I)  # compact queries (option last_q1)
     q_all = 2.0 * M * H * 3 * H + att + 2.0 * B * H * (H + 2 * I)  # split-stream checkpoints: full QKV
