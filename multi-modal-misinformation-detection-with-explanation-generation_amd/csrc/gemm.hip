@@ -369,24 +369,29 @@ MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], c
     const f16_t* Vs = Ks + 8192;
     const f16_t* Qs = qs + sq * 8192;
     const float* kb = kbias + sq * 128;
-    constexpr int NKT = 8;
-#pragma unroll 1
-    for (int it = 0; it < 2; ++it) {
-      const int qt = wq + 4 * it, qq = qt * 16 + fr;
-      f16x8 qf[2];
+    constexpr int NKT = 8, NQ = 2;  // the wave's two 16-query tiles share every K / V fragment read
+    f16x8 qf[NQ][2];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) qf[ks] = as_f16x8(*reinterpret_cast<const uint4*>(Qs + swz(qq, ks * 4 + fg)));
-      f32x4 sc[NKT];
+    for (int it = 0; it < NQ; ++it)
 #pragma unroll
-      for (int j = 0; j < NKT; ++j) {
-        sc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < 2; ++ks)
+        qf[it][ks] = as_f16x8(*reinterpret_cast<const uint4*>(Qs + swz((wq + 4 * it) * 16 + fr, ks * 4 + fg)));
+    f32x4 sc[NQ][NKT];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const f16x8 kf = as_f16x8(*reinterpret_cast<const uint4*>(Ks + swz(j * 16 + fr, ks * 4 + fg)));
-          sc[j] = mfma16x16x32(kf, qf[ks], sc[j]);
-        }
+    for (int j = 0; j < NKT; ++j) {
+#pragma unroll
+      for (int it = 0; it < NQ; ++it) sc[it][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const f16x8 kf = as_f16x8(*reinterpret_cast<const uint4*>(Ks + swz(j * 16 + fr, ks * 4 + fg)));
+#pragma unroll
+        for (int it = 0; it < NQ; ++it) sc[it][j] = mfma16x16x32(kf, qf[it][ks], sc[it][j]);
       }
-      constexpr float kScaleLog2e = 0.125f * 1.44269504088896341f;
+    }
+    constexpr float kScaleLog2e = 0.125f * 1.44269504088896341f;
+    float inv[NQ];
+#pragma unroll
+    for (int it = 0; it < NQ; ++it) {
       float mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < NKT; ++j) {
@@ -394,8 +399,8 @@ MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], c
         const float kbr[4] = {kbv.x, kbv.y, kbv.z, kbv.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float v = fmaf(sc[j][r], kScaleLog2e, kbr[r]);
-          sc[j][r] = v;
+          const float v = fmaf(sc[it][j][r], kScaleLog2e, kbr[r]);
+          sc[it][j][r] = v;
           mx = fmaxf(mx, v);
         }
       }
@@ -407,38 +412,48 @@ MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], c
       for (int j = 0; j < NKT; ++j) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(sc[j][r] - mx);
-          sc[j][r] = e;
+          const float e = __builtin_amdgcn_exp2f(sc[it][j][r] - mx);
+          sc[it][j][r] = e;
           sum += e;
         }
       }
       sum += __shfl_xor(sum, 16, 64);
       sum += __shfl_xor(sum, 32, 64);
-      const float inv = sum > 0.f ? 1.0f / sum : 0.f;
-      f32x4 o[4];
+      inv[it] = sum > 0.f ? 1.0f / sum : 0.f;
+    }
+    f32x4 o[NQ][4];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < NQ; ++it)
 #pragma unroll
-      for (int kq = 0; kq < NKT / 2; ++kq) {
-        const uint4 pk = make_uint4(pack2h(sc[2 * kq][0], sc[2 * kq][1]), pack2h(sc[2 * kq][2], sc[2 * kq][3]),
-                                    pack2h(sc[2 * kq + 1][0], sc[2 * kq + 1][1]),
-                                    pack2h(sc[2 * kq + 1][2], sc[2 * kq + 1][3]));
-        const f16x8 pf = as_f16x8(pk);
-        const int key0 = kq * 32 + fg * 4 + (fr >> 2), p = fr & 3;
+      for (int dt = 0; dt < 4; ++dt) o[it][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const int c = dt * 2 + (p >> 1), e = (p & 1) * 4;
-          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + swz(key0, c) + e));
-          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + swz(key0 + 16, c) + e));
-          const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
-          o[dt] = mfma16x16x32(as_f16x8(make_uint4(l2.x, l2.y, h2.x, h2.y)), pf, o[dt]);
-        }
+    for (int kq = 0; kq < NKT / 2; ++kq) {
+      f16x8 pf[NQ];
+#pragma unroll
+      for (int it = 0; it < NQ; ++it)
+        pf[it] = as_f16x8(make_uint4(pack2h(sc[it][2 * kq][0], sc[it][2 * kq][1]),
+                                     pack2h(sc[it][2 * kq][2], sc[it][2 * kq][3]),
+                                     pack2h(sc[it][2 * kq + 1][0], sc[it][2 * kq + 1][1]),
+                                     pack2h(sc[it][2 * kq + 1][2], sc[it][2 * kq + 1][3])));
+      const int key0 = kq * 32 + fg * 4 + (fr >> 2), p = fr & 3;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int c = dt * 2 + (p >> 1), e = (p & 1) * 4;
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + swz(key0, c) + e));
+        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(Vs + swz(key0 + 16, c) + e));
+        const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+        const f16x8 vf = as_f16x8(make_uint4(l2.x, l2.y, h2.x, h2.y));
+#pragma unroll
+        for (int it = 0; it < NQ; ++it) o[it][dt] = mfma16x16x32(vf, pf[it], o[it][dt]);
       }
-      f16_t* dst = g.c16 + (size_t)(m0 + sq * 128 + qq) * g.ldc + head * 64 + fg * 4;
+    }
+#pragma unroll
+    for (int it = 0; it < NQ; ++it) {
+      f16_t* dst = g.c16 + (size_t)(m0 + sq * 128 + (wq + 4 * it) * 16 + fr) * g.ldc + head * 64 + fg * 4;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        *reinterpret_cast<uint2*>(dst + dt * 16) =
-            make_uint2(pack2h(o[dt][0] * inv, o[dt][1] * inv), pack2h(o[dt][2] * inv, o[dt][3] * inv));
+        *reinterpret_cast<uint2*>(dst + dt * 16) = make_uint2(pack2h(o[it][dt][0] * inv[it], o[it][dt][1] * inv[it]),
+                                                              pack2h(o[it][dt][2] * inv[it], o[it][dt][3] * inv[it]));
     }
   }
   __syncthreads();  // the window is the next tile's second-slab stage
