@@ -148,6 +148,7 @@ struct Options {
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
   int qkv_attn = 1;     // RoBERTa L = 128: attention in the QKV GEMM's epilogue (gemm.hip epi 3)
   int qkv_attn_gm = 0;  // its persistent tile order (gemm_group_m of those launches only; A/B)
+  int splitk_fix = 0;   // 1: split-K GEMMs reduced by the last-arriving slice (one launch; measured slower)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
                         // GEMMs round to as many rounds as QKV: measured slower, off)
@@ -173,7 +174,7 @@ const OptName kOptNames[] = {
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
-    {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"splitk_fix", &Options::splitk_fix, "MMF_SPLITK_FIX"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -704,15 +705,18 @@ GemmArgs gemm_args(const f16_t* A, int lda, const Lin16& l, int M) {
   return g;
 }
 
+// split-K workspace: `elems` floats of partial planes, then kSplitkCounters zeroed arrival counters
 GemmArgs with_ws(GemmArgs g, float* ws, size_t elems) {
   g.ws = ws;
   g.ws_elems = elems;
+  g.ws_cnt = ws ? reinterpret_cast<unsigned*>(ws + elems) : nullptr;
   return g;
 }
 
 int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   apply_options(h->opt, &g);
   if (g.epi == 3 && h->opt.qkv_attn_gm > 0) g.group_m = h->opt.qkv_attn_gm;
+  if (!h->opt.splitk_fix) g.ws_cnt = nullptr;
   g.max_grid = h->grid_cap;
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
@@ -1483,9 +1487,10 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   // max over the skinny-M GEMMs (compact last layers: B rows; whole encoders of small batches: up to
   // the 512 rows gemm_config sends to the split-K path) of (K / 256) * N = 9216 per row
   w.sk_elems = (size_t)std::max(B, 512) * 9216;
-  CHK(A((void**)&w.sk_text, w.sk_elems * 4));
-  CHK(A((void**)&w.sk_vit, w.sk_elems * 4));
-  CHK(A((void**)&w.sk_ctext, w.sk_elems * 4));
+  for (float** sk : {&w.sk_text, &w.sk_vit, &w.sk_ctext}) {  // + the arrival counters, zeroed once (each
+    CHK(A((void**)sk, w.sk_elems * 4 + kSplitkCounters * 4));  // launch's last arrivers reset theirs)
+    HIPCHK(hipMemset(*sk + w.sk_elems, 0, kSplitkCounters * 4));
+  }
   // EfficientNet activation sizes per image
   const EffSizes es = eff_sizes();
   const size_t max_io = es.io, max_exp = es.exp, max_dw = es.dw, max_pool = es.pool, max_c = 1280;

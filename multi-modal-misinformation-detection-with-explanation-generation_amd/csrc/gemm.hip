@@ -39,13 +39,98 @@ struct Cfg {
 
 MMF_DEV int swz(int row, int kc) { return row * BK + ((kc ^ (row & 7)) << 3); }
 
+// split-K in one launch (gemm_f16_kernel FIX).  Hand-off per cdna_hip_programming.md Guideline 16:
+// every partial is stored sc1 (write-through) and drained by its wave before the workgroup's barrier,
+// one lane then adds to the tile's agent-scope counter; the last arriver acquires and reads every
+// plane with sc1 loads.  The sum runs over slices 0..S-1 in order, then bias -> activation ->
+// residual, the operations of splitk_reduce_kernel in the same order (bit-identical results).
+typedef __attribute__((address_space(1))) unsigned gu32;
+template <int ACT>
+MMF_DEV void splitk_fin_rows(const GemmArgs& fin, rsrc_t rp, uint32_t plane, int S, int m0, int n0, int rows, int tid) {
+  const int M = fin.M, N = fin.N;
+  for (int e = tid; e < rows * 32; e += 256) {  // 32 float4 column groups per 128-column tile row
+    const int m = m0 + (e >> 5), n = n0 + (e & 31) * 4;
+    if (m >= M || n >= N) continue;
+    const uint32_t off = ((uint32_t)m * N + n) * 4u;
+    float4 acc;
+    {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 16);
+      acc = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+    }
+    for (int z = 1; z < S; ++z) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, off + (uint32_t)z * plane, 0, 16);
+      acc.x += __uint_as_float(v.x); acc.y += __uint_as_float(v.y);
+      acc.z += __uint_as_float(v.z); acc.w += __uint_as_float(v.w);
+    }
+    float v[4] = {acc.x, acc.y, acc.z, acc.w};
+    if (fin.bias) {
+      const float4 b = *reinterpret_cast<const float4*>(fin.bias + n);
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    if (ACT != ACT_NONE) act4<ACT>(v);
+    if (fin.res32) {
+      const float4 r = *reinterpret_cast<const float4*>(fin.res32 + (size_t)m * fin.ldr + n);
+      v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+    } else if (fin.res16) {
+      const uint2 r = *reinterpret_cast<const uint2*>(fin.res16 + (size_t)m * fin.ldr + n);
+      v[0] += lo_h(r.x); v[1] += hi_h(r.x); v[2] += lo_h(r.y); v[3] += hi_h(r.y);
+    }
+    if (fin.c32) *reinterpret_cast<float4*>(fin.c32 + (size_t)m * fin.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+    if (fin.c16)
+      *reinterpret_cast<uint2*>(fin.c16 + (size_t)m * fin.ldc + n) = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
+  }
+}
+template <int BM, int BN, int NI, int MI>
+MMF_DEV void splitk_fixup(const GemmArgs& g, const GemmArgs& fin, const f32x4 (&acc)[NI][MI], int tile, int m0, int n0,
+                          int rl, int cl, int tid) {
+  static_assert(BN == 128, "32 float4 groups per tile row");
+  const int S = gridDim.y, z = blockIdx.y, M = g.M, N = g.N;
+  const uint32_t plane = (uint32_t)M * N * 4u;
+  const rsrc_t rp = make_rsrc(fin.ws, plane * (uint32_t)S);
+#pragma unroll
+  for (int j = 0; j < MI; ++j)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int m = m0 + rl + j * 16, n = n0 + cl + i * 16;
+      const uint32_t off = (m < M && n < N) ? (uint32_t)z * plane + ((uint32_t)m * N + n) * 4u : kOOB;
+      const u32x4 w = {__float_as_uint(acc[i][j][0]), __float_as_uint(acc[i][j][1]), __float_as_uint(acc[i][j][2]),
+                       __float_as_uint(acc[i][j][3])};
+      __builtin_amdgcn_raw_buffer_store_b128(w, rp, off, 0, 16);  // sc1: write-through
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
+  __shared__ unsigned last;
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add((gu32*)(fin.ws_cnt + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)(S - 1);
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int rows = BM;
+  switch (fin.act) {
+    case ACT_GELU: splitk_fin_rows<ACT_GELU>(fin, rp, plane, S, m0, n0, rows, tid); break;
+    case ACT_QUICK_GELU: splitk_fin_rows<ACT_QUICK_GELU>(fin, rp, plane, S, m0, n0, rows, tid); break;
+    case ACT_SILU: splitk_fin_rows<ACT_SILU>(fin, rp, plane, S, m0, n0, rows, tid); break;
+    case ACT_RELU: splitk_fin_rows<ACT_RELU>(fin, rp, plane, S, m0, n0, rows, tid); break;
+    default: splitk_fin_rows<ACT_NONE>(fin, rp, plane, S, m0, n0, rows, tid); break;
+  }
+  if (tid == 0) __hip_atomic_store((gu32*)(fin.ws_cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // PF = 2: the global loads of K-step kt + 2 are issued at step kt into a second register set, so
 // two K-steps of compute cover each load's latency instead of one (long-K, few-workgroup launches:
 // the EfficientNet SE-scaled projects, M = B * 49 or B * 196 rows, K = 480 ... 1152)
 // ASC: the A operand carries an SE scale (g.ascale); instantiated apart so that plain launches keep
 // their register budget
-template <int BM, int BN, int WGM, int WGN, int PF = 1, bool ASC = false>
-__global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
+// FIX (split-K slices, grid.y = S): each slice stores its fp32 partial tile write-through (sc1), the
+// last slice of a tile to arrive (agent-scope counter in g.ws_cnt) sums the S partials in slice order
+// and applies fin's epilogue exactly as splitk_reduce_kernel does -- one launch instead of two
+template <int BM, int BN, int WGM, int WGN, int PF = 1, bool ASC = false, bool FIX = false>
+__global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN, GemmArgs fin) {
   using C = Cfg<BM, BN, WGM, WGN>;
   __shared__ __attribute__((aligned(16))) f16_t lds[2 * (BM + BN) * BK];
   auto Xs = [&](int buf) { return lds + buf * (BM + BN) * BK; };
@@ -185,6 +270,10 @@ __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
     }
   }
 
+  if constexpr (FIX) {
+    splitk_fixup<BM, BN>(g, fin, acc, wgid, m0, n0, wm * C::TM + fr, wn * C::TN + fg * 4, tid);
+    return;
+  }
   // epilogue: lane holds C[m][n..n+3].  All loads (bias, fp16 residual) are issued before the
   // first store and from clamped addresses (no divergent region around them): with one in-order
   // vmcnt a load issued after a store waits for that store, and a store's data VGPRs cannot be
@@ -992,11 +1081,11 @@ hipError_t run(const GemmArgs& a, hipStream_t s) {
   const dim3 grid(tilesM * tilesN);
   const bool pf2 = MMF_GEMM_PF2_K > 0 && a.K >= MMF_GEMM_PF2_K;
   if (a.ascale) {
-    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2, true>), grid, dim3(256), 0, s, a, tilesN);
-    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 1, true>), grid, dim3(256), 0, s, a, tilesN);
+    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2, true>), grid, dim3(256), 0, s, a, tilesN, a);
+    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 1, true>), grid, dim3(256), 0, s, a, tilesN, a);
   } else {
-    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2>), grid, dim3(256), 0, s, a, tilesN);
-    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), grid, dim3(256), 0, s, a, tilesN);
+    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2>), grid, dim3(256), 0, s, a, tilesN, a);
+    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), grid, dim3(256), 0, s, a, tilesN, a);
   }
   return hipGetLastError();
 }
@@ -1044,7 +1133,12 @@ hipError_t run_splitk(const GemmArgs& a, int S, hipStream_t s) {
   p.A = a.A; p.lda = a.lda; p.W = a.W; p.ldw = a.ldw;
   p.c32 = a.ws; p.ldc = a.N;
   p.M = a.M; p.N = a.N; p.K = a.K / S;
-  hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p, tilesN);
+  if (a.ws_cnt && tilesM * tilesN <= kSplitkCounters) {  // one launch: the last slice reduces (FIX)
+    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 1, false, true>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p,
+                       tilesN, a);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p, tilesN, a);
   const int threads = a.M * (a.N >> 2);
   const dim3 grid((threads + 255) / 256);
   switch (a.act) {

@@ -32,6 +32,8 @@ struct GemmArgs {
                                  //     partials fit (N % 256 == 0, N / 64 <= kLnPMax: CLIP text, N = 512)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
+  unsigned* ws_cnt;              // kSplitkCounters zeroed arrival counters next to ws (split-K reduced by
+                                 //     the last-arriving slice of each tile; null: a reduction kernel)
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
   // (mean_p, M2_p) over consecutive column blocks of tn columns ([rows][P] float2, buffers padded
   // to whole 256-row blocks), combined with Chan's formula by the reader.
@@ -54,6 +56,7 @@ int gemm_ln_tn(const GemmArgs& a);
 // split-K factor the skinny-M (M <= 512) GEMM path uses for this (K) -- independent of M, so
 // results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
 int gemm_splitk_factor(const GemmArgs& a);
+constexpr int kSplitkCounters = 1024;  // >= tiles of any split-K launch (64 x 128 tiles, M <= 512, N <= 3072)
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 // ring-pipelined 256x192 kernel (gemm_ring.hip): epi 0, fp16 output only, bias, no residual / A scale,
 // K % 64 == 0, N % 8 == 0

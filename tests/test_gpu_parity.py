@@ -432,3 +432,30 @@ def test_qkv_attention_epilogue_bit_identical(det_sd, B, lengths, last_q1):
         outs[qa] = [t.clone() for t in res]
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("B", [1, 3, 37, 256])
+def test_splitk_last_arriver_reduction_bit_identical(det_sd, clip_sd, B):
+    """Split-K GEMMs (skinny M: the compact last layers at every batch size, whole encoders at
+    B <= 4) reduced by the last-arriving slice of each tile (gemm.hip splitk_fixup: write-through
+    partials, agent-scope arrival counter, acquire) against the separate reduction kernel (option
+    splitk_fix = 0): bit-identical text heads and CLIP embeddings, repeated calls included (the
+    counters are reset by their last arrivers)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    eng = Engine(0, det_sd, clip_sd, max_batch=256)
+    rid, rm = syn.roberta_ids(B, 128, 21, [128, 77, 9, 128, 40])
+    cid, cm = syn.clip_ids(B, 77, 21, [77, 12, 40])
+    imgs = syn.images(B, 21)
+    outs = {}
+    for fix in (0, 1, 1):
+        eng.set_option("splitk_fix", fix)
+        res = list(eng.text_forward(rid, rm)) + [eng.clip_image(imgs), eng.clip_text(cid, cm)]
+        torch.cuda.synchronize()
+        outs.setdefault(fix, []).append([t.clone() for t in res])
+    ref = outs[0][0]
+    for run in outs[1]:
+        for a, b in zip(ref, run):
+            assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
