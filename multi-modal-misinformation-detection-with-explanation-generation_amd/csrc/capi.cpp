@@ -6,10 +6,14 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mmf_hip.h"
@@ -148,6 +152,7 @@ struct Options {
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
   int qkv_attn = 1;     // RoBERTa L = 128: attention in the QKV GEMM's epilogue (gemm.hip epi 3)
   int qkv_attn_gm = 0;  // its persistent tile order (gemm_group_m of those launches only; A/B)
+  int mt_enqueue = 64;  // batches of <= this many pairs: the towers enqueued by host threads side by side
   int splitk_fix = 0;   // 1: split-K GEMMs reduced by the last-arriving slice (one launch; measured slower)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
@@ -174,7 +179,8 @@ const OptName kOptNames[] = {
     {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
-    {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"splitk_fix", &Options::splitk_fix, "MMF_SPLITK_FIX"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"splitk_fix", &Options::splitk_fix, "MMF_SPLITK_FIX"},
+    {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -204,6 +210,72 @@ void apply_options(const Options& o, GemmArgs* g) {
 enum AllocGroup { AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_EFF32, AG_RESIZE, AG_COUNT };
 
 }  // namespace
+
+// Host threads that enqueue mmf_analyze_batch's towers side by side (option mt_enqueue).  A small
+// batch is host-enqueue bound: each tower is a chain of ~140 launches at ~2.3 us of host time each,
+// and enqueued one tower after another the last tower starts ~0.8 ms into the call.  Each worker
+// owns one tower stream; HIP's current device is per thread, so every worker sets it once.
+struct EnqueuePool {
+  struct Slot {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<int()> job;
+    bool busy = false, quit = false;
+    int rc = 0;
+    std::string err;
+  };
+  Slot slots[3];
+  int device = 0;
+  bool started = false;
+  void start(int dev) {
+    device = dev;
+    for (Slot& sl : slots) sl.th = std::thread([this, &sl] { loop(sl); });
+    started = true;
+  }
+  void loop(Slot& sl) {
+    (void)hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(sl.mu);
+    for (;;) {
+      sl.cv.wait(lk, [&] { return sl.busy || sl.quit; });
+      if (sl.quit) return;
+      lk.unlock();
+      const int rc = sl.job();
+      std::string e = rc ? g_err : std::string();  // (g_err is this worker's thread-local message)
+      lk.lock();
+      sl.rc = rc;
+      sl.err = e;
+      sl.busy = false;
+      sl.cv.notify_all();
+    }
+  }
+  void submit(int i, std::function<int()> f) {
+    Slot& sl = slots[i];
+    std::lock_guard<std::mutex> lk(sl.mu);
+    sl.job = std::move(f);
+    sl.busy = true;
+    sl.cv.notify_all();
+  }
+  int wait(int i, std::string* err) {
+    Slot& sl = slots[i];
+    std::unique_lock<std::mutex> lk(sl.mu);
+    sl.cv.wait(lk, [&] { return !sl.busy; });
+    if (sl.rc && err) *err = sl.err;
+    return sl.rc;
+  }
+  ~EnqueuePool() {
+    if (!started) return;
+    for (Slot& sl : slots) {
+      {
+        std::lock_guard<std::mutex> lk(sl.mu);
+        sl.quit = true;
+      }
+      sl.cv.notify_all();
+    }
+    for (Slot& sl : slots)
+      if (sl.th.joinable()) sl.th.join();
+  }
+};
 
 struct mmf_handle {
   int device = 0;
@@ -264,6 +336,7 @@ struct mmf_handle {
   hipEvent_t mjoin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int mtower_split = 0, mtower_layout = 0, ncu = 0;
   int grid_cap = 0;  // persistent-GEMM grid cap of the tower being enqueued (0 = all CUs)
+  std::unique_ptr<EnqueuePool> pool;  // option mt_enqueue (lazily started)
   // mmf_resize_pil workspaces (grow-only, group AG_RESIZE)
   struct ResizeWs {
     ResizeJob* jobs = nullptr;
@@ -274,6 +347,7 @@ struct mmf_handle {
   } rs;
 
   ~mmf_handle() {
+    pool.reset();  // workers joined before their streams go
     for (auto& g : groups)
       for (void* p : g) (void)hipFree(p);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
@@ -1604,8 +1678,21 @@ int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, 
     HIPCHK(hipStreamWaitEvent(h->tower[2], h->fork_ev, 0));
     st = h->tower[2];
   }
-  CHK(run_clip_text(h, ids, mask, B, L, te, st));
-  CHK(run_clip_image(h, img, B, ie, s));
+  if (concurrent && h->opt.mt_enqueue > 0 && B <= h->opt.mt_enqueue) {  // as in mmf_analyze_batch
+    if (!h->pool) {
+      h->pool.reset(new EnqueuePool());
+      h->pool->start(h->device);
+    }
+    h->pool->submit(1, [=] { return run_clip_text(h, ids, mask, B, L, te, st); });
+    const int rc = run_clip_image(h, img, B, ie, s);
+    std::string e;
+    const int wrc = h->pool->wait(1, &e);
+    CHK(rc);
+    if (wrc) return fail(wrc, "%s", e.c_str());
+  } else {
+    CHK(run_clip_text(h, ids, mask, B, L, te, st));
+    CHK(run_clip_image(h, img, B, ie, s));
+  }
   if (concurrent) {
     HIPCHK(hipEventRecord(h->join_ev[2], h->tower[2]));
     HIPCHK(hipStreamWaitEvent(s, h->join_ev[2], 0));
@@ -1727,10 +1814,38 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   // diag_skip (diagnostic only, never set by the API or bench.py): towers left out to measure each
   // tower's marginal cost in the concurrent step (bit 1 text, 2 EfficientNet, 4 CLIP text, 8 ViT)
   const int skip = h->opt.diag_skip;
-  if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
-  if (!(skip & 4)) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
-  if (!(skip & 2)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
-  if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
+  if (concurrent && h->opt.mt_enqueue > 0 && B <= h->opt.mt_enqueue) {
+    // small batches: three host threads enqueue the text, CLIP-text and EfficientNet towers while
+    // this thread enqueues the ViT, so every chain starts at once (each stream keeps its own order)
+    if (!h->pool) {
+      h->pool.reset(new EnqueuePool());
+      h->pool->start(h->device);
+    }
+    float* t_emb = w.t_emb;
+    const bool on[3] = {!(skip & 1), !(skip & 4), !(skip & 2)};
+    if (on[0]) h->pool->submit(0, [=] { return run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text); });
+    if (on[1]) h->pool->submit(1, [=] { return run_clip_text(h, clip_ids, clip_mask, B, Lc, t_emb, st_ctxt); });
+    if (on[2]) h->pool->submit(2, [=] { return run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff, 0); });
+    const int rc = (skip & 8) ? 0 : run_clip_image(h, img_clip, B, w.v_emb, s);
+    int wrc = 0;
+    std::string werr;
+    for (int i = 0; i < 3; ++i) {
+      if (!on[i]) continue;
+      std::string e;
+      const int r = h->pool->wait(i, &e);
+      if (r && !wrc) {
+        wrc = r;
+        werr = e;
+      }
+    }
+    CHK(rc);
+    if (wrc) return fail(wrc, "%s", werr.c_str());
+  } else {
+    if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
+    if (!(skip & 4)) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
+    if (!(skip & 2)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
+    if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
+  }
   if (concurrent) {
     for (int i = 0; i < 3; ++i) {
       HIPCHK(hipEventRecord(h->join_ev[i], h->tower[i]));

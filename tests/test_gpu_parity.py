@@ -459,3 +459,32 @@ def test_splitk_last_arriver_reduction_bit_identical(det_sd, clip_sd, B):
     for run in outs[1]:
         for a, b in zip(ref, run):
             assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("B", [1, 4, 8])
+def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
+    """Small batches with the towers enqueued by host threads side by side (option mt_enqueue:
+    three workers own the text, CLIP-text and EfficientNet streams, the caller's thread the ViT):
+    every output of analyze_batch and clip_consistency bit-identical to the one-thread enqueue, over
+    repeated calls."""
+    import mmf_amd.synthetic as syn
+    rid, rm = syn.roberta_ids(B, 128, 31, [128, 60, 7])
+    cid, cm = syn.clip_ids(B, 77, 31, [77, 20])
+    imgs = syn.images(B, 31)
+    def run():
+        out = {k: v.clone() for k, v in engine.analyze_batch(rid, rm, cid, cm, imgs).items()}
+        out.update({"cons_" + k: v.clone() for k, v in engine.clip_consistency(imgs, cid, cm).items()})
+        torch.cuda.synchronize()
+        return out
+
+    mt = engine.get_option("mt_enqueue")
+    try:
+        engine.set_option("mt_enqueue", 0)
+        ref = run()
+        engine.set_option("mt_enqueue", 8)
+        for _ in range(25):
+            out = run()
+            for k, v in ref.items():
+                assert torch.equal(v, out[k]), k
+    finally:
+        engine.set_option("mt_enqueue", mt)

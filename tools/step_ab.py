@@ -21,11 +21,12 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--what", choices=("step", "clip", "text"), default="step",
                     help="step: analyze_batch; clip: mmf_clip_consistency (configs[3]); text: configs[1]")
+    ap.add_argument("--batch", type=int, default=256, help="pairs per step (the bench workload: 256)")
     a = ap.parse_args()
     import bench
     import mmf_amd.weights as W
     from mmf_amd.engine import Engine
-    B = 256
+    B = a.batch
     eng = Engine(0, W.synthetic_detector_state(0), W.synthetic_clip_state(0), max_batch=B)
     t = bench.build_inputs(eng, B, 0)
     out = eng.alloc_outputs(B)
