@@ -4,6 +4,7 @@ streams only; all arithmetic runs in the HIP kernels of libmmf_hip.so)."""
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -313,8 +314,13 @@ class HostPipeline:
 
     _IN = ("rid", "rm", "cid", "cm", "img")
 
-    def __init__(self, eng: Engine, B: int, Lr: int, Lc: int = 77):
+    def __init__(self, eng: Engine, B: int, Lr: int, Lc: int = 77, d2h_stream: Optional[bool] = None):
         self.eng, self.B = eng, B
+        # result copies on a stream of their own (behind the batch's compute, beside the next batch's)
+        # instead of in the compute stream; MMF_D2H_STREAM=0 restores the in-stream copies (A/B)
+        if d2h_stream is None:
+            d2h_stream = os.environ.get("MMF_D2H_STREAM", "1") != "0"
+        self.d2h = torch.cuda.Stream(device=eng.device) if d2h_stream else None
         d = eng.device
         shapes = {"rid": ((B, Lr), torch.int32), "rm": ((B, Lr), torch.int32), "cid": ((B, Lc), torch.int32),
                   "cm": ((B, Lc), torch.int32), "img": ((B, 224, 224, 3), torch.uint8)}
@@ -346,9 +352,16 @@ class HostPipeline:
         sl = self.slots[k]
         self.eng.analyze_batch(sl["rid"], sl["rm"], sl["cid"], sl["cm"], sl["img"], out=self.outs[k])
         self.free[k].record(main)
-        for n, v in self.outs[k].items():
-            self.host_out[k][n].copy_(v, non_blocking=True)
-        self.done[k].record(main)
+        if self.d2h is not None:
+            with torch.cuda.stream(self.d2h):
+                self.d2h.wait_event(self.free[k])
+                for n, v in self.outs[k].items():
+                    self.host_out[k][n].copy_(v, non_blocking=True)
+                self.done[k].record(self.d2h)
+        else:
+            for n, v in self.outs[k].items():
+                self.host_out[k][n].copy_(v, non_blocking=True)
+            self.done[k].record(main)
         self.i += 1
         return k
 
