@@ -152,6 +152,7 @@ struct Options {
   int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
   int qkv_attn = 1;     // RoBERTa L = 128: attention in the QKV GEMM's epilogue (gemm.hip epi 3)
   int qkv_attn_gm = 0;  // its persistent tile order (gemm_group_m of those launches only; A/B)
+  int se_group = 0;     // EfficientNet SE: 8 = 8 images per block (se_group_kernel; measured slower), 0 = one
   int mt_enqueue = 64;  // batches of <= this many pairs: the towers enqueued by host threads side by side
   int splitk_fix = 0;   // 1: split-K GEMMs reduced by the last-arriving slice (one launch; measured slower)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
@@ -180,7 +181,7 @@ const OptName kOptNames[] = {
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
     {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"splitk_fix", &Options::splitk_fix, "MMF_SPLITK_FIX"},
-    {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"se_group", &Options::se_group, "MMF_SE_GROUP"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -1250,7 +1251,7 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
       const int nch = std::min(dwconv_nchunks(H, W, b.cexp, b.stride), Ho * Wo);
       HIPCHK(launch_sum32(e32_dw, B, Ho * Wo, b.cexp, nch, e_pool, s));
       HIPCHK(launch_se(e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, e_scale, B, b.cexp, b.csq, s,
-                       true));
+                       true, h->opt.se_group));
     }
     {
       ProfScope ps(h, s, PK_PW32, 2.0 * B * Ho * Wo * b.cexp * b.cout,
@@ -1332,7 +1333,8 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
                             h->opt.dw_ct | (h->opt.dw_persist ? 2 : 0) | (h->opt.dw_cw32 ? 8 : 0)));
     }
     ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, (double)B * b.cexp * 4 * (nch + 1));
-    HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s));
+    HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s,
+                     false, h->opt.se_group));
     GemmArgs g = gemm_args(w.e_dw, b.cexp, b.p, B * Ho * Wo);
     g.ascale = w.e_scale;
     g.rows_per_batch = Ho * Wo;

@@ -821,6 +821,125 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
   }
 }
 
+// Squeeze-excitation for G images per block (option se_group): the same per-image arithmetic as
+// se_kernel below, in the same order (bit-identical), but every fc1 / fc2 weight fetched from L2 once
+// per G images -- the late stages' 2 x 221 KB of fp32 weights made the one-image-per-block launch
+// L2-bound (113 MB of weight reads per 256 images).
+constexpr int SE_THREADS_G = 512;  // 8 waves: 256 registers for the G-image accumulators
+template <bool PRECISE, int G>
+__global__ __launch_bounds__(SE_THREADS_G) void se_group_kernel(const float* pool_part, int nchunks, float inv_hw,
+                                                                const float* w1, const float* b1, const float* w2t,
+                                                                const float* b2, float* scale, int B, int C, int Csq) {
+  __shared__ float pooled[G][1280];
+  __shared__ float s1[G][64];
+  const int b0 = blockIdx.x * G, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int idx = tid; idx < G * C; idx += SE_THREADS_G) {
+    const int g = idx / C, c = idx - g * C;
+    float v = 0.f;
+    if (b0 + g < B) {
+      const float* pp = pool_part + (size_t)(b0 + g) * nchunks * C;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int k = 0;
+      for (; k + 4 <= nchunks; k += 4) {
+        a0 += pp[(size_t)k * C + c];
+        a1 += pp[(size_t)(k + 1) * C + c];
+        a2 += pp[(size_t)(k + 2) * C + c];
+        a3 += pp[(size_t)(k + 3) * C + c];
+      }
+      for (; k < nchunks; ++k) a0 += pp[(size_t)k * C + c];
+      v = ((a0 + a1) + (a2 + a3)) * inv_hw;
+    }
+    pooled[g][c] = v;
+  }
+  __syncthreads();
+  {
+    constexpr int NWV = SE_THREADS_G / 64, OPW = 64 / NWV;  // outputs per wave (Csq <= 64)
+    float acc[OPW][G];
+#pragma unroll
+    for (int t = 0; t < OPW; ++t)
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[t][g] = 0.f;
+#pragma unroll
+    for (int t = 0; t < OPW; ++t) {
+      const int o = wave + NWV * t;
+      if (o < Csq) {
+        const float* wr = w1 + (size_t)o * C;
+        int c = lane;
+        for (; c + 192 < C; c += 256) {
+          const float w0 = wr[c], w1v = wr[c + 64], w2v = wr[c + 128], w3 = wr[c + 192];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            acc[t][g] = fmaf(w0, pooled[g][c], acc[t][g]);
+            acc[t][g] = fmaf(w1v, pooled[g][c + 64], acc[t][g]);
+            acc[t][g] = fmaf(w2v, pooled[g][c + 128], acc[t][g]);
+            acc[t][g] = fmaf(w3, pooled[g][c + 192], acc[t][g]);
+          }
+        }
+        for (; c < C; c += 64) {
+          const float wv = wr[c];
+#pragma unroll
+          for (int g = 0; g < G; ++g) acc[t][g] = fmaf(wv, pooled[g][c], acc[t][g]);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < OPW; ++t) {
+      const int o = wave + NWV * t;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float a = wave_sum(acc[t][g]);
+        if (o < Csq && lane == 0) s1[g][o] = PRECISE ? silu_precise(a + b1[o]) : act_apply(a + b1[o], ACT_SILU);
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += SE_THREADS_G) {
+    float a0[G], a1[G], a2[G], a3[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a0[g] = b2[c];
+      a1[g] = a2[g] = a3[g] = 0.f;
+    }
+    int j = 0;
+    for (; j + 16 <= Csq; j += 16) {
+      float wv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) wv[u] = w2t[(size_t)(j + u) * C + c];
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+          a0[g] = fmaf(wv[u], s1[g][j + u], a0[g]);
+          a1[g] = fmaf(wv[u + 1], s1[g][j + u + 1], a1[g]);
+          a2[g] = fmaf(wv[u + 2], s1[g][j + u + 2], a2[g]);
+          a3[g] = fmaf(wv[u + 3], s1[g][j + u + 3], a3[g]);
+        }
+    }
+    for (; j + 4 <= Csq; j += 4) {
+      const float w0 = w2t[(size_t)j * C + c], w1v = w2t[(size_t)(j + 1) * C + c];
+      const float w2v = w2t[(size_t)(j + 2) * C + c], w3 = w2t[(size_t)(j + 3) * C + c];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        a0[g] = fmaf(w0, s1[g][j], a0[g]);
+        a1[g] = fmaf(w1v, s1[g][j + 1], a1[g]);
+        a2[g] = fmaf(w2v, s1[g][j + 2], a2[g]);
+        a3[g] = fmaf(w3, s1[g][j + 3], a3[g]);
+      }
+    }
+    for (; j < Csq; ++j) {
+      const float wv = w2t[(size_t)j * C + c];
+#pragma unroll
+      for (int g = 0; g < G; ++g) a0[g] = fmaf(wv, s1[g][j], a0[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (b0 + g >= B) continue;
+      const float a = (a0[g] + a1[g]) + (a2[g] + a3[g]);
+      scale[(size_t)(b0 + g) * C + c] = 1.0f / (1.0f + expf(-a));
+    }
+  }
+}
+
 // Squeeze-excitation, one 1024-thread block per image.  The three phases are each a few dependent
 // L2 round trips, so the kernel is latency-bound: every phase keeps many independent loads in
 // flight (unrolled partial sums) instead of walking dependent chains.
@@ -1172,8 +1291,18 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
 
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s,
-                     bool precise) {
+                     bool precise, int group) {
   if (C > 1280 || Csq > 64) return hipErrorInvalidValue;
+  if (group == 8) {
+    const dim3 grid((B + 7) / 8);
+    if (precise)
+      hipLaunchKernelGGL((se_group_kernel<true, 8>), grid, dim3(SE_THREADS_G), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2,
+                         b2, scale, B, C, Csq);
+    else
+      hipLaunchKernelGGL((se_group_kernel<false, 8>), grid, dim3(SE_THREADS_G), 0, s, pool_part, nchunks, inv_hw, w1, b1,
+                         w2, b2, scale, B, C, Csq);
+    return hipGetLastError();
+  }
   if (precise)
     hipLaunchKernelGGL(se_kernel<true>, dim3(B), dim3(SE_THREADS), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2, b2,
                        scale, C, Csq);

@@ -163,7 +163,8 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
                          int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s,
-                     bool precise = false);  // precise: the fc1 SiLU in silu_precise form (fp32 tower)
+                     bool precise = false, int group = 0);  // precise: the fc1 SiLU in silu_precise form (fp32
+                                                             // tower); group 8: se_group_kernel (8 images a block)
 hipError_t launch_gap_classifier(const f16_t* x, int HW, int C, const float* w, const float* b, float* logits,
                                  float* score, int score_stride, int B, hipStream_t s);
 hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);

@@ -488,3 +488,28 @@ def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
                 assert torch.equal(v, out[k]), k
     finally:
         engine.set_option("mt_enqueue", mt)
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+@pytest.mark.parametrize("B", [13, 256])
+def test_se_image_groups_bit_identical(B, fp32):
+    """EfficientNet squeeze-excitation with 8 images per block (option se_group, every SE weight
+    fetched once per 8 images) against one image per block: the same per-image arithmetic in the
+    same order, so bit-identical logits -- a batch that is not a multiple of 8 included, fp16 and
+    fp32 towers."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    import mmf_amd.weights as W
+    from mmf_amd.engine import Engine
+    eng = Engine(0, W.synthetic_detector_state(0, effnet_gain=2 ** 0.5), None, max_batch=256)
+    eng.set_option("effnet_fp32", 1 if fp32 else 0)
+    imgs = syn.images(B, 41)
+    res = {}
+    for grp in (0, 8):
+        eng.set_option("se_group", grp)
+        lg, sc = eng.effnet_forward(imgs)
+        torch.cuda.synchronize()
+        res[grp] = (lg.clone(), sc.clone())
+    assert torch.equal(res[0][0], res[8][0]), (res[0][0] - res[8][0]).abs().max().item()
+    assert torch.equal(res[0][1], res[8][1])
