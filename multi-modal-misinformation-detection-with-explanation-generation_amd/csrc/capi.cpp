@@ -154,6 +154,7 @@ struct Options {
   int qkv_attn_gm = 0;  // its persistent tile order (gemm_group_m of those launches only; A/B)
   int se_group = 0;     // EfficientNet SE: 8 = 8 images per block (se_group_kernel; measured slower), 0 = one
   int mt_enqueue = 64;  // batches of <= this many pairs: the towers enqueued by host threads side by side
+  int splitk_min_k = 0; // skinny-M GEMMs split K only from this depth (0: from 512)
   int splitk_fix = 0;   // 1: split-K GEMMs reduced by the last-arriving slice (one launch; measured slower)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
@@ -181,6 +182,7 @@ const OptName kOptNames[] = {
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
     {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"splitk_fix", &Options::splitk_fix, "MMF_SPLITK_FIX"},
+    {"splitk_min_k", &Options::splitk_min_k, "MMF_SPLITK_MIN_K"},
     {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"se_group", &Options::se_group, "MMF_SE_GROUP"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
 Options& process_options() {
@@ -198,6 +200,7 @@ Options& process_options() {
 void apply_options(const Options& o, GemmArgs* g) {
   g->force_cfg = o.gemm_config >= 0 ? o.gemm_config + 1 : 0;
   g->no_splitk = o.gemm_splitk ? 0 : 1;
+  g->splitk_min_k = o.splitk_min_k;
   g->group_m = o.gemm_group_m;
   g->prio = o.gemm_prio;
   g->ring = o.gemm_ring;

@@ -1235,6 +1235,7 @@ int gemm_splitk_factor(const GemmArgs& a) {
   // and 16-B aligned rows for the reduction's float4 accesses
   if (a.ascale || (a.K % 256) || a.K < 512 || (a.N & 3) || (a.ldc & 3) || (a.ldr & 3)) return 1;
   if (a.no_splitk) return 1;  // handle option "gemm_splitk" = 0 (A/B tests)
+  if (a.splitk_min_k > 0 && a.K < a.splitk_min_k) return 1;  // option splitk_min_k (A/B)
   return a.K / 256;
 }
 

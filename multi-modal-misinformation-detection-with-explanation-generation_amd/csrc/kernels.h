@@ -21,6 +21,7 @@ struct GemmArgs {
   int M, N, K, act;
   int force_cfg;                 // 0 = automatic tile choice, c + 1 = instantiation c (A/B option)
   int no_splitk;                 // 1 = never split K on the skinny-M path (A/B option)
+  int splitk_min_k;              // skinny-M GEMMs split K only from this depth (0 = 512; a K-only rule)
   int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
   int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
   int ring;                      // 1 = plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
