@@ -307,7 +307,7 @@ class Engine:
 
 class HostPipeline:
     """analyze_batch over batches that start in HOST memory (the boundary of analyze_pairs and of a
-    serving loop): two device input slots, H2D copies of batch i+1 on a copy stream while batch i
+    serving loop): three device input slots (MMF_PIPE_SLOTS), H2D copies of batch i+1 on a copy stream while batch i
     computes on the current stream (ids int32 + uint8 images, ~38.6 MB per 256 pairs), results
     copied back into pinned host tensors.  Host inputs should be pinned (`torch.Tensor.pin_memory`)
     for the copies to run asynchronously."""
@@ -324,27 +324,32 @@ class HostPipeline:
         d = eng.device
         shapes = {"rid": ((B, Lr), torch.int32), "rm": ((B, Lr), torch.int32), "cid": ((B, Lc), torch.int32),
                   "cm": ((B, Lc), torch.int32), "img": ((B, 224, 224, 3), torch.uint8)}
-        self.slots = [{k: torch.empty(sh, dtype=dt, device=d) for k, (sh, dt) in shapes.items()} for _ in range(2)]
-        self.outs = [eng.alloc_outputs(B) for _ in range(2)]
+        # input/output slots = batches in flight (MMF_PIPE_SLOTS, default 3): the copy of batch i+1 beside
+        # the compute of batch i, and the host one more batch ahead.  With 2, a host hiccup longer than
+        # one batch's compute left the device idle: bench headline 18,365 -> 18,562 pairs/s (3
+        # interleaved processes), now level with the HBM-resident rate (profiles/r04_ab_pipe_slots.txt)
+        self.n = max(2, int(os.environ.get("MMF_PIPE_SLOTS", "3")))
+        self.slots = [{k: torch.empty(sh, dtype=dt, device=d) for k, (sh, dt) in shapes.items()} for _ in range(self.n)]
+        self.outs = [eng.alloc_outputs(B) for _ in range(self.n)]
         self.host_out = [{k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in o.items()}
                          for o in self.outs]
         self.copy_stream = torch.cuda.Stream(device=d)
-        self.ready = [torch.cuda.Event() for _ in range(2)]
-        self.free = [torch.cuda.Event() for _ in range(2)]
-        self.done = [torch.cuda.Event() for _ in range(2)]
+        self.ready = [torch.cuda.Event() for _ in range(self.n)]
+        self.free = [torch.cuda.Event() for _ in range(self.n)]
+        self.done = [torch.cuda.Event() for _ in range(self.n)]
         self.i = 0
 
     def submit(self, batch: Dict[str, torch.Tensor]) -> int:
         """Queue one host batch {rid, rm, cid, cm, img}; returns the slot whose results
         `result(slot)` returns once the batch has finished.  Never blocks on the device except
-        when the slot is still in use by the batch submitted two calls earlier."""
-        k = self.i & 1
+        when the slot is still in use by the batch submitted `n` calls earlier."""
+        k = self.i % self.n
         main = torch.cuda.current_stream(self.eng.device)
-        if self.i >= 2:
+        if self.i >= self.n:
             self.done[k].synchronize()  # the host copy of that slot's previous results is complete
         with torch.cuda.stream(self.copy_stream):
-            if self.i >= 2:
-                self.copy_stream.wait_event(self.free[k])  # compute of batch i-2 has read the slot
+            if self.i >= self.n:
+                self.copy_stream.wait_event(self.free[k])  # compute of batch i-n has read the slot
             for n in self._IN:
                 self.slots[k][n].copy_(batch[n], non_blocking=True)
             self.ready[k].record(self.copy_stream)

@@ -319,12 +319,13 @@ def test_long_text_up_to_512(det_sd, clip_sd):
 
 
 def test_host_pipeline_matches_device_batches(engine, golden_inputs):
-    """engine.HostPipeline (host inputs, double-buffered H2D on a copy stream) returns, per
-    submitted batch, exactly what analyze_batch returns for the same device-resident batch."""
+    """engine.HostPipeline (host inputs, H2D on a copy stream, three slots in flight) returns, per
+    submitted batch, exactly what analyze_batch returns for the same device-resident batch -- over
+    more batches than slots, so every slot is reused."""
     import mmf_amd.synthetic as syn
     B = 16
     batches = []
-    for seed in (5, 6, 7):
+    for seed in (5, 6, 7, 8, 9, 10, 11):
         rid, rm = syn.roberta_ids(B, 128, seed, [128, 70, 9])
         cid, cm = syn.clip_ids(B, 77, seed, [77, 30, 4])
         batches.append({"rid": torch.from_numpy(rid).pin_memory(), "rm": torch.from_numpy(rm).pin_memory(),
