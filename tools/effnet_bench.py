@@ -1,6 +1,6 @@
 """EfficientNet-B0 tower alone (B images, synthetic weights/inputs) for per-kernel profiling:
 
-    python tools/effnet_bench.py [--batch 256 --iters 10] [--ab dw_v2=0 dw_v2=1 --rounds 5]
+    python tools/effnet_bench.py [--batch 256 --iters 10] [--ab dw_v2=0 dw_v2=1 --rounds 5] [--opt effnet_chunks=1]
     rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES ... -- python tools/effnet_bench.py --iters 2
 """
 import argparse
@@ -19,11 +19,15 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--ab", nargs="*", default=[], help="interleaved option variants 'opt=v[,opt2=v]'")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--opt", nargs="*", default=[], help="handle options set before the run 'opt=v'")
     a = ap.parse_args()
     import mmf_amd.synthetic as syn
     import mmf_amd.weights as W
     from mmf_amd.engine import Engine
     eng = Engine(0, W.synthetic_detector_state(0), None, max_batch=a.batch)
+    for kv in a.opt:
+        k, x = kv.split("=", 1)
+        eng.set_option(k, int(x))
     img = torch.from_numpy(syn.images(a.batch, 3)).cuda()
     eng.effnet_forward(img)
     torch.cuda.synchronize()

@@ -38,6 +38,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--match", default="expand_dw,stem_dw,dwconv,se_kernel,pw_kernel,gemm_f16,gemm_glds,gap")
+    ap.add_argument("--images", type=int, default=0,
+                    help="images the profiled command pushed through the tower (all its forwards): prints MB/img")
     a = ap.parse_args()
     passes = [load(os.path.join(a.dir, f"p{i}", "run_counter_collection.csv")) for i in range(1, 5)]
     # per-dispatch means (a counter row is repeated per dimension instance: sum per dispatch first)
@@ -49,6 +51,11 @@ def main():
                 cnt[k][c] = vals
             durs[k] += dur[k]
     match = a.match.split(",")
+    if a.images:
+        tot = sum(2 * sum(cs.get("FETCH_SIZE", [])) + sum(cs.get("WRITE_SIZE", []))
+                  for k, cs in cnt.items() if any(m in k for m in match)) * 1024
+        print(f"# HBM bytes of every matching launch (FETCH_SIZE x2 + WRITE_SIZE) / {a.images} images: "
+              f"{tot / a.images / 1e6:.2f} MB per image")
     rows = []
     for k, cs in cnt.items():
         if not any(m in k for m in match):

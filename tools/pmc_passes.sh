@@ -18,6 +18,7 @@ i=0
 for P in "${PASSES[@]}"; do
   i=$((i + 1))
   echo "pass $i: $P" >> $OUT/passes.log
-  timeout -s KILL 120 rocprofv3 --pmc $P -f csv -d $OUT/p$i -o run -- "$@" > $OUT/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $P -f csv -d $OUT/p$i -o run -- "$@" > $OUT/p$i.log 2>&1 ||
+    { echo "pass $i failed: exit $?" >> $OUT/passes.log; exit 1; }
 done
 echo done >> $OUT/passes.log
