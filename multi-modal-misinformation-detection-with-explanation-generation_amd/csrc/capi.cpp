@@ -156,6 +156,7 @@ struct Options {
   int mt_enqueue = 64;  // batches of <= this many pairs: the towers enqueued by host threads side by side
   int splitk_min_k = 0; // skinny-M GEMMs split K only from this depth (0: from 512)
   int splitk_fix = 0;   // 1: split-K GEMMs reduced by the last-arriving slice (one launch; measured slower)
+  int gemm_tq = 0;      // 1: persistent GEMMs take their tiles after the first from per-XCD queues (gemm.hip; A/B)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
                         // GEMMs round to as many rounds as QKV: measured slower, off)
@@ -182,6 +183,7 @@ const OptName kOptNames[] = {
     {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
     {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"splitk_fix", &Options::splitk_fix, "MMF_SPLITK_FIX"},
+    {"gemm_tq", &Options::gemm_tq, "MMF_GEMM_TQ"},
     {"splitk_min_k", &Options::splitk_min_k, "MMF_SPLITK_MIN_K"},
     {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"se_group", &Options::se_group, "MMF_SE_GROUP"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
 };
@@ -341,6 +343,13 @@ struct mmf_handle {
   int mtower_split = 0, mtower_layout = 0, ncu = 0;
   int grid_cap = 0;  // persistent-GEMM grid cap of the tower being enqueued (0 = all CUs)
   std::unique_ptr<EnqueuePool> pool;  // option mt_enqueue (lazily started)
+  // option gemm_tq: kTileQueueWords zeroed words per stream that launches persistent GEMMs (zeroed
+  // at mmf_create; each launch's last workgroup zeroes its words again)
+  static constexpr int kTqSlots = 32;
+  unsigned* tq_words = nullptr;
+  hipStream_t tq_stream[kTqSlots] = {};
+  int tq_n = 0;
+  std::mutex tq_mu;
   // mmf_resize_pil workspaces (grow-only, group AG_RESIZE)
   struct ResizeWs {
     ResizeJob* jobs = nullptr;
@@ -364,6 +373,7 @@ struct mmf_handle {
       if (mjoin_ev[i]) (void)hipEventDestroy(mjoin_ev[i]);
     }
     if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (tq_words) (void)hipFree(tq_words);
   }
 };
 
@@ -791,8 +801,20 @@ GemmArgs with_ws(GemmArgs g, float* ws, size_t elems) {
   return g;
 }
 
+// the tile-queue words of stream s (launches on one stream run in order, so one set per stream);
+// null when every slot is taken (the launch then keeps the static schedule)
+unsigned* tile_queue(mmf_handle* h, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(h->tq_mu);
+  for (int i = 0; i < h->tq_n; ++i)
+    if (h->tq_stream[i] == s) return h->tq_words + i * kTileQueueWords;
+  if (h->tq_n == mmf_handle::kTqSlots) return nullptr;
+  h->tq_stream[h->tq_n] = s;
+  return h->tq_words + (h->tq_n++) * kTileQueueWords;
+}
+
 int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   apply_options(h->opt, &g);
+  if (h->opt.gemm_tq && h->tq_words) g.tq = tile_queue(h, s);
   if (g.epi == 3 && h->opt.qkv_attn_gm > 0) g.group_m = h->opt.qkv_attn_gm;
   if (!h->opt.splitk_fix) g.ws_cnt = nullptr;
   g.max_grid = h->grid_cap;
@@ -1456,6 +1478,16 @@ int mmf_create(int device, mmf_handle** out) {
   if (!h) return fail(MMF_ENOMEM, "out of host memory");
   h->device = device;
   h->opt = process_options();
+  {
+    const size_t bytes = sizeof(unsigned) * kTileQueueWords * mmf_handle::kTqSlots;
+    hipError_t e = hipMalloc(&h->tq_words, bytes);
+    if (e == hipSuccess) e = hipMemset(h->tq_words, 0, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      delete h;
+      return fail(MMF_ENOMEM, "tile-queue words: %s", hipGetErrorString(e));
+    }
+  }
   *out = h;
   g_err.clear();
   return 0;

@@ -554,7 +554,7 @@ MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], c
 
 // DBG (measurement builds, forced configs 15 / 16 only; outputs garbage): 1 = LDS-DMA + barriers only,
 // 2 = fragment reads + MFMAs + barriers only
-template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0>
+template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0, bool TQ = false>
 __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 : 2) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
                                                                      int gm) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
@@ -610,6 +610,27 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
 
   int t = wgid;
   if (t >= tiles) return;
+  // Tile queue (option gemm_tq; the launcher sets g.tq only when every workgroup has a first tile and
+  // nk >= 3).  The first tile is the static one; after it, each workgroup takes the next tile of its
+  // XCD's share of the static schedule from that XCD's counter.  Under a concurrent launch the
+  // workgroups that start late then take fewer tiles, rather than each running its fixed share
+  // behind the others.  The tile order within an XCD is the static one, so L2 locality is kept.
+  // Static index of XCD x's c-th tile: (c / qx) * nwg + xbase + c % qx.
+  // (instantiated apart: the queue's scalars cost the static kernels registers; 256x384 tiles have
+  // all 160 KB of LDS taken, so they stay static)
+  constexpr bool dyn = TQ && !WIDE;
+  const int qx = xcd < r ? q + 1 : q, xbase = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  // the ticket's LDS slots (two, by tile parity): lds_stat's two unused entries where no row statistics
+  // are kept (the 256x384 tiles have no other LDS byte free)
+  int* lds_tq;
+  if constexpr (ROWST) {
+    __shared__ int tq_own[2];
+    lds_tq = tq_own;
+  } else {
+    lds_tq = reinterpret_cast<int*>(lds_stat);
+  }
+  int par = 0, tnext = 0;
+  unsigned cq = 0;
   if ((g.prio == 1 && wave >= NW / 2) || (g.prio == 2 && wave < NW / 2)) __builtin_amdgcn_s_setprio(1);
   // descriptor fills (glds_tile_buf) for every full row / column panel whose operand's byte extent
   // fits 32 bits (WIDE: checked by the launcher): the per-lane source offset is one loop-invariant
@@ -666,7 +687,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
   stage(0, t, 0);
   __syncthreads();
   int cur = 0;
-  for (; t < tiles; t += nwg) {
+  for (; t < tiles; t = tnext, par ^= 1) {
+    tnext = t + nwg;
+    // one lane takes the queue's next ticket now; its return is first used at kt = 1, after the
+    // first K-step's barrier (vmcnt(0)) has waited for it anyway
+    if (dyn && tid == 0) cq = __hip_atomic_fetch_add((gu32*)(g.tq + xcd * kTqStride), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int tm, tn;
     tile_coords(t, tilesM, tilesN, gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
@@ -741,8 +766,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      if (kt + 1 < nk) stage(cur ^ 1, t, kt + 1);
-      else if (t + nwg < tiles) stage(cur ^ 1, t + nwg, 0);
+      if (dyn && kt == 1 && wave == 0) {  // (wave-uniform: no exec-masked region inside the K loop)
+        // the empty asm pins the ticket's first use here: without it hipcc hoists the readfirstlane
+        // to the atomic, and wave 0 waits out the atomic's round trip (vmcnt(0)) at every tile start
+        unsigned cv = cq;
+        asm volatile("" : "+v"(cv));
+        const unsigned c = (unsigned)qx + __builtin_amdgcn_readfirstlane(cv);
+        const int tq_ = (int)(c / (unsigned)qx) * nwg + xbase + (int)(c % (unsigned)qx);
+        lds_tq[par] = tq_ < tiles ? tq_ : tiles;
+      }
+      if (kt + 1 < nk) {
+        stage(cur ^ 1, t, kt + 1);
+      } else {
+        if (dyn) tnext = __builtin_amdgcn_readfirstlane(lds_tq[par]);  // written at kt = 1, barriers since
+        if (tnext < tiles) stage(cur ^ 1, tnext, 0);
+      }
       const f16_t* Xs = lds + cur * SOFF;
       const f16_t* Ws = Xs + BM * BK;
       if constexpr (DBG == 1) {
@@ -1002,6 +1040,25 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
     if (g.res32) epilogue(std::true_type{});
     else epilogue(std::false_type{});
   }
+  // tile queue: every workgroup has taken its last ticket; the last one to finish zeroes the words for
+  // the stream's next launch (kernel boundary: visible).  Relaxed is enough: a workgroup issues its
+  // finish add only after its last ticket's value has returned (the loop exit depends on it), so
+  // every ticket add has been performed when the finish count reaches nwg -- an acq_rel add would
+  // write back and invalidate the XCD's L2 in every workgroup.
+  if (dyn && tid == 0) {
+    const unsigned d = __hip_atomic_fetch_add((gu32*)(g.tq + 8 * kTqStride), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (unsigned)nwg - 1) {
+      for (int x = 0; x < 9; ++x) __hip_atomic_store((gu32*)(g.tq + x * kTqStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// the tile queue only where it can act: more tiles than workgroups (every workgroup then has a
+// static first tile) and K-steps enough for the ticket hand-off (written at kt = 1, read at nk - 1)
+static GemmArgs with_tile_queue(const GemmArgs& a, int tiles, int grid) {
+  GemmArgs b = a;
+  if (!(a.tq && tiles > grid && a.K / BK >= 3)) b.tq = nullptr;
+  return b;
 }
 
 template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false, int DBG = 0>
@@ -1013,13 +1070,21 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int grid = tiles < cap ? tiles : cap;
   const dim3 blk(64 * WGM * WGN);
   const int gm = a.group_m;  // tile-order option (handle option "gemm_group_m"; 0 = row-major)
+  const GemmArgs b = with_tile_queue(a, tiles, grid);
+  // queue instantiations: the pipelined production tiles without an activation (with GELU's epilogue
+  // the 256x256 kernel's queue variant spills ~20 VGPRs; those launches keep the static schedule)
+  constexpr bool kTq = PIPE2 && BN != 384 && DBG == 0;
 #define MMF_GLDS_CASE(ACT)                                                                                  \
   case ACT:                                                                                                 \
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, a, tilesN, tiles, tilesM, \
-                       gm);                                                                                      \
+    if (kTq && ACT == ACT_NONE && b.tq)                                                                     \
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG, kTq && ACT == ACT_NONE>), dim3(grid), blk, 0, s, \
+                         b, tilesN, tiles, tilesM, gm);                                                      \
+    else                                                                                                    \
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, b, tilesN, tiles, tilesM, \
+                         gm);                                                                                    \
     break;
   if constexpr (DBG != 0) {
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT_NONE, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, a, tilesN,
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT_NONE, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, b, tilesN,
                        tiles, tilesM, gm);
     return hipGetLastError();
   }
@@ -1045,9 +1110,14 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
   const int grid = tiles < cap ? tiles : cap;
   const dim3 blk(64 * WGM * WGN);
   const int gm = a.group_m;
+  const GemmArgs b = with_tile_queue(a, tiles, grid);
 #define MMF_EPI_CASE(EPI, ACT)                                                                                 \
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, true, EPI>), dim3(grid), blk, 0, s, a, tilesN, tiles, \
-                     tilesM, gm)
+  if (b.tq)                                                                                                    \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, true, EPI, 0, true>), dim3(grid), blk, 0, s, b, tilesN, \
+                       tiles, tilesM, gm);                                                                     \
+  else                                                                                                         \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, true, EPI>), dim3(grid), blk, 0, s, b, tilesN, tiles, \
+                       tilesM, gm)
   if (a.epi == 1) {
     switch (a.act) {
       case ACT_NONE: MMF_EPI_CASE(1, ACT_NONE); break;

@@ -35,6 +35,9 @@ struct GemmArgs {
   size_t ws_elems;               // its capacity in floats
   unsigned* ws_cnt;              // kSplitkCounters zeroed arrival counters next to ws (split-K reduced by
                                  //     the last-arriving slice of each tile; null: a reduction kernel)
+  unsigned* tq;                  // option gemm_tq: kTileQueueWords zeroed words private to the launch's
+                                 //     stream (per-XCD tile counters + a finish count; the launch's last
+                                 //     workgroup zeroes them again); null: the static persistent schedule
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
   // (mean_p, M2_p) over consecutive column blocks of tn columns ([rows][P] float2, buffers padded
   // to whole 256-row blocks), combined with Chan's formula by the reader.
@@ -57,6 +60,8 @@ int gemm_ln_tn(const GemmArgs& a);
 // split-K factor the skinny-M (M <= 512) GEMM path uses for this (K) -- independent of M, so
 // results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
 int gemm_splitk_factor(const GemmArgs& a);
+constexpr int kTqStride = 64;  // gemm_tq: one counter per 256-B line (same-line atomics serialise)
+constexpr int kTileQueueWords = 9 * kTqStride;  // gemm_tq words per stream: 8 XCD counters, the finish count
 constexpr int kSplitkCounters = 1024;  // >= tiles of any split-K launch (64 x 128 tiles, M <= 512, N <= 3072)
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 // ring-pipelined 256x192 kernel (gemm_ring.hip): epi 0, fp16 output only, bias, no residual / A scale,

@@ -491,6 +491,37 @@ def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
         engine.set_option("mt_enqueue", mt)
 
 
+@pytest.mark.parametrize("B", [37, 256])
+def test_tile_queue_bit_identical(engine, B):
+    """Persistent GEMMs that take their tiles after the first from per-XCD queues (option gemm_tq:
+    an agent-scope ticket per tile, the launch's last workgroup zeroes the words for the stream's
+    next launch) against the static schedule: the same tiles with the same arithmetic, so every
+    output of analyze_batch and clip_consistency is bit-identical, over repeated calls on the four
+    tower streams (a ticket word left non-zero would skip or repeat tiles in the next launch)."""
+    import mmf_amd.synthetic as syn
+    rid, rm = syn.roberta_ids(B, 128, 41, [128, 77, 9, 128, 40])
+    cid, cm = syn.clip_ids(B, 77, 41, [77, 12, 40])
+    imgs = syn.images(B, 41)
+
+    def run():
+        out = {k: v.clone() for k, v in engine.analyze_batch(rid, rm, cid, cm, imgs).items()}
+        out.update({"cons_" + k: v.clone() for k, v in engine.clip_consistency(imgs, cid, cm).items()})
+        torch.cuda.synchronize()
+        return out
+
+    tq = engine.get_option("gemm_tq")
+    try:
+        engine.set_option("gemm_tq", 0)
+        ref = run()
+        engine.set_option("gemm_tq", 1)
+        for _ in range(4):
+            out = run()
+            for k, v in ref.items():
+                assert torch.equal(v, out[k]), k
+    finally:
+        engine.set_option("gemm_tq", tq)
+
+
 @pytest.mark.parametrize("fp32", [False, True])
 @pytest.mark.parametrize("B", [13, 256])
 def test_se_image_groups_bit_identical(B, fp32):
