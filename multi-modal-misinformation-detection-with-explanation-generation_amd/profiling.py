@@ -60,12 +60,21 @@ def kind_symbol(kind: str) -> str:
         return kind
     dims = m.group(2).split(",")
     epi = m.group(4) or "0"
-    # (the last template argument is the measurement-build selector DBG, 0 in production)
+    # (then the measurement-build selector DBG, 0 in production, and TQ, the tile-queue variant of
+    # option gemm_tq, false by default)
     if m.group(1) == "glds":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi, '0'])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi, '0', 'false'])}>"
     if m.group(1) == "glds_pipe2":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi, '0'])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi, '0', 'false'])}>"
     return f"gemm_f16_kernel<{', '.join(dims)}, 1, false>"  # (PF, ASC: plain launches)
+
+
+def same_kernel(a: str, b: str) -> bool:
+    """Symbols equal up to gemm_glds_kernel's trailing TQ = false (summaries from before the
+    template argument existed print 8 arguments)."""
+    def norm(s):
+        return re.sub(r"^(gemm_glds_kernel<(?:[^,<>]+, ){7}[^,<>]+), false>$", r"\1>", s)
+    return norm(a) == norm(b)
 
 
 def pmc_traffic(symbol: str, path: str | None = None) -> float | None:
@@ -78,7 +87,7 @@ def pmc_traffic(symbol: str, path: str | None = None) -> float | None:
         except (OSError, ValueError):
             continue
         for row in d.get("all_kernels", []):
-            if row["kernel"] == symbol:
+            if same_kernel(row["kernel"], symbol):
                 return float(row["hbm_bytes_per_launch"])
     return None
 

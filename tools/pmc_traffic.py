@@ -15,6 +15,13 @@ import re
 from collections import defaultdict
 
 
+def same_kernel(a, b):
+    """Symbols equal up to gemm_glds_kernel's trailing TQ = false (as profiling.same_kernel)."""
+    def norm(s):
+        return re.sub(r"^(gemm_glds_kernel<(?:[^,<>]+, ){7}[^,<>]+), false>$", r"\1>", s)
+    return norm(a) == norm(b)
+
+
 def short(name):
     name = re.sub(r"\(anonymous namespace\)::", "", name)
     return re.sub(r"\(.*\)$", "", re.sub(r"^void ", "", name))
@@ -49,7 +56,7 @@ def main():
     for t in table[:25]:
         print(f"{t['kernel'][:48]:48s} {t['launches_per_step']:6.1f}/step  fetch {t['fetch_bytes_per_launch'] / 1e6:9.2f} MB"
               f"  write {t['write_bytes_per_launch'] / 1e6:9.2f} MB")
-    dom = next((t for t in table if t["kernel"] == a.symbol), None)
+    dom = next((t for t in table if same_kernel(t["kernel"], a.symbol)), None)
     if a.json and dom:
         json.dump({"symbol": a.symbol, "steps": steps, "hbm_bytes_per_launch": round(dom["hbm_bytes_per_launch"]),
                    "fetch_bytes_per_launch": round(dom["fetch_bytes_per_launch"]),
