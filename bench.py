@@ -45,6 +45,35 @@ EFFNET_FLOOR_BYTES_PER_IMG, EFFNET_WEIGHT_BYTES = 4.35e6, 8.0e6
 PEAK_TFLOPS, PEAK_GBS = 2500.0, 8000.0
 
 
+def encoder_gflop(L: int, H: int, I: int, heads: int, layers: int = 12, compact_last: bool = False,
+                  q1_last: bool = False) -> float:
+    """GFLOP of one sequence through a transformer encoder (2 flops per MAC; attention 4 L^2 d per
+    head).  compact_last: the last layer's out-proj / FFN run on the pooled row only; q1_last: its
+    QKV GEMM computes K / V of every row and Q of the pooled row, and its attention one query (the
+    device path's compact last layers, capi.cpp run_text / run_clip_encoder)."""
+    d = H // heads
+    qkv, o, ffn, att = 2 * L * H * 3 * H, 2 * L * H * H, 4 * L * H * I, 4 * heads * L * L * d
+    full = qkv + o + ffn + att
+    if not compact_last:
+        return layers * full / 1e9
+    if q1_last:
+        last = 2 * L * H * 2 * H + 2 * H * H + 4 * heads * L * d
+    else:
+        last = qkv + att
+    last += 2 * H * H + 4 * H * I  # out-proj + FFN of the pooled row
+    return ((layers - 1) * full + last) / 1e9
+
+
+# executed work per unit (VERDICT r4 item 5): what the kernels compute, with the compact last layers
+# (RoBERTa: K / V + one query in its last layer; CLIP towers: full last-layer attention, pooled-row
+# out-proj / FFN), against the algorithmic counts above, which price every layer in full
+GFLOP_EXEC_ROBERTA_L128 = round(encoder_gflop(128, 768, 3072, 12, compact_last=True, q1_last=True), 3)
+GFLOP_EXEC_VIT = round(2 * 49 * 3072 * 768 / 1e9 + encoder_gflop(50, 768, 3072, 12, compact_last=True), 3)
+GFLOP_EXEC_CLIP_TEXT_L77 = round(encoder_gflop(77, 512, 2048, 8, compact_last=True), 3)
+GFLOP_EXEC_EFFNET = 0.769
+GFLOP_EXEC_PER_PAIR = round(GFLOP_EXEC_ROBERTA_L128 + GFLOP_EXEC_VIT + GFLOP_EXEC_CLIP_TEXT_L77 + GFLOP_EXEC_EFFNET, 2)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,23 +175,29 @@ def config_lines(eng, t, steps, warmup, det):
         check(lib.mmf_text_forward(h, ptr(t["rid"]), ptr(t["rm"]), B, 128, ptr(ai), ptr(mi), ptr(sc), stream_ptr()))
     dt = benchrun.timed_steps(text, steps, warmup, None, sync)
     tf = B * GFLOP_ROBERTA_L128 * steps / dt / 1e3
+    tfx = B * GFLOP_EXEC_ROBERTA_L128 * steps / dt / 1e3
     out["roberta_text_b256"] = {
         "config": "BASELINE configs[1]: RoBERTa-base dual-head text-only forward, seq_len=128, batch=256",
         "value": round(B * steps / dt, 1), "unit": "texts/s", "ms_per_step": round(1000 * dt / steps, 3),
         "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tf / PEAK_TFLOPS, 4), "work": f"{GFLOP_ROBERTA_L128} GFLOP/text"}}
+                     "frac": round(tf / PEAK_TFLOPS, 4), "work": f"{GFLOP_ROBERTA_L128} GFLOP/text",
+                     "executed_achieved": round(tfx, 1), "executed_frac": round(tfx / PEAK_TFLOPS, 4),
+                     "executed_work": f"{GFLOP_EXEC_ROBERTA_L128} GFLOP/text (compact last layer)"}}
     # configs[3]: CLIP ViT-B/32 image + text towers + cosine, B=256
     cons = {"img_emb": torch.empty(B, 512, device=dev), "txt_emb": torch.empty(B, 512, device=dev),
             "sim": torch.empty(B, device=dev)}
     dt = benchrun.timed_steps(lambda: eng.clip_consistency(t["img"], t["cid"], t["cm"], out=cons), steps, warmup,
                               None, sync)
     tf = B * (GFLOP_VIT + GFLOP_CLIP_TEXT_L77) * steps / dt / 1e3
+    tfx = B * (GFLOP_EXEC_VIT + GFLOP_EXEC_CLIP_TEXT_L77) * steps / dt / 1e3
     out["clip_b256"] = {
         "config": "BASELINE configs[3]: CLIP ViT-B/32 image+text encoders + cosine similarity, batch=256",
         "value": round(B * steps / dt, 1), "unit": "image-text pairs/s", "ms_per_step": round(1000 * dt / steps, 3),
         "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(tf / PEAK_TFLOPS, 4),
-                     "work": f"{GFLOP_VIT} + {GFLOP_CLIP_TEXT_L77} GFLOP/pair (L=77 text)"}}
+                     "work": f"{GFLOP_VIT} + {GFLOP_CLIP_TEXT_L77} GFLOP/pair (L=77 text)",
+                     "executed_achieved": round(tfx, 1), "executed_frac": round(tfx / PEAK_TFLOPS, 4),
+                     "executed_work": f"{GFLOP_EXEC_VIT} + {GFLOP_EXEC_CLIP_TEXT_L77} GFLOP/pair (compact last layers)"}}
     # configs[2]: EfficientNet-B0, 224x224, B=512 (workspaces re-reserved for 512 rows)
     Be = 512
     eng.reserve(Be, 128, 77)
@@ -180,11 +215,12 @@ def config_lines(eng, t, steps, warmup, det):
                      "frac": round(gbs / PEAK_GBS, 4),
                      "work": "4.35 MB/img block-fused activation floor + 8 MB weights (0.769 GFLOP/img)"}}
     # the same workload on the fp32 tower (option effnet_fp32, the ill-conditioned-weights mode)
+    prev = eng.get_option("effnet_fp32")
     eng.set_option("effnet_fp32", 1)
     try:
         dt = benchrun.timed_steps(effnet, steps, warmup, None, sync)
     finally:
-        eng.set_option("effnet_fp32", 0)
+        eng.set_option("effnet_fp32", prev)
     out["effnet_fp32_b512"] = {
         "config": "configs[2] workload on the fp32-activation EfficientNet tower (option effnet_fp32)",
         "value": round(Be * steps / dt, 1), "unit": "images/s", "ms_per_step": round(1000 * dt / steps, 3)}
@@ -328,7 +364,11 @@ def main():
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = benchrun.init_dist(world, "gloo" if share else "nccl", dev)
+    # MMF_BENCH_FORCE_DIST=1: the process group even at world 1, so the one-GPU box exercises the
+    # RCCL branch of the timing (tests/test_gpu_rccl.py)
+    force_dist = os.environ.get("MMF_BENCH_FORCE_DIST") == "1"
+    backend = "gloo" if share else "nccl"
+    dist = benchrun.init_dist(world, backend, dev, force=force_dist)
     tdev = None if share else dev  # device of the max-over-ranks reduction (gloo: host)
 
     import mmf_amd.weights as W
@@ -381,13 +421,20 @@ def main():
         res = result_line(
             a, world, B, dt, value,
             "synthetic (seeded token ids, structured uint8 images, 2170-row vault); random-init weights",
-            config_extra=dict({"h2d_bytes_per_step_per_gpu": h2d},
+            config_extra=dict({"h2d_bytes_per_step_per_gpu": h2d,
+                               "timing_collective": (f"{'rccl' if backend == 'nccl' else backend}: barrier + "
+                                                     f"all_reduce(MAX) over {world} rank(s)" if dist else None)},
                               **({"rehearsal": f"{world} ranks sharing {torch.cuda.device_count()} GPU(s) over gloo "
                                                 "(MMF_BENCH_SHARE_GPU=1): a functional check, not a measurement"}
                                  if share else {})),
             hbm_resident={"value": round(hbm, 2), "unit": "pairs/s", "ms_per_step": round(1000 * dt_hbm / a.steps, 3),
                           "note": "same step with inputs already in HBM and results left on the device"},
             achieved_tflops_whole_path=round(value * GFLOP_PER_PAIR / 1e3, 1),
+            achieved_tflops_whole_path_executed=round(value * GFLOP_EXEC_PER_PAIR / 1e3, 1),
+            work_per_pair={"algorithmic_gflop": GFLOP_PER_PAIR, "executed_gflop": GFLOP_EXEC_PER_PAIR,
+                           "note": "algorithmic = every encoder layer in full (SURVEY.md §8d); executed = what "
+                                   "the kernels compute (compact last layers: pooled rows only after the "
+                                   "attention)"},
             roofline=roofline, configs=configs, per_sample=per_sample, cpu_baseline=cpu)
         print(json.dumps(res), flush=True)
     if dist:

@@ -190,7 +190,9 @@ class MultiModalMisinfoDetector(nn.Module):
             self._synced[c] = fp
             self._held[c] = [t.untyped_storage() for t in self._tensors[c]]
             self.uploads[c] += 1
-        return [c for c, _, _ in todo]
+        names = [c for c, _, _ in todo]
+        eng.calibrate(names)  # load-time precision selection of the re-packed towers
+        return names
 
     def sync_fusion(self, force: bool = False) -> None:
         """Re-upload fusion_layer to the device engine after it was trained / reloaded."""
@@ -336,9 +338,9 @@ class MisinfoForensics:
                  device: str = "cuda",
                  *, roberta_tokenizer=None, clip_processor=None, detector_state=None, clip_state=None,
                  synthetic_seed: Optional[int] = None, max_batch: int = 256, max_text_len: int = 128,
-                 effnet_precision: str = "fp16", verbose: bool = True):
-        if effnet_precision not in ("fp16", "fp32"):
-            raise ValueError(f"effnet_precision must be 'fp16' or 'fp32', got {effnet_precision!r}")
+                 effnet_precision: str = "auto", verbose: bool = True):
+        if effnet_precision not in Engine.EFFNET_PRECISIONS:
+            raise ValueError(f"effnet_precision must be one of {Engine.EFFNET_PRECISIONS}, got {effnet_precision!r}")
         self.device = _require_hip(device)
         self._verbose = verbose
         self._log(f"Using device: {self.device}")
@@ -393,11 +395,11 @@ class MisinfoForensics:
         self.detector.eval()
 
         self.clip_eos_token_id = clip_eos_token_id(clip_model_dir)
+        # effnet_precision "auto" (default): the fp32-activation tower is selected at
+        # every EfficientNet (re)load when the fp16 tower's deepfake_score moves by more than 5e-4 on
+        # the calibration images (Engine.check_effnet_precision); "fp16" / "fp32" pin the tower
         self.engine = Engine(self.device.index or 0, None, clip_state, eos_token_id=self.clip_eos_token_id,
-                             max_batch=max_batch, max_text_len=max_text_len)
-        # fp32 EfficientNet activations: for towers whose logits reach O(100), where
-        # fp16 storage rounding is amplified past the 1e-3 parity bar
-        self.engine.set_option("effnet_fp32", int(effnet_precision == "fp32"))
+                             max_batch=max_batch, max_text_len=max_text_len, effnet_precision=effnet_precision)
         self.detector.bind(self.engine)  # uploads RoBERTa + heads, EfficientNet, FusionJudge
         self.clip_state = clip_state
 
@@ -514,6 +516,8 @@ class MisinfoForensics:
         if key is not None and self._emb_cache is not None and self._emb_cache[0] == key:
             return self._emb_cache[1]
         emb = self.engine.clip_image(px[None])
+        if self.engine.clip_stream_overflow(emb):  # fp16 stream overflow: re-run on fp32 streams
+            emb = self.engine.clip_image(px[None])
         self._emb_cache = (key, emb)
         self.vit_passes += 1
         return emb
@@ -522,6 +526,9 @@ class MisinfoForensics:
         """misinfo_forensics.py:375-408."""
         ids, mask = self._clip_ids([text])
         t = self.engine.clip_text(ids, mask)
+        if self.engine.clip_stream_overflow(t):
+            self._emb_cache = None
+            t = self.engine.clip_text(ids, mask)
         i = self._image_emb(io_utils.to_pil(image_path))
         return {"clip_similarity": float((t * i).sum().item())}
 
@@ -534,6 +541,8 @@ class MisinfoForensics:
         if user_caption:
             ids, mask = self._clip_ids([user_caption], truncation=True)
             temb = self.engine.clip_text(ids, mask)
+            if self.engine.clip_stream_overflow(temb):
+                temb = self.engine.clip_text(ids, mask)
         k = len(range(len(self.vault_metadata))[-top_k:])  # np.argsort(s)[-top_k:] keeps this many rows
         if k == 0:
             raise IndexError("index 0 is out of bounds for axis 0 with size 0")  # top_similarities[0]
@@ -573,11 +582,16 @@ class MisinfoForensics:
         cap = self.engine.max_batch  # frames beyond the reserved batch run as further launches
         dsc = torch.cat([self.engine.effnet_forward(eff[i:i + cap])[1] for i in range(0, F, cap)])
         iemb = torch.cat([self.engine.clip_image(clp[i:i + cap]) for i in range(0, F, cap)])
+        if self.engine.clip_stream_overflow(iemb):
+            iemb = torch.cat([self.engine.clip_image(clp[i:i + cap]) for i in range(0, F, cap)])
         clip_mean = 0.0
         temb_vault = None
         if text:
             ids, mask = self._clip_ids([text])  # analyze_consistency: no truncation (Q8)
             temb = self.engine.clip_text(ids, mask)
+            if self.engine.clip_stream_overflow(temb):
+                temb = self.engine.clip_text(ids, mask)
+                iemb = torch.cat([self.engine.clip_image(clp[i:i + cap]) for i in range(0, F, cap)])
             # per-frame fp32 cosines (the reference's .item()), mean over python floats
             clip_mean = float(np.mean([float(v) for v in (iemb * temb).sum(1).cpu().numpy()]))
             tids, tmask = self._clip_ids([text], truncation=True)  # search_vault's caption
@@ -710,7 +724,12 @@ class MisinfoForensics:
                     fut = ex.submit(host_stage, *chunks[k + 1])
                 self._fit_text(rid.shape[1])
                 eff, clp = self._windows(*rgb)
-                res.extend(self.batch_to_dicts(self.analyze_batch(rid, rm, cid, cm, eff, clp)))
+                out = self.analyze_batch(rid, rm, cid, cm, eff, clp)
+                # clip_similarity is the cosine of the two CLIP embeddings: non-finite only when a
+                # stream overflowed fp16 (a zero vault row's NaN stays in top_sims)
+                if self.engine.clip_stream_overflow(out["scores"][:, 3]):
+                    out = self.analyze_batch(rid, rm, cid, cm, eff, clp)
+                res.extend(self.batch_to_dicts(out))
         return res
 
     def _windows(self, n: int, st, rest: List[int], rgb: List[np.ndarray]):
@@ -831,6 +850,9 @@ class CLIPSimilarityEngine:
             ids, mask = io_utils.pad_ids(seqs, self.model.eos_token_id)
             t = self.model.clip_text(ids, mask)
             i = self.model.clip_image(io_utils.clip_pixels(image)[None])
+            if self.model.clip_stream_overflow(t, i):  # fp16 stream overflow: re-run on fp32 streams
+                t = self.model.clip_text(ids, mask)
+                i = self.model.clip_image(io_utils.clip_pixels(image)[None])
             similarity = float((i * t).sum().item())
             label = "Match" if similarity >= self.threshold else "Mismatch"
             return similarity, label

@@ -107,11 +107,17 @@ def input_seed(rank: int) -> int:
     return INPUT_SEED + rank
 
 
-def init_dist(world: int, backend: str, device: Optional[torch.device] = None):
+def init_dist(world: int, backend: str, device: Optional[torch.device] = None, force: bool = False):
     """torch.distributed with `backend` ("nccl" = RCCL over xGMI on the GPU node, "gloo" in the CPU
-    tests) when world > 1, else None."""
-    if world <= 1:
+    tests) when world > 1, else None.  force: initialise it at world 1 too (MMF_BENCH_FORCE_DIST=1:
+    the one-GPU box runs the RCCL branch -- device_id binding, barrier, device all_reduce(MAX) --
+    that an 8-GPU SCALE run takes, tests/test_gpu_rccl.py)."""
+    if world <= 1 and not force:
         return None
+    for k, v in (("MASTER_ADDR", "127.0.0.1"), ("RANK", "0"), ("WORLD_SIZE", str(world))):
+        os.environ.setdefault(k, v)
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(free_port())
     import torch.distributed as dist
     if backend == "nccl":
         dist.init_process_group(backend, device_id=device)

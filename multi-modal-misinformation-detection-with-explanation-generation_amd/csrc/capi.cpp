@@ -130,62 +130,40 @@ struct Options {
   int concurrent = 1;   // towers of mmf_analyze_batch on concurrent streams
   int fuse_stem = 1;    // stem fused into the stage-1 depthwise conv
   int fuse_expand = 1;  // 1x1 expand fused into the depthwise conv (stages 2-4)
-  int dw_ct = 1;        // compile-time depthwise tile geometries
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
   int text_hilo = -1;   // RoBERTa residual stream as fp16 hi + fp16 lo (1), fp16 alone (0), or chosen at
                         // weight-load time from the LayerNorm parameters (-1, default: DESIGN §4)
-  int gemm_prio = 2;    // s_setprio 1 for waves 0-3 of the persistent GEMM (+0.4 % step; A/B)
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
   int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
-  int dw_v2 = 0;        // depthwise phases with one channel group per wave, weights in SGPRs (effnet.hip)
-  int gemm_ring = 0;    // plain fp16-output encoder GEMMs on the loader / consumer kernel (gemm_ring.hip)
   int pw32_mfma = 2;    // fp32 tower's 1x1 convs on the fp32-input MFMA (2: loads 3 K-chunks ahead, 1: one ahead)
                         // or the fp32-FMA VALU kernel (0) -- every mode bit-identical
-  int gemm_wide = 0;    // 256x384 tiles where they save a persistent round (gemm.hip glds_pick; step A/B: a tie)
-  int gemm_w4 = 0;      // 192-column GEMM picks on the 4-wave 256x192 tiles (config 21; A/B)
-  int dw_persist = 0;   // persistent depthwise kernels with the next tile's loads in flight (effnet.hip; A/B: slower)
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
-  int ln_prod256 = 0;   // CLIP-text lazy-LN producers on 256x256 tiles (gemm.hip gemm_config; A/B)
   int qkv_attn = 1;     // RoBERTa L = 128: attention in the QKV GEMM's epilogue (gemm.hip epi 3)
-  int qkv_attn_gm = 0;  // its persistent tile order (gemm_group_m of those launches only; A/B)
-  int se_group = 0;     // EfficientNet SE: 8 = 8 images per block (se_group_kernel; measured slower), 0 = one
   int mt_enqueue = 64;  // batches of <= this many pairs: the towers enqueued by host threads side by side
-  int splitk_min_k = 0; // skinny-M GEMMs split K only from this depth (0: from 512)
-  int splitk_fix = 0;   // 1: split-K GEMMs reduced by the last-arriving slice (one launch; measured slower)
-  int gemm_tq = 0;      // 1: persistent GEMMs take their tiles after the first from per-XCD queues (gemm.hip; A/B)
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
                         // GEMMs round to as many rounds as QKV: measured slower, off)
   int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
-  int fuse_expand32 = 0;  // fp32 tower: expand + depthwise fused for the <= 40-channel inputs (bit-identical;
-                          // measured 11.82 -> 13.79 ms per 512 images: kept off)
-  int cu_split = 0;     // > 0: EfficientNet on that many CUs, the encoders on the rest (CU-masked streams; A/B)
-  int cu_split_layout = 0;  // which mask bits: 0 = the n lowest, 1 = n / 8 from each 32-bit word (one per XCD
-                            // if the driver maps bit words to XCDs), 2 = bits i with i % 8 < ... (see ensure_masked_towers)
 };
+// (Round 5 removed the options whose variants were measured slower and stayed off: gemm_ring, gemm_wide,
+// gemm_w4, dw_v2, dw_persist, ln_prod256, cu_split, fuse_expand32, qkv_attn_gm, splitk_fix, gemm_tq,
+// se_group, splitk_min_k, and pinned gemm_prio = 2 / dw_ct = 1; DESIGN.md §3 keeps each measurement.)
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
-    {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"}, {"dw_ct", &Options::dw_ct, "MMF_DW_CT"},
+    {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
-    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_prio", &Options::gemm_prio, "MMF_GEMM_PRIO"},
+    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
-    {"dw_v2", &Options::dw_v2, "MMF_DW_V2"},            {"gemm_ring", &Options::gemm_ring, "MMF_GEMM_RING"},
-    {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},     {"gemm_wide", &Options::gemm_wide, "MMF_GEMM_WIDE"},
-    {"gemm_w4", &Options::gemm_w4, "MMF_GEMM_W4"},
-    {"dw_persist", &Options::dw_persist, "MMF_DW_PERSIST"}, {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"},
-    {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},     {"ln_prod256", &Options::ln_prod256, "MMF_LN_PROD256"},
-    {"cu_split", &Options::cu_split, "MMF_CU_SPLIT"},  {"fuse_expand32", &Options::fuse_expand32, "MMF_FUSE_EXPAND32"},
+    {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},
+    {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"}, {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
-    {"qkv_attn_gm", &Options::qkv_attn_gm, "MMF_QKV_ATTN_GM"}, {"splitk_fix", &Options::splitk_fix, "MMF_SPLITK_FIX"},
-    {"gemm_tq", &Options::gemm_tq, "MMF_GEMM_TQ"},
-    {"splitk_min_k", &Options::splitk_min_k, "MMF_SPLITK_MIN_K"},
-    {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"se_group", &Options::se_group, "MMF_SE_GROUP"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},  {"cu_split_layout", &Options::cu_split_layout, "MMF_CU_SPLIT_LAYOUT"},
+    {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -202,13 +180,7 @@ Options& process_options() {
 void apply_options(const Options& o, GemmArgs* g) {
   g->force_cfg = o.gemm_config >= 0 ? o.gemm_config + 1 : 0;
   g->no_splitk = o.gemm_splitk ? 0 : 1;
-  g->splitk_min_k = o.splitk_min_k;
   g->group_m = o.gemm_group_m;
-  g->prio = o.gemm_prio;
-  g->ring = o.gemm_ring;
-  g->wide = o.gemm_wide;
-  g->w4 = o.gemm_w4;
-  g->prod256 = o.ln_prod256;
 }
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the
@@ -336,20 +308,11 @@ struct mmf_handle {
   // fork/join streams of mmf_analyze_batch (text, effnet, clip-text towers beside the caller's)
   hipStream_t tower[3] = {nullptr, nullptr, nullptr};
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
-  // option cu_split = n > 0: CU-masked tower streams -- EfficientNet on n CUs, the three encoders
-  // (text, CLIP text, ViT) on the other CUs (mtower: text, effnet, clip-text, vit)
-  hipStream_t mtower[4] = {nullptr, nullptr, nullptr, nullptr};
-  hipEvent_t mjoin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  int mtower_split = 0, mtower_layout = 0, ncu = 0;
-  int grid_cap = 0;  // persistent-GEMM grid cap of the tower being enqueued (0 = all CUs)
-  std::unique_ptr<EnqueuePool> pool;  // option mt_enqueue (lazily started)
-  // option gemm_tq: kTileQueueWords zeroed words per stream that launches persistent GEMMs (zeroed
-  // at mmf_create; each launch's last workgroup zeroes its words again)
-  static constexpr int kTqSlots = 32;
-  unsigned* tq_words = nullptr;
-  hipStream_t tq_stream[kTqSlots] = {};
-  int tq_n = 0;
-  std::mutex tq_mu;
+  // option mt_enqueue (lazily started).  Invariant: while the workers enqueue, no tower writes to the
+  // handle -- every per-launch choice is read from `opt` (set between calls, never during one) and
+  // every workspace is reserved before the call (mmf_reserve); the towers' launch sequences only read
+  // the handle and enqueue on their own streams.
+  std::unique_ptr<EnqueuePool> pool;
   // mmf_resize_pil workspaces (grow-only, group AG_RESIZE)
   struct ResizeWs {
     ResizeJob* jobs = nullptr;
@@ -368,12 +331,7 @@ struct mmf_handle {
       if (tower[i]) (void)hipStreamDestroy(tower[i]);
       if (join_ev[i]) (void)hipEventDestroy(join_ev[i]);
     }
-    for (int i = 0; i < 4; ++i) {
-      if (mtower[i]) (void)hipStreamDestroy(mtower[i]);
-      if (mjoin_ev[i]) (void)hipEventDestroy(mjoin_ev[i]);
-    }
     if (fork_ev) (void)hipEventDestroy(fork_ev);
-    if (tq_words) (void)hipFree(tq_words);
   }
 };
 
@@ -793,31 +751,15 @@ GemmArgs gemm_args(const f16_t* A, int lda, const Lin16& l, int M) {
   return g;
 }
 
-// split-K workspace: `elems` floats of partial planes, then kSplitkCounters zeroed arrival counters
+// split-K workspace: `elems` floats of partial planes
 GemmArgs with_ws(GemmArgs g, float* ws, size_t elems) {
   g.ws = ws;
   g.ws_elems = elems;
-  g.ws_cnt = ws ? reinterpret_cast<unsigned*>(ws + elems) : nullptr;
   return g;
-}
-
-// the tile-queue words of stream s (launches on one stream run in order, so one set per stream);
-// null when every slot is taken (the launch then keeps the static schedule)
-unsigned* tile_queue(mmf_handle* h, hipStream_t s) {
-  std::lock_guard<std::mutex> lk(h->tq_mu);
-  for (int i = 0; i < h->tq_n; ++i)
-    if (h->tq_stream[i] == s) return h->tq_words + i * kTileQueueWords;
-  if (h->tq_n == mmf_handle::kTqSlots) return nullptr;
-  h->tq_stream[h->tq_n] = s;
-  return h->tq_words + (h->tq_n++) * kTileQueueWords;
 }
 
 int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   apply_options(h->opt, &g);
-  if (h->opt.gemm_tq && h->tq_words) g.tq = tile_queue(h, s);
-  if (g.epi == 3 && h->opt.qkv_attn_gm > 0) g.group_m = h->opt.qkv_attn_gm;
-  if (!h->opt.splitk_fix) g.ws_cnt = nullptr;
-  g.max_grid = h->grid_cap;
   const double M = g.M, N = g.N, K = g.K;
   const double out_b = (g.c32 ? 4.0 : 0.0) + (g.c16 ? 2.0 : 0.0) + (g.res32 ? 4.0 : 0.0) + (g.res16 ? 2.0 : 0.0);
   // epi 3 also runs the attention of its rows (4 L^2 64 flops per sequence and head, L = 128) and
@@ -1250,23 +1192,13 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
   for (const EffBlock& b : h->e_blocks) {
     const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
     const float* src = cur;
-    bool fused = false;
-    if (b.expand != 1 && h->opt.fuse_expand32) {
-      ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k + 2.0 * B * H * W * b.cin * b.cexp,
-                   4.0 * B * ((double)H * W * b.cin + (double)Ho * Wo * b.cexp));
-      const hipError_t e = launch_expand_dw32(cur, b.e.w32, b.e.b, b.wd_t, b.bd, e32_dw, B, H, W, b.cin, b.cexp, b.k,
-                                              b.stride, s);
-      if (e != hipErrorNotSupported) HIPCHK(e);
-      fused = e == hipSuccess;
-    }
-    if (fused) {
-    } else if (b.expand != 1) {
+    if (b.expand != 1) {
       ProfScope ps(h, s, PK_PW32, 2.0 * B * H * W * b.cin * b.cexp, 4.0 * B * H * W * (b.cin + b.cexp));
       HIPCHK(launch_pw32(cur, b.e.w32, b.e.b, nullptr, 1, nullptr, e32_exp, B * H * W, b.cexp, b.cin, 3 /* SiLU */, s,
                              h->opt.pw32_mfma));
       src = e32_exp;
     }
-    if (!fused) {
+    {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k, 4.0 * B * b.cexp * ((double)H * W + Ho * Wo));
       HIPCHK(launch_dw32(src, b.wd_t, b.bd, e32_dw, B, H, W, b.cexp, b.k, b.stride, s));
     }
@@ -1276,7 +1208,7 @@ int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, fl
       const int nch = std::min(dwconv_nchunks(H, W, b.cexp, b.stride), Ho * Wo);
       HIPCHK(launch_sum32(e32_dw, B, Ho * Wo, b.cexp, nch, e_pool, s));
       HIPCHK(launch_se(e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, e_scale, B, b.cexp, b.csq, s,
-                       true, h->opt.se_group));
+                       true));
     }
     {
       ProfScope ps(h, s, PK_PW32, 2.0 * B * Ho * Wo * b.cexp * b.cout,
@@ -1338,12 +1270,12 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
       // stem output recomputed per 18x18 halo tile: 1.27x the stem MACs, image patch read once
       ProfScope ps(h, s, PK_DW, 2.0 * B * 112 * 112 * 32 * (9 + 27 * 1.27),
                    (double)B * (224 * 224 * 3 * 1.34 + 112 * 112 * 32 * 2));
-      HIPCHK(launch_effnet_stem_dw(img, xf32, h->e_stem_w, h->e_stem_b, b.wd, h->opt.dw_v2 ? b.wd_t : nullptr, b.bd, w.e_dw, w.e_pool, B, &nch, s));
+      HIPCHK(launch_effnet_stem_dw(img, xf32, h->e_stem_w, h->e_stem_b, b.wd, b.bd, w.e_dw, w.e_pool, B, &nch, s));
     } else if (fuse) {
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k + 2.0 * B * H * W * b.cin * b.cexp,
                    (double)B * 2 * ((double)H * W * b.cin * (b.cexp / 48) + (double)Ho * Wo * b.cexp));
       HIPCHK(launch_expand_dw(cur, b.cin, b.e.w, b.e.b, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride,
-                              &nch, s, h->opt.dw_ct));
+                              &nch, s));
     } else if (b.expand != 1) {
       GemmArgs g = gemm_args(cur, b.cin, b.e, B * H * W);
       g.act = 3;  // SiLU
@@ -1355,11 +1287,10 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
       ProfScope ps(h, s, PK_DW, 2.0 * B * Ho * Wo * b.cexp * b.k * b.k,
                    (double)B * b.cexp * 2 * ((double)H * W + (double)Ho * Wo));
       HIPCHK(launch_dwconv(src, b.wd, b.bd, w.e_dw, w.e_pool, B, H, W, b.cexp, b.k, b.stride, &nch, s,
-                            h->opt.dw_ct | (h->opt.dw_persist ? 2 : 0) | (h->opt.dw_cw32 ? 8 : 0)));
+                            1 | (h->opt.dw_cw32 ? 8 : 0)));
     }
     ProfScope ps(h, s, PK_SE, 4.0 * B * b.cexp * b.csq, (double)B * b.cexp * 4 * (nch + 1));
-    HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s,
-                     false, h->opt.se_group));
+    HIPCHK(launch_se(w.e_pool, nch, 1.0f / (float)(Ho * Wo), b.w1, b.b1, b.w2, b.b2, w.e_scale, B, b.cexp, b.csq, s));
     GemmArgs g = gemm_args(w.e_dw, b.cexp, b.p, B * Ho * Wo);
     g.ascale = w.e_scale;
     g.rows_per_batch = Ho * Wo;
@@ -1389,40 +1320,6 @@ int ensure_towers(mmf_handle* h) {
     HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
   }
   HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-  return 0;
-}
-
-// CU-masked tower streams (option cu_split = n): EfficientNet's stream may run on n CUs, the three
-// encoder streams on the remaining ones, so the latency-bound EfficientNet kernels keep a fixed CU
-// slice for the whole step instead of queueing behind the encoders' persistent GEMMs (which then
-// size their grids to the encoders' CUs).  Mask bit i is CU i; the driver interleaves the bits
-// over the 8 XCDs (bit i -> XCD i % 8), so a run of low bits is an even share of every XCD.
-int ensure_masked_towers(mmf_handle* h, int n) {
-  const int layout = h->opt.cu_split_layout;
-  if (h->mtower_split == n && h->mtower_layout == layout && h->mtower[0]) return 0;
-  if (!h->ncu) HIPCHK(hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-  if (n <= 0 || n >= h->ncu) return fail(MMF_EINVAL, "cu_split %d outside 1..%d", n, h->ncu - 1);
-  for (int i = 0; i < 4; ++i) {
-    if (h->mtower[i]) HIPCHK(hipStreamDestroy(h->mtower[i]));
-    h->mtower[i] = nullptr;
-    if (!h->mjoin_ev[i]) HIPCHK(hipEventCreateWithFlags(&h->mjoin_ev[i], hipEventDisableTiming));
-  }
-  if (!h->fork_ev) HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-  const int words = (h->ncu + 31) / 32;
-  std::vector<uint32_t> eff(words, 0u), enc(words, 0u);
-  // layout 0: bits [0, n); 1: the first n / 32 * ... of every 32-bit word (n / (ncu / 32) per word);
-  // 2: every (ncu / n)-th bit
-  const int words32 = h->ncu / 32;
-  for (int c = 0; c < h->ncu; ++c) {
-    bool e = c < n;
-    if (layout == 1) e = (c & 31) < n / (words32 ? words32 : 1);
-    if (layout == 2) e = (c % (h->ncu / n)) == 0 && c / (h->ncu / n) < n;
-    (e ? eff : enc)[c >> 5] |= 1u << (c & 31);
-  }
-  for (int i = 0; i < 4; ++i)
-    HIPCHK(hipExtStreamCreateWithCUMask(&h->mtower[i], (uint32_t)words, i == 1 ? eff.data() : enc.data()));  // size in 32-bit words
-  h->mtower_split = n;
-  h->mtower_layout = layout;
   return 0;
 }
 
@@ -1478,16 +1375,6 @@ int mmf_create(int device, mmf_handle** out) {
   if (!h) return fail(MMF_ENOMEM, "out of host memory");
   h->device = device;
   h->opt = process_options();
-  {
-    const size_t bytes = sizeof(unsigned) * kTileQueueWords * mmf_handle::kTqSlots;
-    hipError_t e = hipMalloc(&h->tq_words, bytes);
-    if (e == hipSuccess) e = hipMemset(h->tq_words, 0, bytes);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-      delete h;
-      return fail(MMF_ENOMEM, "tile-queue words: %s", hipGetErrorString(e));
-    }
-  }
   *out = h;
   g_err.clear();
   return 0;
@@ -1598,10 +1485,7 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   // max over the skinny-M GEMMs (compact last layers: B rows; whole encoders of small batches: up to
   // the 512 rows gemm_config sends to the split-K path) of (K / 256) * N = 9216 per row
   w.sk_elems = (size_t)std::max(B, 512) * 9216;
-  for (float** sk : {&w.sk_text, &w.sk_vit, &w.sk_ctext}) {  // + the arrival counters, zeroed once (each
-    CHK(A((void**)sk, w.sk_elems * 4 + kSplitkCounters * 4));  // launch's last arrivers reset theirs)
-    HIPCHK(hipMemset(*sk + w.sk_elems, 0, kSplitkCounters * 4));
-  }
+  for (float** sk : {&w.sk_text, &w.sk_vit, &w.sk_ctext}) CHK(A((void**)sk, w.sk_elems * 4));
   // EfficientNet activation sizes per image
   const EffSizes es = eff_sizes();
   const size_t max_io = es.io, max_exp = es.exp, max_dw = es.dw, max_pool = es.pool, max_c = 1280;
@@ -1818,26 +1702,6 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   Workspace& w = h->ws;
   // the per-kernel profiling pass runs the towers sequentially so event intervals are clean
   const int concurrent = h->opt.concurrent && !h->prof;
-  if (concurrent && h->opt.cu_split > 0) {
-    // CU-split fork: four masked streams; the caller's stream only forks and joins
-    CHK(ensure_masked_towers(h, h->opt.cu_split));
-    HIPCHK(hipEventRecord(h->fork_ev, s));
-    for (int i = 0; i < 4; ++i) HIPCHK(hipStreamWaitEvent(h->mtower[i], h->fork_ev, 0));
-    const int enc = h->ncu - h->opt.cu_split;
-    h->grid_cap = enc;
-    int rc = run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, h->mtower[0]);
-    if (!rc) rc = run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, h->mtower[2]);
-    if (!rc) rc = run_clip_image(h, img_clip, B, w.v_emb, h->mtower[3]);
-    h->grid_cap = h->opt.cu_split;
-    if (!rc) rc = run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, h->mtower[1]);
-    h->grid_cap = 0;
-    CHK(rc);
-    for (int i = 0; i < 4; ++i) {
-      HIPCHK(hipEventRecord(h->mjoin_ev[i], h->mtower[i]));
-      HIPCHK(hipStreamWaitEvent(s, h->mjoin_ev[i], 0));
-    }
-    return analyze_tail(h, B, scores5, text_sim, probs2, verdict, conf, rule, top_sims, top_idx, s);
-  }
   if (concurrent) CHK(ensure_towers(h));
   // fork: the four towers only share read-only inputs and write disjoint workspaces/outputs
   hipStream_t st_text = s, st_eff = s, st_ctxt = s;

@@ -393,74 +393,6 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
   EST_END()
 }
 
-// Persistent form of dwconv_kernel's compile-time geometries (option dw_persist, default): a block
-// keeps one channel group (blockIdx.y) and walks the (tile, image) items blockIdx.x, + gridDim.x, ...
-// Its weights are staged once, and the NEXT item's input tile (+halo) is loaded into registers right
-// after the current one is in LDS, so its HBM latency runs under the current item's taps, stores and
-// pool reduction instead of at the head of every block (stamps: 30-57 % of a one-shot block's life).
-// Out-of-image pixels read 0 through the buffer descriptor (no divergent region around the loads).
-// Same per-(image, tile, channel) pool partials and outputs as dwconv_kernel, bit for bit.
-template <int K, int S, int TT, int CWT, int R>
-__global__ __launch_bounds__(256, 3) void dwconv_persist_kernel(const f16_t* __restrict__ in, const float* __restrict__ w,
-                                                             const float* __restrict__ bias, f16_t* __restrict__ out,
-                                                             float* __restrict__ pool_part, int H, int W, int C,
-                                                             int tiles_x, int ntiles, int nitems) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
-  constexpr int PAD = (K - 1) / 2, CW = CWT, NG = CW / 8, IT = (TT - 1) * S + K;
-  constexpr int NL = (IT * IT * NG + 255) / 256, NW = (K * K * CW + 255) / 256;
-  const int tid = threadIdx.x, c0 = blockIdx.y * CW;
-  const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
-  f16_t* tile = (f16_t*)dw_smem;                              // [IT][IT][CW]
-  float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, true));  // [K*K][CW]
-  float* sb = sw + K * K * CW;                                  // [CW]
-  float* red = (float*)dw_smem;                                 // pool slots alias the tile
-  int item = blockIdx.x;
-  if (item >= nitems) return;  // (block-uniform)
-  EST_BEGIN(8 + ((K == 5) * 2 + (S == 2)) * 4 + (TT == 14 ? 1 : TT == 7 ? 2 : TT == 16 ? 3 : 0))
-  const rsrc_t rin = make_rsrc(in, (uint32_t)((size_t)(nitems / ntiles) * H * W * C * 2));
-  uint4 v[NL];
-  auto load_item = [&](int it) {
-    const int bi = it / ntiles, t = it - bi * ntiles;
-    const int ty0 = t / tiles_x, tx0 = t - ty0 * tiles_x;
-    const int iy0 = ty0 * TT * S - PAD, ix0 = tx0 * TT * S - PAD;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int idx = tid + i * 256, g = idx % NG, pix = idx / NG;
-      const int ty = pix / IT, tx = pix - ty * IT, iy = iy0 + ty, ix = ix0 + tx;
-      const bool ok = idx < IT * IT * NG && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                 rin, ok ? (uint32_t)((((size_t)bi * H + iy) * W + ix) * C + c0 + g * 8) * 2u : kOOB, 0, 0));
-    }
-  };
-  load_item(item);
-  {
-    float wv[NW];
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      const int i = tid + j * 256, t = i / CW, c = i - t * CW;
-      wv[j] = i < K * K * CW ? w[(size_t)(c0 + c) * K * K + t] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < NW; ++j)
-      if (tid + j * 256 < K * K * CW) sw[tid + j * 256] = wv[j];
-    if (tid < CW) sb[tid] = bias[c0 + tid];
-  }
-  for (; item < nitems; item += gridDim.x) {
-    const int bi = item / ntiles, t = item - bi * ntiles;
-    const int ty0 = t / tiles_x, tx0 = t - ty0 * tiles_x;
-#pragma unroll
-    for (int i = 0; i < NL; ++i)
-      if (tid + i * 256 < IT * IT * NG) *reinterpret_cast<uint4*>(tile + (size_t)(tid + i * 256) * 8) = v[i];
-    __syncthreads();
-    EST()
-    if (item + (int)gridDim.x < nitems) load_item(item + gridDim.x);
-    dw_compute_ct<K, S, TT, CW, R>(tile, sw, sb, red, out, pool_part, bi, c0, ty0 * TT, tx0 * TT, Ho, Wo, C, t, ntiles);
-    __syncthreads();  // the reduction has read `red` (aliasing the tile) before the next item's tile
-    EST()
-  }
-  EST_END()
-}
-
 // MBConv front, fused: 1x1 expand (BN folded) + SiLU computed per input tile on the MFMA, straight
 // into the depthwise conv's LDS tile, then the depthwise conv of dwconv_kernel.  The expanded
 // activation (6x the block's input channels, the largest tensor of the block) never touches HBM:
@@ -629,25 +561,16 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : 3) void expand_dw_ke
 // grid (49, 1, B); block 256
 constexpr int SD_T = 16, SD_IT = 18, SD_PR = 2 * SD_IT + 1, SD_PW = SD_PR * 3;
 
-//
-// V2 (option dw_v2, default): each wave owns one 8-channel group of the 32 -- wave-uniform, so the
-// depthwise weights (tap-major copy) and bias arrive by scalar loads into SGPRs and no LDS cycle is
-// spent on weights; the stem tile is stored channel-group-planar [4][18][SD2_ITP][8] with a row
-// pitch of 21 pixels, so the 16 lanes of every ds_read_b128 lane group hit 16 distinct bank quads
-// (lane = (row, run of 4 outputs): 16 rows x 4 runs = the wave); the SE pool partial of the group
-// is a fixed-order butterfly over the wave's lanes (no LDS slots, no second barrier).
-constexpr int SD2_ITP = 21;
-
-template <bool F32, bool V2>
+template <bool F32>
 __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const float* __restrict__ ws,
                                                       const float* __restrict__ bs, const float* __restrict__ wd,
                                                       const float* __restrict__ bd, f16_t* __restrict__ out,
                                                       float* __restrict__ pool_part) {
   constexpr int CW = 32, NPIX = SD_IT * SD_IT, NMT = (NPIX + 15) / 16;
   __shared__ __attribute__((aligned(16))) float patch[(SD_PR * SD_PW + 255) / 256 * 256];  // image patch, HWC
-  __shared__ __attribute__((aligned(16))) f16_t tile[V2 ? 4 * SD_IT * SD2_ITP * 8 : NPIX * CW];  // stem tile (+halo)
-  __shared__ __attribute__((aligned(16))) float sw[V2 ? 4 : 9 * CW];  // (V2: 40,320 B in all -> 4 WGs/CU)
-  __shared__ __attribute__((aligned(16))) float sb[V2 ? 4 : CW];
+  __shared__ __attribute__((aligned(16))) f16_t tile[NPIX * CW];  // stem tile (+halo)
+  __shared__ __attribute__((aligned(16))) float sw[9 * CW];
+  __shared__ __attribute__((aligned(16))) float sb[CW];
   float* red = patch;  // pool-partial slots [64][32]: the patch is dead once the stem tile is built
   static_assert((SD_PR * SD_PW + 255) / 256 * 256 >= (256 / (CW / 8)) * CW, "red fits in the patch");
   const uint8_t* img = (const uint8_t*)src;
@@ -660,10 +583,10 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
   const int py0 = 2 * oy0 - 3, px0 = 2 * ox0 - 3;  // image coords of patch (0, 0)
   EST_BEGIN(24)
 
-  // (V1: depthwise weights [C][9] transposed into LDS; V2 reads `wd` as the tap-major [9][C] copy)
-  const float wd0 = V2 ? 0.f : wd[(tid % CW) * 9 + tid / CW];
-  const float wd1 = (!V2 && tid + 256 < 9 * CW) ? wd[((tid + 256) % CW) * 9 + (tid + 256) / CW] : 0.f;
-  const float bd0 = (!V2 && tid < CW) ? bd[tid] : 0.f;
+  // depthwise weights [C][9] transposed into LDS
+  const float wd0 = wd[(tid % CW) * 9 + tid / CW];
+  const float wd1 = tid + 256 < 9 * CW ? wd[((tid + 256) % CW) * 9 + (tid + 256) / CW] : 0.f;
+  const float bd0 = tid < CW ? bd[tid] : 0.f;
   // stem weight fragments (A operand: row = output channel nt*16 + fr, k = fg*8 + e), split hi/lo
   int offk[8];
   f16x8 whi[2], wlo[2];
@@ -722,11 +645,9 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
     }
     patch[tid + i * 256] = c < 0 ? 0.f : v;
   }
-  if constexpr (!V2) {
-    sw[tid] = wd0;
-    if (tid + 256 < 9 * CW) sw[tid + 256] = wd1;
-    if (tid < CW) sb[tid] = bd0;
-  }
+  sw[tid] = wd0;
+  if (tid + 256 < 9 * CW) sw[tid + 256] = wd1;
+  if (tid < CW) sb[tid] = bd0;
   __syncthreads();
   EST()
 
@@ -758,186 +679,16 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
       float e4[4] = {acc[0] + sbias[nt].x, acc[1] + sbias[nt].y, acc[2] + sbias[nt].z, acc[3] + sbias[nt].w};
       act4<ACT_SILU>(e4);
       const int ch = nt * 16 + fg * 4;
-      f16_t* dst = V2 ? tile + (((ch >> 3) * SD_IT + sy) * SD2_ITP + sx) * 8 + (ch & 7) : tile + p * CW + ch;
+      f16_t* dst = tile + p * CW + ch;
       if (p < NPIX)
         *reinterpret_cast<uint2*>(dst) = inimg ? make_uint2(pack2h(e4[0], e4[1]), pack2h(e4[2], e4[3])) : make_uint2(0, 0);
     }
   }
   __syncthreads();
   EST()
-  if constexpr (!V2) {
-    dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW, blockIdx.x, 49);
-    EST()
-    EST_END()
-  } else {
-    const int g = __builtin_amdgcn_readfirstlane(wave);  // this wave's channel group
-    const int oy = lane >> 2, ox = (lane & 3) * 4;       // a run of 4 outputs of one tile row
-    float wk[9][8], acc[4][8];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) wk[t][j] = wd[t * CW + g * 8 + j];
-#pragma unroll
-    for (int o = 0; o < 4; ++o)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[o][j] = bd[g * 8 + j];
-    const f16_t* tp = tile + ((g * SD_IT + oy) * SD2_ITP + ox) * 8;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-#pragma unroll
-      for (int col = 0; col < 6; ++col) {
-        const uint4 v = *reinterpret_cast<const uint4*>(tp + (ky * SD2_ITP + col) * 8);
-        const float f[8] = {lo_h(v.x), hi_h(v.x), lo_h(v.y), hi_h(v.y), lo_h(v.z), hi_h(v.z), lo_h(v.w), hi_h(v.w)};
-#pragma unroll
-        for (int o = 0; o < 4; ++o) {
-          const int kx = col - o;
-          if (kx >= 0 && kx < 3) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[o][j] = fmaf(f[j], wk[ky * 3 + kx][j], acc[o][j]);
-          }
-        }
-      }
-    }
-    float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    f16_t* ob = out + (size_t)bi * 112 * 112 * CW;
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      act4<ACT_SILU>(acc[o]);
-      act4<ACT_SILU>(acc[o] + 4);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ps[j] += acc[o][j];
-      *reinterpret_cast<uint4*>(at_bytes(ob, (uint32_t)(((oy0 + oy) * 112 + ox0 + ox + o) * CW + g * 8) * 2u)) =
-          make_uint4(pack2h(acc[o][0], acc[o][1]), pack2h(acc[o][2], acc[o][3]), pack2h(acc[o][4], acc[o][5]),
-                     pack2h(acc[o][6], acc[o][7]));
-    }
-    // fixed-order butterfly: every lane ends with the wave's sum (deterministic, no atomics)
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ps[j] += __shfl_xor(ps[j], m, 64);
-    if (lane < 2)
-      *reinterpret_cast<float4*>(pool_part + ((size_t)bi * 49 + blockIdx.x) * CW + g * 8 + lane * 4) =
-          lane ? make_float4(ps[4], ps[5], ps[6], ps[7]) : make_float4(ps[0], ps[1], ps[2], ps[3]);
-  }
-}
-
-// Squeeze-excitation for G images per block (option se_group): the same per-image arithmetic as
-// se_kernel below, in the same order (bit-identical), but every fc1 / fc2 weight fetched from L2 once
-// per G images -- the late stages' 2 x 221 KB of fp32 weights made the one-image-per-block launch
-// L2-bound (113 MB of weight reads per 256 images).
-constexpr int SE_THREADS_G = 512;  // 8 waves: 256 registers for the G-image accumulators
-template <bool PRECISE, int G>
-__global__ __launch_bounds__(SE_THREADS_G) void se_group_kernel(const float* pool_part, int nchunks, float inv_hw,
-                                                                const float* w1, const float* b1, const float* w2t,
-                                                                const float* b2, float* scale, int B, int C, int Csq) {
-  __shared__ float pooled[G][1280];
-  __shared__ float s1[G][64];
-  const int b0 = blockIdx.x * G, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int idx = tid; idx < G * C; idx += SE_THREADS_G) {
-    const int g = idx / C, c = idx - g * C;
-    float v = 0.f;
-    if (b0 + g < B) {
-      const float* pp = pool_part + (size_t)(b0 + g) * nchunks * C;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-      int k = 0;
-      for (; k + 4 <= nchunks; k += 4) {
-        a0 += pp[(size_t)k * C + c];
-        a1 += pp[(size_t)(k + 1) * C + c];
-        a2 += pp[(size_t)(k + 2) * C + c];
-        a3 += pp[(size_t)(k + 3) * C + c];
-      }
-      for (; k < nchunks; ++k) a0 += pp[(size_t)k * C + c];
-      v = ((a0 + a1) + (a2 + a3)) * inv_hw;
-    }
-    pooled[g][c] = v;
-  }
-  __syncthreads();
-  {
-    constexpr int NWV = SE_THREADS_G / 64, OPW = 64 / NWV;  // outputs per wave (Csq <= 64)
-    float acc[OPW][G];
-#pragma unroll
-    for (int t = 0; t < OPW; ++t)
-#pragma unroll
-      for (int g = 0; g < G; ++g) acc[t][g] = 0.f;
-#pragma unroll
-    for (int t = 0; t < OPW; ++t) {
-      const int o = wave + NWV * t;
-      if (o < Csq) {
-        const float* wr = w1 + (size_t)o * C;
-        int c = lane;
-        for (; c + 192 < C; c += 256) {
-          const float w0 = wr[c], w1v = wr[c + 64], w2v = wr[c + 128], w3 = wr[c + 192];
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            acc[t][g] = fmaf(w0, pooled[g][c], acc[t][g]);
-            acc[t][g] = fmaf(w1v, pooled[g][c + 64], acc[t][g]);
-            acc[t][g] = fmaf(w2v, pooled[g][c + 128], acc[t][g]);
-            acc[t][g] = fmaf(w3, pooled[g][c + 192], acc[t][g]);
-          }
-        }
-        for (; c < C; c += 64) {
-          const float wv = wr[c];
-#pragma unroll
-          for (int g = 0; g < G; ++g) acc[t][g] = fmaf(wv, pooled[g][c], acc[t][g]);
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < OPW; ++t) {
-      const int o = wave + NWV * t;
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float a = wave_sum(acc[t][g]);
-        if (o < Csq && lane == 0) s1[g][o] = PRECISE ? silu_precise(a + b1[o]) : act_apply(a + b1[o], ACT_SILU);
-      }
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < C; c += SE_THREADS_G) {
-    float a0[G], a1[G], a2[G], a3[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = b2[c];
-      a1[g] = a2[g] = a3[g] = 0.f;
-    }
-    int j = 0;
-    for (; j + 16 <= Csq; j += 16) {
-      float wv[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) wv[u] = w2t[(size_t)(j + u) * C + c];
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int u = 0; u < 16; u += 4) {
-          a0[g] = fmaf(wv[u], s1[g][j + u], a0[g]);
-          a1[g] = fmaf(wv[u + 1], s1[g][j + u + 1], a1[g]);
-          a2[g] = fmaf(wv[u + 2], s1[g][j + u + 2], a2[g]);
-          a3[g] = fmaf(wv[u + 3], s1[g][j + u + 3], a3[g]);
-        }
-    }
-    for (; j + 4 <= Csq; j += 4) {
-      const float w0 = w2t[(size_t)j * C + c], w1v = w2t[(size_t)(j + 1) * C + c];
-      const float w2v = w2t[(size_t)(j + 2) * C + c], w3 = w2t[(size_t)(j + 3) * C + c];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        a0[g] = fmaf(w0, s1[g][j], a0[g]);
-        a1[g] = fmaf(w1v, s1[g][j + 1], a1[g]);
-        a2[g] = fmaf(w2v, s1[g][j + 2], a2[g]);
-        a3[g] = fmaf(w3, s1[g][j + 3], a3[g]);
-      }
-    }
-    for (; j < Csq; ++j) {
-      const float wv = w2t[(size_t)j * C + c];
-#pragma unroll
-      for (int g = 0; g < G; ++g) a0[g] = fmaf(wv, s1[g][j], a0[g]);
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (b0 + g >= B) continue;
-      const float a = (a0[g] + a1[g]) + (a2[g] + a3[g]);
-      scale[(size_t)(b0 + g) * C + c] = 1.0f / (1.0f + expf(-a));
-    }
-  }
+  dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW, blockIdx.x, 49);
+  EST()
+  EST_END()
 }
 
 // Squeeze-excitation, one 1024-thread block per image.  The three phases are each a few dependent
@@ -1093,18 +844,12 @@ hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* b
 }
 
 hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
-                                 const float* wd, const float* wd_t, const float* bd, f16_t* out, float* pool_part, int B,
+                                 const float* wd, const float* bd, f16_t* out, float* pool_part, int B,
                                  int* nchunks_out, hipStream_t s) {
   *nchunks_out = 49;  // = dwconv_nchunks(112, 112, 32, 1): the SE reads the same partial layout
   const dim3 grid(49, 1, B), blk(256);
-  // wd_t (tap-major [9][32] copy) selects the V2 depthwise phase
-  if (wd_t) {
-    if (xf32) hipLaunchKernelGGL((stem_dw_kernel<true, true>), grid, blk, 0, s, (const void*)xf32, ws, bs, wd_t, bd, out, pool_part);
-    else hipLaunchKernelGGL((stem_dw_kernel<false, true>), grid, blk, 0, s, (const void*)img, ws, bs, wd_t, bd, out, pool_part);
-  } else {
-    if (xf32) hipLaunchKernelGGL((stem_dw_kernel<true, false>), grid, blk, 0, s, (const void*)xf32, ws, bs, wd, bd, out, pool_part);
-    else hipLaunchKernelGGL((stem_dw_kernel<false, false>), grid, blk, 0, s, (const void*)img, ws, bs, wd, bd, out, pool_part);
-  }
+  if (xf32) hipLaunchKernelGGL((stem_dw_kernel<true>), grid, blk, 0, s, (const void*)xf32, ws, bs, wd, bd, out, pool_part);
+  else hipLaunchKernelGGL((stem_dw_kernel<false>), grid, blk, 0, s, (const void*)img, ws, bs, wd, bd, out, pool_part);
   return hipGetLastError();
 }
 
@@ -1186,39 +931,14 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
   const size_t smem = (size_t)dw_tile_bytes(IT, CW, false) + (size_t)(k * k * CW + CW + PX * CW) * 4;
   const size_t smem_ct = (size_t)dw_tile_bytes(IT, CW, true) + (size_t)(k * k * CW + CW) * 4;
   const dim3 grid(ntiles, C / CW, B), blk(256);
-  // persistent form (flag 2): about four resident blocks per CU over all channel groups, and the
-  // buffer descriptor's out-of-range offset must stay past the whole input
-  const int nitems = ntiles * B;
-  const bool persist = (ct & 2) && (size_t)B * H * W * C * 2 < (size_t)kOOB;
-  // one wave of resident blocks exactly (a block that does not fit at launch would run its whole
-  // item list after the others: a tail), spread over the channel groups
-  auto pgrid = [&](const void* kern) {
-    static int ncu = 0;
-    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
-    static const void* ck[16];
-    static int co[16], nc = 0;
-    int occ = 0;
-    for (int i = 0; i < nc; ++i)
-      if (ck[i] == kern) occ = co[i];
-    if (!occ) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, smem_ct) != hipSuccess || occ < 1) occ = 1;
-      if (nc < 16) { ck[nc] = kern; co[nc++] = occ; }
-    }
-    return dim3(std::max(1, std::min(nitems, ncu * occ / (C / CW))), C / CW);
-  };
   // compile-time geometries of EfficientNet-B0 at 224^2 (output runs R chosen so that items <= 256)
 #define MMF_DWCT(KK, SS, TT, CC, RR)                                                                          \
   if (k == KK && stride == SS && T == TT && CW == CC) {                                                        \
-    if (persist)                                                                                              \
-      hipLaunchKernelGGL((dwconv_persist_kernel<KK, SS, TT, CC, RR>),                                          \
-                         pgrid((const void*)dwconv_persist_kernel<KK, SS, TT, CC, RR>), blk, smem_ct, s, in, w,  \
-                         bias, out, pool_part, H, W, C, tiles_x, ntiles, nitems);                             \
-    else                                                                                                      \
-      hipLaunchKernelGGL((dwconv_kernel<KK, SS, TT, CC, RR>), grid, blk, smem_ct, s, in, w, bias, out, pool_part, H, \
-                         W, C, CW, T, tiles_x);                                                               \
+    hipLaunchKernelGGL((dwconv_kernel<KK, SS, TT, CC, RR>), grid, blk, smem_ct, s, in, w, bias, out, pool_part, H,   \
+                       W, C, CW, T, tiles_x);                                                                 \
     return hipGetLastError();                                                                                 \
   }
-  if (ct & 1) {  // bit 0 clear: runtime-geometry kernels only (A/B option "dw_ct")
+  if (ct & 1) {  // bit 0 clear: runtime-geometry kernels only (parity tests)
     MMF_DWCT(3, 1, 16, 32, MMF_R_D16)
     MMF_DWCT(3, 1, 14, 32, MMF_R_D14)
     MMF_DWCT(5, 1, 14, 32, MMF_R_D14)
@@ -1283,7 +1003,7 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
                        pool_part, H, W, C, CW, T, tiles_x);                                                      \
     return hipGetLastError();                                                                                    \
   }
-  // runtime-geometry kernels (option dw_ct = 0)
+  // runtime-geometry kernels (shapes past B0's, or ct = 0)
   MMF_EDW(3, 2, 1) MMF_EDW(3, 1, 1) MMF_EDW(5, 2, 1) MMF_EDW(5, 1, 2) MMF_EDW(3, 2, 2)
 #undef MMF_EDW
   return hipErrorInvalidValue;
@@ -1291,18 +1011,8 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
 
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s,
-                     bool precise, int group) {
+                     bool precise) {
   if (C > 1280 || Csq > 64) return hipErrorInvalidValue;
-  if (group == 8) {
-    const dim3 grid((B + 7) / 8);
-    if (precise)
-      hipLaunchKernelGGL((se_group_kernel<true, 8>), grid, dim3(SE_THREADS_G), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2,
-                         b2, scale, B, C, Csq);
-    else
-      hipLaunchKernelGGL((se_group_kernel<false, 8>), grid, dim3(SE_THREADS_G), 0, s, pool_part, nchunks, inv_hw, w1, b1,
-                         w2, b2, scale, B, C, Csq);
-    return hipGetLastError();
-  }
   if (precise)
     hipLaunchKernelGGL(se_kernel<true>, dim3(B), dim3(SE_THREADS), 0, s, pool_part, nchunks, inv_hw, w1, b1, w2, b2,
                        scale, C, Csq);

@@ -321,114 +321,6 @@ __global__ __launch_bounds__(256) void gap32_kernel(const float* __restrict__ x,
 }
 
 
-// Fused MBConv front of the fp32 tower (option fuse_expand32): 1x1 expand + BN + SiLU computed per
-// output tile (+ halo) straight into LDS, then the depthwise k x k + BN + SiLU from LDS -- the
-// expanded tensor (stage 2.1: 4.8 MB per image in fp32) never touches HBM.  BIT-IDENTICAL to
-// pw32m_kernel + dw32_kernel: the expand runs the same v_mfma_f32_16x16x4_f32 sequence (K padded with
-// zeros to whole 16-deep chunks, chunk stored k-transposed so lane group g supplies k = 4 s + g: an
-// ascending fmaf chain), then + bias and silu_precise; the depthwise keeps dw32's chain (bias, then
-// (ky, kx) ascending, out-of-image taps skipped).  One block: image b, T x T output tile, CG
-// expanded channels; 4 waves.
-//   Xs [NPP][CINP]  input tile (NP = IT^2 pixels, IT = (T - 1) S + K), k-transposed per 16-chunk
-//   Ws [CG][CINP]   the group's expand weights, same layout
-//   Es [NP][CG]     SiLU(expand) of the tile's pixels (out-of-image pixels hold junk, never read)
-template <int K, int S, int T, int CG, int CIN, int R>
-__global__ __launch_bounds__(256) void expand_dw32_kernel(const float* __restrict__ in, const float* __restrict__ we,
-                                                          const float* __restrict__ be, const float* __restrict__ wd,
-                                                          const float* __restrict__ bd, float* __restrict__ out, int H,
-                                                          int W, int C, int Ho, int Wo, int tiles_x) {
-  constexpr int P = (K - 1) / 2, IT = (T - 1) * S + K, NP = IT * IT, NPP = (NP + 15) / 16 * 16;
-  constexpr int CINP = (CIN + 15) / 16 * 16, NCH = CINP / 16;
-  static_assert(CG % 16 == 0 && CIN % 4 == 0 && T % R == 0, "tile geometry");
-  __shared__ __attribute__((aligned(16))) float Xs[NPP * CINP];
-  __shared__ __attribute__((aligned(16))) float Ws[CG * CINP];
-  __shared__ __attribute__((aligned(16))) float Es[NP * CG];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fg = lane >> 4;
-  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
-  const int c0 = blockIdx.y * CG, bi = blockIdx.z;
-  const int oy0 = ty * T, ox0 = tx * T, iy0 = oy0 * S - P, ix0 = ox0 * S - P;
-  // k-transposed offset of (row, k) in a [rows][CINP] array: chunk k / 16, lane group k % 4, step (k % 16) / 4
-  auto toff = [](int row, int k) { return row * CINP + (k & ~15) + ((k & 3) << 2) + ((k & 15) >> 2); };
-  // ---- input tile and weights -> LDS (zeros: K padding, pad rows, out-of-image pixels) ----
-  for (int idx = tid; idx < NPP * (CINP / 4); idx += 256) {
-    const int p = idx / (CINP / 4), k = (idx - p * (CINP / 4)) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int iy = iy0 + p / IT, ix = ix0 + p % IT;
-    if (p < NP && k < CIN && iy >= 0 && iy < H && ix >= 0 && ix < W)
-      v = *reinterpret_cast<const float4*>(in + (((size_t)bi * H + iy) * W + ix) * CIN + k);
-    Xs[toff(p, k)] = v.x; Xs[toff(p, k + 1)] = v.y; Xs[toff(p, k + 2)] = v.z; Xs[toff(p, k + 3)] = v.w;
-  }
-  for (int idx = tid; idx < CG * (CINP / 4); idx += 256) {
-    const int n = idx / (CINP / 4), k = (idx - n * (CINP / 4)) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (k < CIN) v = *reinterpret_cast<const float4*>(we + (size_t)(c0 + n) * CIN + k);
-    Ws[toff(n, k)] = v.x; Ws[toff(n, k + 1)] = v.y; Ws[toff(n, k + 2)] = v.z; Ws[toff(n, k + 3)] = v.w;
-  }
-  __syncthreads();
-  // ---- expand on the f32 MFMA: (16-pixel row block, 16-channel column block) pairs over the waves ----
-  for (int pb = wave; pb < (NPP / 16) * (CG / 16); pb += 4) {
-    const int rb = pb / (CG / 16), cb = pb - rb * (CG / 16);
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      const float4 wf = *reinterpret_cast<const float4*>(&Ws[(cb * 16 + fr) * CINP + ch * 16 + fg * 4]);
-      const float4 xf = *reinterpret_cast<const float4*>(&Xs[(rb * 16 + fr) * CINP + ch * 16 + fg * 4]);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.x, xf.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.y, xf.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.z, xf.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.w, xf.w, acc, 0, 0, 0);
-    }
-    // lane: E[pixel rb * 16 + fr][channels cb * 16 + 4 fg .. + 3] (operands swapped, as pw32m)
-    const int p = rb * 16 + fr, n = cb * 16 + fg * 4;
-    if (p < NP) {
-      const float4 bv = *reinterpret_cast<const float4*>(be + c0 + n);
-      const float4 o = make_float4(act_precise(acc[0] + bv.x, ACT_SILU), act_precise(acc[1] + bv.y, ACT_SILU),
-                                   act_precise(acc[2] + bv.z, ACT_SILU), act_precise(acc[3] + bv.w, ACT_SILU));
-      *reinterpret_cast<float4*>(&Es[p * CG + n]) = o;
-    }
-  }
-  __syncthreads();
-  // ---- depthwise from LDS: items (output row, run of R outputs, channel quad) ----
-  constexpr int NQ = CG / 4, NRUN = T / R;
-  for (int it = tid; it < T * NRUN * NQ; it += 256) {
-    const int q = it % NQ, rest = it / NQ, run = rest % NRUN, ry = rest / NRUN;
-    const int oy = oy0 + ry, oxs = ox0 + run * R, c = c0 + q * 4;
-    if (oy >= Ho) continue;
-    const float4 b4 = *reinterpret_cast<const float4*>(bd + c);
-    float4 acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = b4;
-#pragma unroll
-    for (int ky = 0; ky < K; ++ky) {
-      const int iy = oy * S - P + ky;
-      if (iy < 0 || iy >= H) continue;
-      const int ly = iy - iy0;
-      float4 wt[K];
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx) wt[kx] = *reinterpret_cast<const float4*>(wd + (size_t)(ky * K + kx) * C + c);
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int kx = 0; kx < K; ++kx) {
-          const int ix = (oxs + r) * S - P + kx;
-          if (ix < 0 || ix >= W) continue;
-          const float4 v = *reinterpret_cast<const float4*>(&Es[(ly * IT + (ix - ix0)) * CG + q * 4]);
-          acc[r].x = fmaf(v.x, wt[kx].x, acc[r].x);
-          acc[r].y = fmaf(v.y, wt[kx].y, acc[r].y);
-          acc[r].z = fmaf(v.z, wt[kx].z, acc[r].z);
-          acc[r].w = fmaf(v.w, wt[kx].w, acc[r].w);
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int ox = oxs + r;
-      if (ox < Wo)
-        *reinterpret_cast<float4*>(out + (((size_t)bi * Ho + oy) * Wo + ox) * C + c) =
-            make_float4(silu_precise(acc[r].x), silu_precise(acc[r].y), silu_precise(acc[r].z), silu_precise(acc[r].w));
-    }
-  }
-}
-
 }  // namespace
 
 hipError_t launch_pw32(const float* A, const float* W, const float* bias, const float* ascale, int rows_per_image,
@@ -491,24 +383,3 @@ hipError_t launch_gap32(const float* x, int HW, int C, const float* w, const flo
   return hipGetLastError();
 }
 
-// The fused expand + depthwise front of the fp32 tower for the EfficientNet-B0 blocks whose input
-// has <= 40 channels (stages 2.1 - 4.1); hipErrorNotSupported for any other geometry (the caller
-// then runs pw32 + dw32).
-hipError_t launch_expand_dw32(const float* in, const float* we, const float* be, const float* wd, const float* bd,
-                              float* out, int B, int H, int W, int cin, int cexp, int k, int stride, hipStream_t s) {
-  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-#define MMF_EDW32(HH, KK, SS, TT, CGG, CI, CE, RR)                                                              \
-  if (H == HH && W == HH && k == KK && stride == SS && cin == CI && cexp == CE) {                              \
-    const int tx = (Wo + TT - 1) / TT, ty = (Ho + TT - 1) / TT;                                                \
-    hipLaunchKernelGGL((expand_dw32_kernel<KK, SS, TT, CGG, CI, RR>), dim3(tx * ty, CE / CGG, B), dim3(256), 0, s, \
-                       in, we, be, wd, bd, out, H, W, cexp, Ho, Wo, tx);                                       \
-    return hipGetLastError();                                                                                  \
-  }
-  MMF_EDW32(112, 3, 2, 8, 32, 16, 96, 2)    // stage 2.1
-  MMF_EDW32(56, 3, 1, 8, 48, 24, 144, 4)    // stage 2.2
-  MMF_EDW32(56, 5, 2, 7, 16, 24, 144, 1)    // stage 3.1
-  MMF_EDW32(28, 5, 1, 7, 48, 40, 240, 1)    // stage 3.2
-  MMF_EDW32(28, 3, 2, 7, 16, 40, 240, 1)    // stage 4.1
-#undef MMF_EDW32
-  return hipErrorNotSupported;
-}

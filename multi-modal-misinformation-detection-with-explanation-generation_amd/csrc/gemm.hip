@@ -22,9 +22,6 @@
 namespace {
 
 constexpr int BK = 64;
-#ifndef WIDE_XD
-#define WIDE_XD 2  // 256x384 tiles: X fragments read ahead of their MFMAs
-#endif
 
 template <int BM, int BN, int WGM, int WGN>
 struct Cfg {
@@ -39,98 +36,13 @@ struct Cfg {
 
 MMF_DEV int swz(int row, int kc) { return row * BK + ((kc ^ (row & 7)) << 3); }
 
-// split-K in one launch (gemm_f16_kernel FIX).  Hand-off per cdna_hip_programming.md Guideline 16:
-// every partial is stored sc1 (write-through) and drained by its wave before the workgroup's barrier,
-// one lane then adds to the tile's agent-scope counter; the last arriver acquires and reads every
-// plane with sc1 loads.  The sum runs over slices 0..S-1 in order, then bias -> activation ->
-// residual, the operations of splitk_reduce_kernel in the same order (bit-identical results).
-typedef __attribute__((address_space(1))) unsigned gu32;
-template <int ACT>
-MMF_DEV void splitk_fin_rows(const GemmArgs& fin, rsrc_t rp, uint32_t plane, int S, int m0, int n0, int rows, int tid) {
-  const int M = fin.M, N = fin.N;
-  for (int e = tid; e < rows * 32; e += 256) {  // 32 float4 column groups per 128-column tile row
-    const int m = m0 + (e >> 5), n = n0 + (e & 31) * 4;
-    if (m >= M || n >= N) continue;
-    const uint32_t off = ((uint32_t)m * N + n) * 4u;
-    float4 acc;
-    {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 16);
-      acc = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-    }
-    for (int z = 1; z < S; ++z) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, off + (uint32_t)z * plane, 0, 16);
-      acc.x += __uint_as_float(v.x); acc.y += __uint_as_float(v.y);
-      acc.z += __uint_as_float(v.z); acc.w += __uint_as_float(v.w);
-    }
-    float v[4] = {acc.x, acc.y, acc.z, acc.w};
-    if (fin.bias) {
-      const float4 b = *reinterpret_cast<const float4*>(fin.bias + n);
-      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-    }
-    if (ACT != ACT_NONE) act4<ACT>(v);
-    if (fin.res32) {
-      const float4 r = *reinterpret_cast<const float4*>(fin.res32 + (size_t)m * fin.ldr + n);
-      v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
-    } else if (fin.res16) {
-      const uint2 r = *reinterpret_cast<const uint2*>(fin.res16 + (size_t)m * fin.ldr + n);
-      v[0] += lo_h(r.x); v[1] += hi_h(r.x); v[2] += lo_h(r.y); v[3] += hi_h(r.y);
-    }
-    if (fin.c32) *reinterpret_cast<float4*>(fin.c32 + (size_t)m * fin.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
-    if (fin.c16)
-      *reinterpret_cast<uint2*>(fin.c16 + (size_t)m * fin.ldc + n) = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
-  }
-}
-template <int BM, int BN, int NI, int MI>
-MMF_DEV void splitk_fixup(const GemmArgs& g, const GemmArgs& fin, const f32x4 (&acc)[NI][MI], int tile, int m0, int n0,
-                          int rl, int cl, int tid) {
-  static_assert(BN == 128, "32 float4 groups per tile row");
-  const int S = gridDim.y, z = blockIdx.y, M = g.M, N = g.N;
-  const uint32_t plane = (uint32_t)M * N * 4u;
-  const rsrc_t rp = make_rsrc(fin.ws, plane * (uint32_t)S);
-#pragma unroll
-  for (int j = 0; j < MI; ++j)
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int m = m0 + rl + j * 16, n = n0 + cl + i * 16;
-      const uint32_t off = (m < M && n < N) ? (uint32_t)z * plane + ((uint32_t)m * N + n) * 4u : kOOB;
-      const u32x4 w = {__float_as_uint(acc[i][j][0]), __float_as_uint(acc[i][j][1]), __float_as_uint(acc[i][j][2]),
-                       __float_as_uint(acc[i][j][3])};
-      __builtin_amdgcn_raw_buffer_store_b128(w, rp, off, 0, 16);  // sc1: write-through
-    }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
-  __shared__ unsigned last;
-  __syncthreads();
-  if (tid == 0)
-    last = __hip_atomic_fetch_add((gu32*)(fin.ws_cnt + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-           (unsigned)(S - 1);
-  __syncthreads();
-  if (!last) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  const int rows = BM;
-  switch (fin.act) {
-    case ACT_GELU: splitk_fin_rows<ACT_GELU>(fin, rp, plane, S, m0, n0, rows, tid); break;
-    case ACT_QUICK_GELU: splitk_fin_rows<ACT_QUICK_GELU>(fin, rp, plane, S, m0, n0, rows, tid); break;
-    case ACT_SILU: splitk_fin_rows<ACT_SILU>(fin, rp, plane, S, m0, n0, rows, tid); break;
-    case ACT_RELU: splitk_fin_rows<ACT_RELU>(fin, rp, plane, S, m0, n0, rows, tid); break;
-    default: splitk_fin_rows<ACT_NONE>(fin, rp, plane, S, m0, n0, rows, tid); break;
-  }
-  if (tid == 0) __hip_atomic_store((gu32*)(fin.ws_cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // PF = 2: the global loads of K-step kt + 2 are issued at step kt into a second register set, so
 // two K-steps of compute cover each load's latency instead of one (long-K, few-workgroup launches:
 // the EfficientNet SE-scaled projects, M = B * 49 or B * 196 rows, K = 480 ... 1152)
 // ASC: the A operand carries an SE scale (g.ascale); instantiated apart so that plain launches keep
 // their register budget
-// FIX (split-K slices, grid.y = S): each slice stores its fp32 partial tile write-through (sc1), the
-// last slice of a tile to arrive (agent-scope counter in g.ws_cnt) sums the S partials in slice order
-// and applies fin's epilogue exactly as splitk_reduce_kernel does -- one launch instead of two
-template <int BM, int BN, int WGM, int WGN, int PF = 1, bool ASC = false, bool FIX = false>
-__global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN, GemmArgs fin) {
+template <int BM, int BN, int WGM, int WGN, int PF = 1, bool ASC = false>
+__global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN) {
   using C = Cfg<BM, BN, WGM, WGN>;
   __shared__ __attribute__((aligned(16))) f16_t lds[2 * (BM + BN) * BK];
   auto Xs = [&](int buf) { return lds + buf * (BM + BN) * BK; };
@@ -270,10 +182,6 @@ __global__ __launch_bounds__(256) void gemm_f16_kernel(GemmArgs g, int tilesN, G
     }
   }
 
-  if constexpr (FIX) {
-    splitk_fixup<BM, BN>(g, fin, acc, wgid, m0, n0, wm * C::TM + fr, wn * C::TN + fg * 4, tid);
-    return;
-  }
   // epilogue: lane holds C[m][n..n+3].  All loads (bias, fp16 residual) are issued before the
   // first store and from clamped addresses (no divergent region around them): with one in-order
   // vmcnt a load issued after a store waits for that store, and a store's data VGPRs cannot be
@@ -554,30 +462,23 @@ MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], c
 
 // DBG (measurement builds, forced configs 15 / 16 only; outputs garbage): 1 = LDS-DMA + barriers only,
 // 2 = fragment reads + MFMAs + barriers only
-template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0, bool TQ = false>
-__global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 : 2) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
-                                                                     int gm) {
+template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
+                                                                       int gm) {
   // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
   // K-slab of the NEXT tile is DMA'd into the free LDS stage during the current tile's last
   // K-step, so only the very first tile pays the load latency and each epilogue's stores drain
   // underneath the next tile's first MFMAs.
-  // BM = 128 variants use 4 waves and <= 80 KB of LDS so TWO workgroups share a CU: one's
-  // epilogue (stores) then overlaps the other's MFMA main loop.
   constexpr int NW = WGM * WGN;
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int STAGE = (BM + BN) * BK;
-  static_assert(NW == 8 || NW == 4, "4 or 8 waves");
+  static_assert(NW == 8 && BM == 256, "8 waves, 256-row tiles");
   // EPI 3 (attention epilogue, RoBERTa QKV): a 40 KB gap between the two stages, so that the stage
   // the last K-step freed plus the gap hold q (32 KB) and k | v (64 KB) of the tile's two sequences
   constexpr bool ATT = EPI == 3;
   static_assert(!ATT || (BM == 256 && BN == 192 && WGM == 4 && WGN == 2 && PIPE2), "attention epilogue: 256x192");
   constexpr int XGAP = ATT ? 20480 : 0;  // f16 elements
   constexpr int SOFF = STAGE + XGAP;     // stage 1's offset
-  // 256x384 tiles (two stages = all 160 KB of LDS; 192 accumulator registers per lane): the bias
-  // columns are fetched after the K loop and the residual rows without look-ahead, so that neither
-  // is live beside the accumulators
-  constexpr bool WIDE = BN == 384;
-  static_assert(!WIDE || (EPI == 0 && !PIPE2), "256x384 tiles: plain epilogues, one-step K loop");
   __shared__ __attribute__((aligned(16))) f16_t lds[2 * STAGE + XGAP];
   constexpr bool ROWST = EPI == 1;  // reads row statistics
   static_assert(EPI == 0 || BM == 256, "lazy-LN epilogues assume 256-row tiles");
@@ -610,34 +511,15 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
 
   int t = wgid;
   if (t >= tiles) return;
-  // Tile queue (option gemm_tq; the launcher sets g.tq only when every workgroup has a first tile and
-  // nk >= 3).  The first tile is the static one; after it, each workgroup takes the next tile of its
-  // XCD's share of the static schedule from that XCD's counter.  Under a concurrent launch the
-  // workgroups that start late then take fewer tiles, rather than each running its fixed share
-  // behind the others.  The tile order within an XCD is the static one, so L2 locality is kept.
-  // Static index of XCD x's c-th tile: (c / qx) * nwg + xbase + c % qx.
-  // (instantiated apart: the queue's scalars cost the static kernels registers; 256x384 tiles have
-  // all 160 KB of LDS taken, so they stay static)
-  constexpr bool dyn = TQ && !WIDE;
-  const int qx = xcd < r ? q + 1 : q, xbase = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  // the ticket's LDS slots (two, by tile parity): lds_stat's two unused entries where no row statistics
-  // are kept (the 256x384 tiles have no other LDS byte free)
-  int* lds_tq;
-  if constexpr (ROWST) {
-    __shared__ int tq_own[2];
-    lds_tq = tq_own;
-  } else {
-    lds_tq = reinterpret_cast<int*>(lds_stat);
-  }
-  int par = 0, tnext = 0;
-  unsigned cq = 0;
-  if ((g.prio == 1 && wave >= NW / 2) || (g.prio == 2 && wave < NW / 2)) __builtin_amdgcn_s_setprio(1);
+  int tnext = 0;
+  // s_setprio 1 for waves 0-3 (+0.4 % on the step, round-1 A/B; the old option gemm_prio = 2)
+  if (wave < NW / 2) __builtin_amdgcn_s_setprio(1);
   // descriptor fills (glds_tile_buf) for every full row / column panel whose operand's byte extent
-  // fits 32 bits (WIDE: checked by the launcher): the per-lane source offset is one loop-invariant
+  // fits 32 bits: the per-lane source offset is one loop-invariant
   // VGPR and the panel base rides in the scalar soffset, so a K-step's DMA issue costs no VALU
   // (glds_tile: a clamped row and a 64-bit address per piece, ~6 VALU each, every K-step)
-  const bool bufA = WIDE || (MMF_GLDS_BUF && (size_t)M * g.lda * 2 < ((size_t)1 << 32));
-  const bool bufW = WIDE || (MMF_GLDS_BUF && (size_t)N * g.ldw * 2 < ((size_t)1 << 32));
+  const bool bufA = MMF_GLDS_BUF && (size_t)M * g.lda * 2 < ((size_t)1 << 32);
+  const bool bufW = MMF_GLDS_BUF && (size_t)N * g.ldw * 2 < ((size_t)1 << 32);
   const rsrc_t ra = make_rsrc(g.A, bufA ? (uint32_t)((size_t)M * g.lda * 2) : 0u);
   const rsrc_t rw = make_rsrc(g.W, bufW ? (uint32_t)((size_t)N * g.ldw * 2) : 0u);
   const uint32_t lchunk = (uint32_t)(((lane & 7) ^ (lane >> 3)) * 16);
@@ -648,15 +530,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
     int tm_, tn_;
     tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);
     f16_t* nb = lds + buf * SOFF;
-    if constexpr (WIDE) {
-      if (tm_ * BM + BM <= M) {  // (N % 384 == 0: every column panel is full)
-        glds_tile_buf<BM, NW>(ra, (uint32_t)g.lda * 2u, tm_ * BM, kt * BK, aoff, nb, wave);
-      } else {
-        glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
-      }
-      glds_tile_buf<BN, NW>(rw, (uint32_t)g.ldw * 2u, tn_ * BN, kt * BK, woff, nb + BM * BK, wave);
-      return;
-    }
     if (bufA && tm_ * BM + BM <= M) glds_tile_buf<BM, NW>(ra, (uint32_t)g.lda * 2u, tm_ * BM, kt * BK, aoff, nb, wave);
     else glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
     if (bufW && tn_ * BN + BN <= N)
@@ -687,11 +560,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
   stage(0, t, 0);
   __syncthreads();
   int cur = 0;
-  for (; t < tiles; t = tnext, par ^= 1) {
+  for (; t < tiles; t = tnext) {
     tnext = t + nwg;
-    // one lane takes the queue's next ticket now; its return is first used at kt = 1, after the
-    // first K-step's barrier (vmcnt(0)) has waited for it anyway
-    if (dyn && tid == 0) cq = __hip_atomic_fetch_add((gu32*)(g.tq + xcd * kTqStride), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int tm, tn;
     tile_coords(t, tilesM, tilesN, gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
@@ -701,7 +571,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
 #pragma unroll
       for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     float4 bias_r[ROWST ? 1 : NI];  // this lane's epilogue bias columns, fetched under the K loop
-    if constexpr (!ROWST && !WIDE) {
+    if constexpr (!ROWST) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
     }
@@ -766,19 +636,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      if (dyn && kt == 1 && wave == 0) {  // (wave-uniform: no exec-masked region inside the K loop)
-        // the empty asm pins the ticket's first use here: without it hipcc hoists the readfirstlane
-        // to the atomic, and wave 0 waits out the atomic's round trip (vmcnt(0)) at every tile start
-        unsigned cv = cq;
-        asm volatile("" : "+v"(cv));
-        const unsigned c = (unsigned)qx + __builtin_amdgcn_readfirstlane(cv);
-        const int tq_ = (int)(c / (unsigned)qx) * nwg + xbase + (int)(c % (unsigned)qx);
-        lds_tq[par] = tq_ < tiles ? tq_ : tiles;
-      }
       if (kt + 1 < nk) {
         stage(cur ^ 1, t, kt + 1);
       } else {
-        if (dyn) tnext = __builtin_amdgcn_readfirstlane(lds_tq[par]);  // written at kt = 1, barriers since
         if (tnext < tiles) stage(cur ^ 1, tnext, 0);
       }
       const f16_t* Xs = lds + cur * SOFF;
@@ -816,32 +676,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
 #pragma unroll
           for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(w1[i], x1[j], acc[i][j]);
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (WIDE) {
-        // 256x384 (wave tile 128x96, 192 accumulator registers): the 6 W fragments of a 32-deep
-        // half-step are held, the 8 X fragments stream through two registers sets, one read per
-        // 6 MFMAs (sched_barriers keep hipcc from hoisting all 14 reads, which would spill)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          constexpr int XD = WIDE_XD;  // X fragments in flight
-          f16x8 wf[NI], xf[XD + 1];
-          xf[0] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + fr, ks * 4 + fg)));
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-            wf[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
-#pragma unroll
-          for (int j = 1; j < XD; ++j)
-            xf[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int j = 0; j < MI; ++j) {
-            if (j + XD < MI)
-              xf[(j + XD) % (XD + 1)] =
-                  as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + (j + XD) * 16 + fr, ks * 4 + fg)));
-#pragma unroll
-            for (int i = 0; i < NI; ++i) acc[i][j] = mfma16x16x32(wf[i], xf[j % (XD + 1)], acc[i][j]);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
       } else if constexpr (BN == 192) {
         // 256x192 (wave tile 64x96): all 20 fragment reads of the K-step first, then its 48 MFMAs,
         // then the barrier -- pinned with sched_barriers (hipcc otherwise interleaves 2 reads +
@@ -886,10 +720,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
       cur ^= 1;
     }
 
-    if constexpr (WIDE) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
-    }
     // Epilogue.  The activation is a compile-time parameter (no per-element branch).  All traffic
     // is raw-buffer: out-of-range rows/columns read 0 / drop their stores, so there is no divergent
     // branch and no load that has to wait on the stores issued before it -- bias columns were
@@ -1012,11 +842,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
           }
         }
       };
-      if constexpr (!WIDE) load_res(rcur, 0);
+      load_res(rcur, 0);
 #pragma unroll
       for (int j = 0; j < MI; ++j) {
-        if constexpr (WIDE) load_res(rcur, j);
-        else if (j + 1 < MI) load_res(rnext, j + 1);
+        if (j + 1 < MI) load_res(rnext, j + 1);
         const uint32_t m = m0 + wm * TM + j * 16 + fr;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -1031,60 +860,30 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4 && BM == 256) ? 1 :
           if (g.c32) buf_store_f4(rc32, e * 4u, make_float4(v[0], v[1], v[2], v[3]));
           if (g.c16) buf_store_u2(rc16, e * 2u, make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3])));
         }
-        if constexpr (!WIDE) {
 #pragma unroll
-          for (int i = 0; i < NI; ++i) rcur[i] = rnext[i];
-        }
+        for (int i = 0; i < NI; ++i) rcur[i] = rnext[i];
       }
     };
     if (g.res32) epilogue(std::true_type{});
     else epilogue(std::false_type{});
   }
-  // tile queue: every workgroup has taken its last ticket; the last one to finish zeroes the words for
-  // the stream's next launch (kernel boundary: visible).  Relaxed is enough: a workgroup issues its
-  // finish add only after its last ticket's value has returned (the loop exit depends on it), so
-  // every ticket add has been performed when the finish count reaches nwg -- an acq_rel add would
-  // write back and invalidate the XCD's L2 in every workgroup.
-  if (dyn && tid == 0) {
-    const unsigned d = __hip_atomic_fetch_add((gu32*)(g.tq + 8 * kTqStride), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (unsigned)nwg - 1) {
-      for (int x = 0; x < 9; ++x) __hip_atomic_store((gu32*)(g.tq + x * kTqStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
-// the tile queue only where it can act: more tiles than workgroups (every workgroup then has a
-// static first tile) and K-steps enough for the ticket hand-off (written at kt = 1, read at nk - 1)
-static GemmArgs with_tile_queue(const GemmArgs& a, int tiles, int grid) {
-  GemmArgs b = a;
-  if (!(a.tq && tiles > grid && a.K / BK >= 3)) b.tq = nullptr;
-  return b;
-}
-
+// persistent grid: one workgroup per CU (256 CUs), fewer when the launch has fewer tiles
 template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false, int DBG = 0>
 hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
-  const int per_cu = (BM == 128) ? 2 : 1;  // co-resident workgroups per CU (LDS / VGPR budget)
-  const int cap = (a.max_grid > 0 && a.max_grid < 256 ? a.max_grid : 256) * per_cu;
-  const int grid = tiles < cap ? tiles : cap;
+  const int grid = tiles < 256 ? tiles : 256;
   const dim3 blk(64 * WGM * WGN);
   const int gm = a.group_m;  // tile-order option (handle option "gemm_group_m"; 0 = row-major)
-  const GemmArgs b = with_tile_queue(a, tiles, grid);
-  // queue instantiations: the pipelined production tiles without an activation (with GELU's epilogue
-  // the 256x256 kernel's queue variant spills ~20 VGPRs; those launches keep the static schedule)
-  constexpr bool kTq = PIPE2 && BN != 384 && DBG == 0;
 #define MMF_GLDS_CASE(ACT)                                                                                  \
   case ACT:                                                                                                 \
-    if (kTq && ACT == ACT_NONE && b.tq)                                                                     \
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG, kTq && ACT == ACT_NONE>), dim3(grid), blk, 0, s, \
-                         b, tilesN, tiles, tilesM, gm);                                                      \
-    else                                                                                                    \
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, b, tilesN, tiles, tilesM, \
-                         gm);                                                                                    \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, a, tilesN, tiles, \
+                       tilesM, gm);                                                                          \
     break;
   if constexpr (DBG != 0) {
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT_NONE, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, b, tilesN,
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT_NONE, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, a, tilesN,
                        tiles, tilesM, gm);
     return hipGetLastError();
   }
@@ -1101,23 +900,17 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// lazy-LN epilogues (pipelined 256-row tiles only)
+// lazy-LN / attention epilogues (pipelined 256-row tiles only)
 template <int BM, int BN, int WGM, int WGN>
 hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
-  const int cap = a.max_grid > 0 && a.max_grid < 256 ? a.max_grid : 256;
-  const int grid = tiles < cap ? tiles : cap;
+  const int grid = tiles < 256 ? tiles : 256;
   const dim3 blk(64 * WGM * WGN);
   const int gm = a.group_m;
-  const GemmArgs b = with_tile_queue(a, tiles, grid);
 #define MMF_EPI_CASE(EPI, ACT)                                                                                 \
-  if (b.tq)                                                                                                    \
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, true, EPI, 0, true>), dim3(grid), blk, 0, s, b, tilesN, \
-                       tiles, tilesM, gm);                                                                     \
-  else                                                                                                         \
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, true, EPI>), dim3(grid), blk, 0, s, b, tilesN, tiles, \
-                       tilesM, gm)
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, true, EPI>), dim3(grid), blk, 0, s, a, tilesN, tiles, \
+                     tilesM, gm)
   if (a.epi == 1) {
     switch (a.act) {
       case ACT_NONE: MMF_EPI_CASE(1, ACT_NONE); break;
@@ -1125,16 +918,12 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
       case ACT_QUICK_GELU: MMF_EPI_CASE(1, ACT_QUICK_GELU); break;
       default: return hipErrorInvalidValue;
     }
-  } else if (a.act != ACT_NONE) {
+  } else if (a.act != ACT_NONE || BN != 192) {
     return hipErrorInvalidValue;
   } else if (a.epi == 2) {
-    MMF_EPI_CASE(2, ACT_NONE);
+    if constexpr (BN == 192) MMF_EPI_CASE(2, ACT_NONE);
   } else if (a.epi == 3) {
-    if constexpr (BN == 192) {
-      MMF_EPI_CASE(3, ACT_NONE);
-    } else {
-      return hipErrorInvalidValue;
-    }
+    if constexpr (BN == 192) MMF_EPI_CASE(3, ACT_NONE);
   } else {
     return hipErrorInvalidValue;
   }
@@ -1151,11 +940,11 @@ hipError_t run(const GemmArgs& a, hipStream_t s) {
   const dim3 grid(tilesM * tilesN);
   const bool pf2 = MMF_GEMM_PF2_K > 0 && a.K >= MMF_GEMM_PF2_K;
   if (a.ascale) {
-    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2, true>), grid, dim3(256), 0, s, a, tilesN, a);
-    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 1, true>), grid, dim3(256), 0, s, a, tilesN, a);
+    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2, true>), grid, dim3(256), 0, s, a, tilesN);
+    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 1, true>), grid, dim3(256), 0, s, a, tilesN);
   } else {
-    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2>), grid, dim3(256), 0, s, a, tilesN, a);
-    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), grid, dim3(256), 0, s, a, tilesN, a);
+    if (pf2) hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 2>), grid, dim3(256), 0, s, a, tilesN);
+    else hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), grid, dim3(256), 0, s, a, tilesN);
   }
   return hipGetLastError();
 }
@@ -1203,12 +992,7 @@ hipError_t run_splitk(const GemmArgs& a, int S, hipStream_t s) {
   p.A = a.A; p.lda = a.lda; p.W = a.W; p.ldw = a.ldw;
   p.c32 = a.ws; p.ldc = a.N;
   p.M = a.M; p.N = a.N; p.K = a.K / S;
-  if (a.ws_cnt && tilesM * tilesN <= kSplitkCounters) {  // one launch: the last slice reduces (FIX)
-    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN, 1, false, true>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p,
-                       tilesN, a);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p, tilesN, a);
+  hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WGM, WGN>), dim3(tilesM * tilesN, S), dim3(256), 0, s, p, tilesN);
   const int threads = a.M * (a.N >> 2);
   const dim3 grid((threads + 255) / 256);
   switch (a.act) {
@@ -1233,33 +1017,35 @@ static bool glds_ok(const GemmArgs& a) {
   return (a.K % BK) == 0 && !a.ascale && rows * a.ldc * 4 < lim && rows * (a.ldr > 0 ? a.ldr : 0) * 4 < lim;
 }
 
-// 256x384 tiles: whole column panels and 32-bit descriptor extents for both operands
-static bool wide_ok(const GemmArgs& a) {
-  const size_t lim = (size_t)1 << 32;
-  return glds_ok(a) && a.N % 384 == 0 && (size_t)a.M * a.lda * 2 < lim && (size_t)a.N * a.ldw * 2 < lim;
+#ifndef MMF_GEMM_DIAG
+#define MMF_GEMM_DIAG 0  // 1: the measurement builds of the 256x192 kernel (forced configs 15 / 16; tools/)
+#endif
+
+// Instantiations launch_gemm can run (the rest of the numbering belonged to variants measured slower
+// and removed in round 5 -- 128-row and 256x384 tiles, the ring / loader-consumer kernels, the 4-wave
+// 256x192 tile: DESIGN.md §3 records each measurement and its last commit).
+static bool config_exists(int c) {
+  return c == 0 || c == 1 || c == 2 || c == 3 || c == 5 || c == 9 || c == 10 || c == 11 ||
+         (MMF_GEMM_DIAG && (c == 15 || c == 16));
 }
 
 static int forced_config(const GemmArgs& a) {
   // handle option "gemm_config" (benchmarking override, tools/gemm_bench.py); ignored if inapplicable
   if (a.force_cfg <= 0) return -1;
   const int c = a.force_cfg - 1;
-  if (((c >= 4 && c <= 8) || c >= 10) && !glds_ok(a)) return -1;
+  if (!config_exists(c)) return -1;
+  if ((c == 5 || c >= 10) && !glds_ok(a)) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
-  if (((c >= 12 && c <= 14) || c >= 17) && !gemm_ring_ok(a)) return -1;
-  if (c == 20 && !wide_ok(a)) return -1;
-  return (c >= 0 && c <= 21) ? c : -1;
+  return c;
 }
 
 // persistent 256-row LDS-DMA tiles: the column tile that minimises whole "rounds" of 256 CUs x
 // per-tile time (wider tiles are more efficient per flop); with_128 = also consider 256x128
 static int glds_pick(const GemmArgs& a, bool with_128) {
-  // (the 256- and 192-column tiles run the half-step-pipelined K loop, configs 11 / 10; with the
-  // option gemm_ring, 192-column tiles that gemm_lc_kernel can serve run it instead, config 17)
+  // (the 256- and 192-column tiles run the half-step-pipelined K loop, configs 11 / 10)
   const long tm = (a.M + 255) / 256;
-  const bool lc = a.ring && gemm_ring_ok(a);
-  const int bns[3] = {256, 192, 128}, cfg[3] = {11, lc ? 17 : (a.w4 ? 21 : 10), 5};
-  // measured per-flop efficiency (tools/gemm_bench.py; the loader / consumer kernel 0.95)
-  const double eff[3] = {1.0, lc ? 0.95 : 0.88, 0.80};
+  const int bns[3] = {256, 192, 128}, cfg[3] = {11, 10, 5};
+  const double eff[3] = {1.0, 0.88, 0.80};  // measured per-flop efficiency (tools/gemm_bench.py)
   int best = 11;
   double bc = 1e30;
   for (int i = 0; i < (with_128 ? 3 : 2); ++i) {
@@ -1267,25 +1053,13 @@ static int glds_pick(const GemmArgs& a, bool with_128) {
     const double c = (double)((tiles + 255) / 256) * bns[i] / eff[i];
     if (c < bc) { bc = c; best = cfg[i]; }
   }
-  // 256x384 (config 20, plain epilogues): per flop no faster than 256x256 (its fill is exposed:
-  // profiles/r03_gemm_clock_probe.txt) and slower in a single round (no next tile to hide the
-  // first slab and the epilogue under), so it is taken only with >= 2 rounds and when it saves a
-  // round: RoBERTa QKV (N = 2304: 3 rounds instead of 4.5) +11-15 % isolated
-  if (a.wide && a.epi == 0 && wide_ok(a)) {
-    const long tiles = tm * (a.N / 384);
-    const double c = (double)((tiles + 255) / 256) * 384 / 0.97;
-    if (tiles >= 512 && c < bc) best = 20;
-  }
   return best;
 }
 
 int gemm_config(const GemmArgs& a) {
-  // producers: 96-column partials (P = ceil(N / 96) <= kLnPMax); option ln_prod256: 256x256 tiles
-  // (64-column partials) where N is whole 256-column panels and N / 64 <= kLnPMax -- the CLIP text
-  // tower's N = 512, whose third 192-column tile is one-third empty.  Decided from N only, so a
-  // row's statistics (and so its result) do not depend on the batch it runs in.
-  if (a.epi == 2) return (a.prod256 && a.N % 256 == 0 && a.N / 64 <= kLnPMax) ? 11 : 10;
-  if (a.epi == 3) return 10;
+  // producers: 256x192 tiles, 96-column partials (P = ceil(N / 96) <= kLnPMax), decided from N
+  // only, so a row's statistics (and so its result) do not depend on the batch it runs in
+  if (a.epi == 2 || a.epi == 3) return 10;
   const int f = forced_config(a);
   if (a.epi == 1) return (f == 10 || f == 11) ? f : glds_pick(a, false);
   if (f >= 0) return f;
@@ -1305,11 +1079,10 @@ int gemm_splitk_factor(const GemmArgs& a) {
   // and 16-B aligned rows for the reduction's float4 accesses
   if (a.ascale || (a.K % 256) || a.K < 512 || (a.N & 3) || (a.ldc & 3) || (a.ldr & 3)) return 1;
   if (a.no_splitk) return 1;  // handle option "gemm_splitk" = 0 (A/B tests)
-  if (a.splitk_min_k > 0 && a.K < a.splitk_min_k) return 1;  // option splitk_min_k (A/B)
   return a.K / 256;
 }
 
-int gemm_ln_tn(const GemmArgs& a) { return gemm_config(a) == 11 ? 64 : 96; }
+int gemm_ln_tn(const GemmArgs&) { return 96; }
 
 // what the lazy-LN epilogues need (the host mirrors it before choosing that path)
 static bool epi_ok(const GemmArgs& a) {
@@ -1325,30 +1098,26 @@ static bool epi_ok(const GemmArgs& a) {
 }
 
 const char* gemm_config_name(int c) {
-  static const char* names[] = {"gemm_f16<256,32,4,1>",  "gemm_f16<256,64,4,1>",  "gemm_f16<64,128,1,4>",
-                                "gemm_f16<128,128,2,2>", "gemm_glds<256,256,2,4>", "gemm_glds<256,128,4,2>",
-                                "gemm_glds<256,192,4,2>", "gemm_glds<128,192,2,2>", "gemm_glds<128,128,2,2>",
-                                "pw_conv", "gemm_glds_pipe2<256,192,4,2>", "gemm_glds_pipe2<256,256,2,4>",
-                                "gemm_ring<256,192,4,2>", "gemm_ring_dma_only", "gemm_ring_compute_only",
-                                "gemm_glds_dma_only", "gemm_glds_compute_only", "gemm_lc<256,192,8+4>", "gemm_lc_dma_only",
-                                "gemm_lc_compute_only", "gemm_glds<256,384,2,4>", "gemm_glds_pipe2<256,192,2,2>"};
+  static const char* names[kGemmConfigs] = {
+      "gemm_f16<256,32,4,1>", "gemm_f16<256,64,4,1>", "gemm_f16<64,128,1,4>", "gemm_f16<128,128,2,2>", "(removed)",
+      "gemm_glds<256,128,4,2>", "(removed)", "(removed)", "(removed)", "pw_conv", "gemm_glds_pipe2<256,192,4,2>",
+      "gemm_glds_pipe2<256,256,2,4>", "(removed)", "(removed)", "(removed)", "gemm_glds_dma_only",
+      "gemm_glds_compute_only"};
   return (c >= 0 && c < kGemmConfigs) ? names[c] : "gemm_f16<?>";
 }
 
-hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
-  if (a0.M <= 0 || a0.N <= 0 || a0.K <= 0) return hipSuccess;
-  if ((a0.K & 7) || (a0.N & 3) || (a0.lda & 7) || (a0.ldw & 7) || (a0.ldc & 3)) return hipErrorInvalidValue;
-  const GemmArgs& a = a0;
+hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return hipSuccess;
+  if ((a.K & 7) || (a.N & 3) || (a.lda & 7) || (a.ldw & 7) || (a.ldc & 3)) return hipErrorInvalidValue;
   if (a.epi != 0) {
     if (!epi_ok(a)) return hipErrorInvalidValue;
     return gemm_config(a) == 11 ? run_glds_epi<256, 256, 2, 4>(a, s) : run_glds_epi<256, 192, 4, 2>(a, s);
   }
   const int cfg = gemm_config(a);
-  if (cfg == 13 || cfg == 14) return launch_gemm_ring(a, s, cfg - 12);  // measurement builds (garbage out)
-  if (cfg >= 17 && cfg <= 19) return launch_gemm_lc(a, s, cfg - 17);
+#if MMF_GEMM_DIAG
   if (cfg == 15) return run_glds<256, 192, 4, 2, true, 1>(a, s);
   if (cfg == 16) return run_glds<256, 192, 4, 2, true, 2>(a, s);
-  if (cfg == 12) return launch_gemm_ring(a, s);
+#endif
   switch (cfg) {
     case 0: return run<256, 32, 4, 1>(a, s);
     case 1: return run<256, 64, 4, 1>(a, s);
@@ -1357,16 +1126,10 @@ hipError_t launch_gemm(const GemmArgs& a0, hipStream_t s) {
       if (S > 1 && a.ws && (size_t)S * a.M * a.N <= a.ws_elems) return run_splitk<64, 128, 1, 4>(a, S, s);
       return run<64, 128, 1, 4>(a, s);
     }
-    case 4: return run_glds<256, 256, 2, 4>(a, s);
     case 5: return run_glds<256, 128, 4, 2>(a, s);
-    case 6: return run_glds<256, 192, 4, 2>(a, s);
-    case 7: return run_glds<128, 192, 2, 2>(a, s);
-    case 8: return run_glds<128, 128, 2, 2>(a, s);
     case 9: return launch_pw(a, s);
     case 10: return run_glds<256, 192, 4, 2, true>(a, s);
     case 11: return run_glds<256, 256, 2, 4, true>(a, s);
-    case 20: return run_glds<256, 384, 2, 4>(a, s);
-    case 21: return run_glds<256, 192, 2, 2, true>(a, s);  // 4 waves, 128x96 wave tiles (A/B)
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

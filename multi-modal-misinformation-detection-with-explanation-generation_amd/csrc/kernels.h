@@ -21,23 +21,9 @@ struct GemmArgs {
   int M, N, K, act;
   int force_cfg;                 // 0 = automatic tile choice, c + 1 = instantiation c (A/B option)
   int no_splitk;                 // 1 = never split K on the skinny-M path (A/B option)
-  int splitk_min_k;              // skinny-M GEMMs split K only from this depth (0 = 512; a K-only rule)
   int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
-  int prio;                      // A/B: 1 = s_setprio 1 for the second half of the waves, 2 = first half
-  int ring;                      // 1 = plain fp16-output encoder GEMMs on the ring-pipelined kernel (gemm_ring.hip)
-  int wide;                      // 1 = 256x384 tiles may be picked (gemm.hip glds_pick)
-  int w4;                        // 1 = 192-column picks run the 4-wave tiles (config 21; A/B)
-  int max_grid;                  // > 0: persistent GEMM grids capped at this many workgroups (the CUs of a
-                                 //     CU-masked tower stream, option cu_split); 0 = 256
-  int prod256;                   // 1 = lazy-LN producers (epi 2) on 256x256 tiles where N's 64-column
-                                 //     partials fit (N % 256 == 0, N / 64 <= kLnPMax: CLIP text, N = 512)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
-  unsigned* ws_cnt;              // kSplitkCounters zeroed arrival counters next to ws (split-K reduced by
-                                 //     the last-arriving slice of each tile; null: a reduction kernel)
-  unsigned* tq;                  // option gemm_tq: kTileQueueWords zeroed words private to the launch's
-                                 //     stream (per-XCD tile counters + a finish count; the launch's last
-                                 //     workgroup zeroes them again); null: the static persistent schedule
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
   // (mean_p, M2_p) over consecutive column blocks of tn columns ([rows][P] float2, buffers padded
   // to whole 256-row blocks), combined with Chan's formula by the reader.
@@ -60,17 +46,9 @@ int gemm_ln_tn(const GemmArgs& a);
 // split-K factor the skinny-M (M <= 512) GEMM path uses for this (K) -- independent of M, so
 // results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
 int gemm_splitk_factor(const GemmArgs& a);
-constexpr int kTqStride = 64;  // gemm_tq: one counter per 256-B line (same-line atomics serialise)
-constexpr int kTileQueueWords = 9 * kTqStride;  // gemm_tq words per stream: 8 XCD counters, the finish count
-constexpr int kSplitkCounters = 1024;  // >= tiles of any split-K launch (64 x 128 tiles, M <= 512, N <= 3072)
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
-// ring-pipelined 256x192 kernel (gemm_ring.hip): epi 0, fp16 output only, bias, no residual / A scale,
-// K % 64 == 0, N % 8 == 0
-bool gemm_ring_ok(const GemmArgs& a);
-hipError_t launch_gemm_ring(const GemmArgs& a, hipStream_t s, int dbg = 0);
-hipError_t launch_gemm_lc(const GemmArgs& a, hipStream_t s, int dbg = 0);  // loader / consumer waves (same conditions)
-int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks (0..9)
-constexpr int kGemmConfigs = 22;  // tile instantiations gemm_config can return (0 .. 21)
+int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks
+constexpr int kGemmConfigs = 17;  // numbering of the tile instantiations (0 .. 16; gemm.hip config_exists)
 const char* gemm_config_name(int c);
 // streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable
 bool pw_applicable(const GemmArgs& a);
@@ -158,19 +136,17 @@ hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* b
 hipError_t launch_effnet_stem_f32(const float* x_nchw, const float* w, const float* bias, f16_t* out, int B,
                                   hipStream_t s);
 // stem fused into the stage-1 depthwise conv (3x3 s1, 32 channels at 112^2) + its SE pool partials;
-// exactly one of img (uint8 HWC) / xf32 (normalised fp32 NCHW) is non-null; wd_t (the tap-major
-// [9][32] weight copy) non-null selects the wave-per-channel-group depthwise phase (V2)
+// exactly one of img (uint8 HWC) / xf32 (normalised fp32 NCHW) is non-null
 hipError_t launch_effnet_stem_dw(const uint8_t* img, const float* xf32, const float* ws, const float* bs,
-                                 const float* wd, const float* wd_t, const float* bd, f16_t* out, float* pool_part, int B,
+                                 const float* wd, const float* bd, f16_t* out, float* pool_part, int B,
                                  int* nchunks_out, hipStream_t s);
-// ct = 0 forces the runtime-geometry kernels (A/B option "dw_ct"; the default uses the
-// compile-time tile geometries)
+// flags: bit 0 = compile-time tile geometries where one exists (runtime-geometry kernels otherwise),
+// bit 3 = 32-channel groups for C in {480, 672, 1152} (option dw_cw32)
 hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16_t* out, float* pool_part,
                          int B, int H, int W, int C, int k, int stride, int* nchunks_out, hipStream_t s, int ct = 1);
 hipError_t launch_se(const float* pool_part, int nchunks, float inv_hw, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* scale, int B, int C, int Csq, hipStream_t s,
-                     bool precise = false, int group = 0);  // precise: the fc1 SiLU in silu_precise form (fp32
-                                                             // tower); group 8: se_group_kernel (8 images a block)
+                     bool precise = false);  // precise: the fc1 SiLU in silu_precise form (fp32 tower)
 hipError_t launch_gap_classifier(const f16_t* x, int HW, int C, const float* w, const float* b, float* logits,
                                  float* score, int score_stride, int B, hipStream_t s);
 hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);
@@ -216,8 +192,6 @@ hipError_t launch_pw32(const float* A, const float* W, const float* bias, const 
 hipError_t launch_dw32(const float* in, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                        int k, int stride, hipStream_t s);
 // part[b][j][c] = sum over pixel chunk j of nchunks (the SE's pool partials)
-hipError_t launch_expand_dw32(const float* in, const float* we, const float* be, const float* wd, const float* bd,
-                              float* out, int B, int H, int W, int cin, int cexp, int k, int stride, hipStream_t s);
 hipError_t launch_sum32(const float* x, int B, int HW, int C, int nchunks, float* part, hipStream_t s);
 hipError_t launch_gap32(const float* x, int HW, int C, const float* w, const float* b, float* logits, float* score,
                         int score_stride, int B, hipStream_t s);

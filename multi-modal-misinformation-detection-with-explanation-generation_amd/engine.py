@@ -26,8 +26,13 @@ def _as_np(v) -> np.ndarray:
 class Engine:
     """MI355X replica of the MisinfoForensics models on one device."""
 
+    EFFNET_PRECISIONS = ("auto", "fp16", "fp32")
+
     def __init__(self, device: int = 0, detector_state=None, clip_state=None, eos_token_id: int = 49407,
-                 max_batch: int = 256, max_text_len: int = 128, max_clip_len: int = 77):
+                 max_batch: int = 256, max_text_len: int = 128, max_clip_len: int = 77,
+                 effnet_precision: str = "auto"):
+        if effnet_precision not in self.EFFNET_PRECISIONS:
+            raise ValueError(f"effnet_precision must be one of {self.EFFNET_PRECISIONS}, got {effnet_precision!r}")
         self.lib = hip.load()
         self.device = torch.device("cuda", device)
         torch.cuda.set_device(self.device)
@@ -35,16 +40,19 @@ class Engine:
         check(self.lib.mmf_create(device, ctypes.byref(h)), "mmf_create")
         self.h = h
         self.eos_token_id = eos_token_id
+        self.effnet_precision = effnet_precision
+        self.effnet_check = None
+        self.clip_stream_check = None
+        self.vault_n = 0
         if detector_state is not None:
             self.load_state(detector_state, "")
         if clip_state is not None:
             self.load_state(clip_state, "clip.")
         self.finalize()
         self.reserve(max_batch, max_text_len, max_clip_len)
-        self.vault_n = 0
-        self.clip_stream_check = None
         if clip_state is not None:
             self.check_clip_streams()
+        self.calibrate(("effnet",) if detector_state is not None else ())
 
     # ------------------------------------------------------------------ weights
     def load_state(self, state: Dict, prefix: str = "") -> None:
@@ -103,6 +111,62 @@ class Engine:
             self.set_option("clip_res16", 1)
         self.clip_stream_check = {"max_dcos": dcos, "max_demb": demb, "fp16_streams": ok, "rows": n}
         return self.clip_stream_check
+
+    def clip_stream_overflow(self, *outputs: torch.Tensor) -> bool:
+        """Run-time overflow trap of the fp16 CLIP streams: the load-time calibration
+        measures 8 seeded inputs, so it bounds nothing for later ones.  An input that drives a
+        stream past fp16's range turns the embedding non-finite, and clip_similarity / the vault
+        scores with it.  The synchronous API paths (which read their results back anyway) pass
+        their CLIP outputs here: if fp16 streams are selected and any value is non-finite, the
+        engine switches to fp32 streams for good and returns True, and the caller re-runs the
+        batch.  Drift short of overflow is what the calibration alone covers."""
+        if self.get_option("clip_res16") != 1:
+            return False
+        if all(bool(torch.isfinite(v).all()) for v in outputs if v is not None):
+            return False
+        self.set_option("clip_res16", 0)
+        self.clip_stream_check = dict(self.clip_stream_check or {}, fp16_streams=False, runtime_overflow=True)
+        return True
+
+    # fp16 EfficientNet tower: largest tolerated change of deepfake_score against the fp32 tower on
+    # the calibration images (half the north-star bar; the ordinary draw measures ~1e-4 over 256)
+    EFFNET_TOL = 5e-4
+
+    def calibrate(self, components=("effnet",)) -> None:
+        """Load-time precision selection for re-packed components (called at construction and by
+        the detector's sync after every re-pack: trained weights reach the engine through
+        misinfo_forensics.py:175-186 / 285-303 after construction)."""
+        if "effnet" in components and self.ready & 2:
+            self.check_effnet_precision()
+
+    def check_effnet_precision(self, n: int = 64) -> dict:
+        """Load-time guard of the fp16 EfficientNet tower (the counterpart of
+        check_clip_streams).  A BN-conditioned tower is insensitive to fp16 activation storage; a
+        chaotic one (logits of O(100): He-gain draws) amplifies it to O(0.1).  With
+        effnet_precision "auto" both towers run on n seeded calibration images; if any deepfake_score
+        is non-finite or moves by more than EFFNET_TOL, the fp32 tower stays selected.  "fp16" /
+        "fp32" pin the tower without measuring.  Returns (and keeps as `effnet_check`) the result."""
+        from . import synthetic as syn
+        if self.effnet_precision != "auto":
+            self.set_option("effnet_fp32", int(self.effnet_precision == "fp32"))
+            self.effnet_check = {"tower": self.effnet_precision, "calibrated": False}
+            return self.effnet_check
+        n = max(1, n)
+        imgs = torch.from_numpy(syn.images(n, 5003)).to(self.device)
+
+        def scores(fp32: int):
+            self.set_option("effnet_fp32", fp32)
+            out = []
+            for i in range(0, n, self.max_batch):
+                out.append(self.effnet_forward(imgs[i:i + self.max_batch])[1].double())
+            return torch.cat(out)
+        s16, s32 = scores(0), scores(1)
+        finite = bool(torch.isfinite(s16).all())
+        d = float((s16 - s32).abs().max()) if finite else float("inf")
+        ok = finite and d <= self.EFFNET_TOL
+        self.set_option("effnet_fp32", 0 if ok else 1)
+        self.effnet_check = {"max_ddeepfake": d, "tower": "fp16" if ok else "fp32", "images": n, "calibrated": True}
+        return self.effnet_check
 
     # ------------------------------------------------------------------ options / accounting
     def set_option(self, name: str, value: int) -> None:
@@ -181,12 +245,19 @@ class Engine:
         return eff, clp
 
     # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _tensor(x) -> torch.Tensor:
+        # a read-only numpy view (an Arrow / PIL export, np.broadcast_to) is copied rather than
+        # wrapped: torch cannot wrap non-writable memory without a UserWarning per process
+        if isinstance(x, np.ndarray) and not x.flags.writeable:
+            x = x.copy()
+        return torch.as_tensor(x)
+
     def _i32(self, x) -> torch.Tensor:
-        t = torch.as_tensor(x)
-        return t.to(self.device, torch.int32).contiguous()
+        return self._tensor(x).to(self.device, torch.int32).contiguous()
 
     def _u8(self, x) -> torch.Tensor:
-        t = torch.as_tensor(x)
+        t = self._tensor(x)
         if not (t.dtype == torch.uint8 and t.dim() == 4 and tuple(t.shape[1:]) == (224, 224, 3)):
             raise ValueError(f"images must be uint8 [B,224,224,3], got {tuple(t.shape)} {t.dtype}")
         return t.to(self.device).contiguous()

@@ -60,18 +60,17 @@ def kind_symbol(kind: str) -> str:
         return kind
     dims = m.group(2).split(",")
     epi = m.group(4) or "0"
-    # (then the measurement-build selector DBG, 0 in production, and TQ, the tile-queue variant of
-    # option gemm_tq, false by default)
+    # (then the measurement-build selector DBG, 0 in production)
     if m.group(1) == "glds":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi, '0', 'false'])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'false', epi, '0'])}>"
     if m.group(1) == "glds_pipe2":
-        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi, '0', 'false'])}>"
+        return f"gemm_glds_kernel<{', '.join(dims + [m.group(3), 'true', epi, '0'])}>"
     return f"gemm_f16_kernel<{', '.join(dims)}, 1, false>"  # (PF, ASC: plain launches)
 
 
 def same_kernel(a: str, b: str) -> bool:
-    """Symbols equal up to gemm_glds_kernel's trailing TQ = false (summaries from before the
-    template argument existed print 8 arguments)."""
+    """Symbols equal up to gemm_glds_kernel's trailing TQ = false (round 4's library had a ninth
+    template argument, the tile-queue variant; its PMC summaries print 9 arguments)."""
     def norm(s):
         return re.sub(r"^(gemm_glds_kernel<(?:[^,<>]+, ){7}[^,<>]+), false>$", r"\1>", s)
     return norm(a) == norm(b)
@@ -101,7 +100,11 @@ def kernel_roofline(eng, step: Callable[[], None], steps: int) -> Dict:
         ach, peak, unit = dom["gbs"], PEAK_HBM_GBS, "GB/s"
     total = sum(r["ms_per_step"] for r in rows)
     return {"bound": dom["bound"], "kernel": dom["kernel"], "achieved": round(ach, 1), "peak": peak,
-            "unit": unit, "frac": round(ach / peak, 4), "traffic": pmc_traffic(kind_symbol(dom["kernel"])),
+            "unit": unit, "frac": round(ach / peak, 4),
+            # the library prices every launch by its own (M, N, K), so the dominant kernel's
+            # algorithmic work IS what it executes (the compact last layers are separate launches)
+            "executed_frac": round(ach / peak, 4),
+            "traffic": pmc_traffic(kind_symbol(dom["kernel"])),
             "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
             "symbol": kind_symbol(dom["kernel"]),
             "avg_launch_us": round(dom["avg_launch_us"], 2),

@@ -82,7 +82,7 @@ class _RecordingEngine:
     """Stands in for the device engine: records what the detector stages and finalizes."""
 
     def __init__(self):
-        self.staged, self.finalized = [], 0
+        self.staged, self.finalized, self.calibrated = [], 0, []
 
     def load_state(self, sd, prefix=""):
         self.staged.append(sorted(sd))
@@ -90,12 +90,17 @@ class _RecordingEngine:
     def finalize(self):
         self.finalized += 1
 
+    def calibrate(self, components):
+        self.calibrated.append(list(components))
+
 
 def test_detector_change_tracking():
     det = _detector()
     eng = _RecordingEngine()
     det.bind(eng)
     assert det.uploads == {"text": 1, "effnet": 1, "fusion": 1} and eng.finalized == 1
+    # every re-pack is followed by the load-time precision calibration of exactly those components
+    assert eng.calibrated == [["text", "effnet", "fusion"]]
     assert det.sync() == [] and det.stale_components() == []
     t0 = time.perf_counter()
     for _ in range(20):

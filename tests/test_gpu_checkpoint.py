@@ -134,13 +134,14 @@ def test_reload_cycles_keep_device_memory_flat(det_sd, clip_sd, trained):
     mf.engine.close()
 
 
-@pytest.mark.parametrize("gain,fp32", [(1.3, 0), (1.3, 1), (2 ** 0.5, 1)])
+@pytest.mark.parametrize("gain,fp32", [(1.3, None), (1.3, 1), (2 ** 0.5, None)])
 def test_full_size_bench_workload_vs_oracle(clip_sd, gain, fp32):
     """All 256 rows of the benchmark's workload (B = 256, L = 128 text, 77-token captions, 224^2
     images, the bench's planted vault) against the fp32 oracle, with the default EfficientNet draw
     and with He fan_in convs (gain sqrt 2, logits of O(100): DESIGN.md §4 -- fp16 activation
-    storage is amplified to ~0.4 there, so that draw runs the fp32 tower, option effnet_fp32).
-    Prints the max |delta| per score."""
+    storage is amplified to ~0.4 there).  fp32 = None: DEFAULT options, so the tower is the one the
+    load-time calibration picks (Engine.check_effnet_precision: fp16 on the default draw, the fp32
+    tower on the He draw).  Prints the max |delta| per score."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import mmf_amd.synthetic as syn
@@ -150,7 +151,13 @@ def test_full_size_bench_workload_vs_oracle(clip_sd, gain, fp32):
     det = W.synthetic_detector_state(0, effnet_gain=gain)
     Bf = 256
     eng = Engine(0, det, clip_sd, max_batch=Bf)
-    eng.set_option("effnet_fp32", fp32)
+    print(f"EfficientNet calibration: {eng.effnet_check}")
+    if fp32 is None:
+        assert eng.effnet_check["calibrated"]
+        assert eng.get_option("effnet_fp32") == (1 if gain > 1.3 else 0)
+        fp32 = eng.get_option("effnet_fp32")
+    else:
+        eng.set_option("effnet_fp32", fp32)
     rid, rm = syn.roberta_ids(Bf, 128, 1234)
     cid, cm = syn.clip_ids(Bf, 77, 1234)
     imgs = syn.images(Bf, 1234)
@@ -188,3 +195,29 @@ def test_full_size_bench_workload_vs_oracle(clip_sd, gain, fp32):
               f"fp32 oracle {np.abs(ref['scores'][:, 2] - p64).max():.2e}")
         np.testing.assert_allclose(got["scores"][:, 2], p64, atol=TOL)
     eng.close()
+
+
+def test_effnet_calibration_follows_reloads(det_sd, clip_sd):
+    """Default constructor options (effnet_precision "auto"): the EfficientNet tower is re-chosen at
+    every re-pack of the detector's EfficientNet -- a reloaded
+    `full_model_state_dict` with an ill-conditioned (He-gain) tower switches the engine to the fp32
+    tower and meets the bar against the oracle on the LOADED weights; reloading ordinary weights
+    switches back to the fp16 tower."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.weights as W
+    inp = _inputs()
+    mf = _mf(det_sd, clip_sd, "/nonexistent")
+    assert mf.engine.effnet_check["tower"] == "fp16", mf.engine.effnet_check
+    he = W.synthetic_detector_state(0, effnet_gain=2 ** 0.5)
+    det = mf.detector
+    det.load_state_dict({k: torch.as_tensor(v) for k, v in he.items()})
+    det.sync()
+    print(f"He-gain reload: {mf.engine.effnet_check}")
+    assert mf.engine.effnet_check["tower"] == "fp32" and mf.engine.get_option("effnet_fp32") == 1
+    _check(mf, _oracle(he, clip_sd, inp), inp, "He-gain EfficientNet reload")
+    det.load_state_dict({k: torch.as_tensor(v) for k, v in det_sd.items()})
+    det.sync()
+    assert mf.engine.effnet_check["tower"] == "fp16" and mf.engine.get_option("effnet_fp32") == 0
+    _check(mf, _oracle(det_sd, clip_sd, inp), inp, "ordinary reload")
+    mf.engine.close()

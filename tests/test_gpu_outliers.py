@@ -223,6 +223,61 @@ def test_dominating_gamma_channel_selects_split_stream(det_sd, clip_sd, gamma_ou
     eng.close()
 
 
+def overflow_clip_state(clip_sd, step=7000.0):
+    """FFN-2 biases of +`step` per layer in 2 text-tower channels: the pre-LN stream passes fp16's
+    range (~8e4) by the last layer."""
+    clip = {k: np.array(v, copy=True) for k, v in clip_sd.items()}
+    c, H = list(TXT_CH), 512
+    nm = np.ones(H, bool)
+    nm[c] = False
+    for i in range(12):
+        p = f"text_model.encoder.layers.{i}."
+        clip[p + "mlp.fc2.bias"][c] += step
+        g = max(1.0, step * i * np.sqrt(len(c) / H))
+        for ln in ("layer_norm1", "layer_norm2"):
+            clip[p + ln + ".weight"][nm] *= g
+            clip[p + ln + ".weight"][c] = 0.05
+    clip["text_model.final_layer_norm.weight"][nm] *= step * 12 * np.sqrt(len(c) / H)
+    clip["text_model.final_layer_norm.weight"][c] = 0.05
+    return clip
+
+
+def test_clip_runtime_overflow_trap(det_sd, clip_sd):
+    """the load-time CLIP calibration is a measurement on 8 inputs, not a bound.  If an
+    input overflows the fp16 streams after it passed (simulated here by forcing clip_res16 = 1 on the
+    overflow draw), the synchronous API paths see the non-finite CLIP output, switch the engine to
+    fp32 streams and re-run: analyze_pairs / analyze_consistency return the fp32-stream values."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mmf_amd.synthetic as syn
+    from mmf_amd.api import MisinfoForensics
+    clip = overflow_clip_state(clip_sd)
+    n = 6
+    texts, rob, clp = syn.text_tables(n, 91)
+    from PIL import Image
+    imgs = [Image.fromarray(a) for a in syn.images(n, 91)]
+
+    def mk():
+        return MisinfoForensics(fusion_weights="", faiss_index_path="", detector_state=det_sd, clip_state=clip,
+                                roberta_tokenizer=rob, clip_processor=clp, max_batch=8, verbose=False)
+    ref = mk()
+    assert ref.engine.get_option("clip_res16") == 0  # the calibration catches this draw
+    want = [d["scores"]["clip_similarity"] for d in ref.analyze_pairs(texts, imgs)]
+    want1 = ref.analyze_consistency(texts[0], imgs[0])["clip_similarity"]
+    ref.engine.close()
+    mf = mk()
+    mf.engine.set_option("clip_res16", 1)  # as if the calibration inputs had not overflowed
+    got = [d["scores"]["clip_similarity"] for d in mf.analyze_pairs(texts, imgs)]
+    print(f"runtime trap: {mf.engine.clip_stream_check}")
+    assert mf.engine.get_option("clip_res16") == 0 and mf.engine.clip_stream_check["runtime_overflow"]
+    assert np.isfinite(got).all()
+    np.testing.assert_allclose(got, want, atol=1e-6)
+    mf.engine.set_option("clip_res16", 1)
+    got1 = mf.analyze_consistency(texts[0], imgs[0])["clip_similarity"]
+    assert np.isfinite(got1) and abs(got1 - want1) < 1e-6 and mf.engine.get_option("clip_res16") == 0
+    mf.engine.close()
+
+
 def test_clip_stream_overflow_selects_fp32_streams(det_sd, clip_sd):
     """CLIP's pre-LN streams have no parameter bound, so the engine measures them at load
     (Engine.check_clip_streams).  A draw whose text-tower stream passes fp16's range (FFN-2 biases
@@ -238,19 +293,7 @@ def test_clip_stream_overflow_selects_fp32_streams(det_sd, clip_sd):
     print(f"plain draw: {chk}")
     assert chk["fp16_streams"] and plain.get_option("clip_res16") == 1
     plain.close()
-    clip = {k: np.array(v, copy=True) for k, v in clip_sd.items()}
-    c, H, step = list(TXT_CH), 512, 7000.0
-    nm = np.ones(H, bool)
-    nm[c] = False
-    for i in range(12):
-        p = f"text_model.encoder.layers.{i}."
-        clip[p + "mlp.fc2.bias"][c] += step
-        g = max(1.0, step * i * np.sqrt(len(c) / H))
-        for ln in ("layer_norm1", "layer_norm2"):
-            clip[p + ln + ".weight"][nm] *= g
-            clip[p + ln + ".weight"][c] = 0.05
-    clip["text_model.final_layer_norm.weight"][nm] *= step * 12 * np.sqrt(len(c) / H)
-    clip["text_model.final_layer_norm.weight"][c] = 0.05
+    clip = overflow_clip_state(clip_sd)
     Bf = 64
     eng = Engine(0, det_sd, clip, max_batch=Bf)
     chk = eng.clip_stream_check

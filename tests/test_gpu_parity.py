@@ -87,30 +87,6 @@ def test_fp32_tower_mfma_pointwise_bit_identical(det_sd, clip_sd):
         eng.close()
 
 
-def test_fp32_tower_fused_fronts_bit_identical(det_sd, clip_sd):
-    """The fp32 tower's fused expand + depthwise fronts (option fuse_expand32 = 1, round 4, off by
-    default -- slower, DESIGN.md §4: stages 2.1 - 4.1, the expanded tensor kept in LDS) against the
-    separate pw32m + dw32 launches:
-    every logit bit-identical, on the ill-conditioned He draw (a reordered sum would show there), at
-    a batch whose tiles include ragged edges (56 / 8, 28 / 7 and 14 / 7 tiles, halos past the image)."""
-    import mmf_amd.synthetic as syn
-    import mmf_amd.weights as W
-    from mmf_amd.engine import Engine
-    eng = Engine(0, W.synthetic_detector_state(0, effnet_gain=2 ** 0.5), None, max_batch=48)
-    try:
-        eng.set_option("effnet_fp32", 1)
-        imgs = syn.images(48, 31)
-        eng.set_option("fuse_expand32", 0)
-        lg0, _ = eng.effnet_forward(imgs)
-        eng.set_option("fuse_expand32", 1)
-        lg1, _ = eng.effnet_forward(imgs)
-        torch.cuda.synchronize()
-        assert torch.isfinite(lg1).all()
-        assert torch.equal(lg0, lg1), (lg0 - lg1).abs().max().item()
-    finally:
-        eng.close()
-
-
 @pytest.mark.parametrize("B", [3, 37])
 def test_compact_last_layer_queries(engine, B):
     """Option last_q1 (round 4): the last encoder layer computes K / V for every row but Q and the
@@ -264,39 +240,6 @@ def test_fused_stem_dwconv_matches_separate(engine):
         np.testing.assert_allclose(f1.cpu().numpy(), f0.cpu().numpy(), atol=TOL)
 
 
-def test_compile_time_dwconv_matches_runtime_geometry(engine):
-    """Depthwise kernels with compile-time tile geometry and output runs (dw_compute_ct, the
-    default) vs the runtime-geometry kernels (option dw_ct = 0).  Conv outputs are computed in the same
-    order; the SE pool partial sums are grouped differently, and those 1-ulp differences flip fp16
-    roundings downstream, so the comparison is at the north-star tolerance on deepfake_score (both
-    paths are also checked against the fp32 oracle by test_effnet_signal for the default)."""
-    import mmf_amd.synthetic as syn
-    imgs = syn.images(64, 19)
-    engine.set_option("dw_ct", 0)
-    _, s0 = engine.effnet_forward(imgs)
-    engine.set_option("dw_ct", 1)
-    _, s1 = engine.effnet_forward(imgs)
-    torch.cuda.synchronize()
-    np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
-
-
-def test_dw_v2_matches_v1(engine):
-    """Depthwise phases with one channel group per wave and SGPR weights (option dw_v2) vs
-    the thread-per-(channel group, run) phases (dw_v2 = 0, default).  The conv taps accumulate in the same
-    order and round to fp16 the same way, so the stage outputs are bit-identical; only the SE pool
-    partial sums are grouped differently (cross-lane butterfly vs LDS slots), a last-bit effect that
-    can flip later fp16 roundings -- compared at the north-star tolerance on deepfake_score."""
-    import mmf_amd.synthetic as syn
-    imgs = syn.images(64, 29)
-    engine.set_option("dw_v2", 0)
-    lg0, s0 = engine.effnet_forward(imgs)
-    engine.set_option("dw_v2", 1)
-    lg1, s1 = engine.effnet_forward(imgs)
-    torch.cuda.synchronize()
-    np.testing.assert_allclose(s1.cpu().numpy(), s0.cpu().numpy(), atol=TOL)
-    np.testing.assert_allclose(lg1.cpu().numpy(), lg0.cpu().numpy(), atol=2e-2)
-
-
 def test_long_text_up_to_512(det_sd, clip_sd):
     """RoBERTa inputs past 128 tokens (the reference truncates at 512, misinfo_forensics.py:327-333):
     each padded row must score like the oracle's unpadded single-text analyze_text."""
@@ -435,33 +378,6 @@ def test_qkv_attention_epilogue_bit_identical(det_sd, B, lengths, last_q1):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
 
 
-@pytest.mark.parametrize("B", [1, 3, 37, 256])
-def test_splitk_last_arriver_reduction_bit_identical(det_sd, clip_sd, B):
-    """Split-K GEMMs (skinny M: the compact last layers at every batch size, whole encoders at
-    B <= 4) reduced by the last-arriving slice of each tile (gemm.hip splitk_fixup: write-through
-    partials, agent-scope arrival counter, acquire) against the separate reduction kernel (option
-    splitk_fix = 0): bit-identical text heads and CLIP embeddings, repeated calls included (the
-    counters are reset by their last arrivers)."""
-    if not torch.cuda.is_available():
-        pytest.skip("no HIP device")
-    import mmf_amd.synthetic as syn
-    from mmf_amd.engine import Engine
-    eng = Engine(0, det_sd, clip_sd, max_batch=256)
-    rid, rm = syn.roberta_ids(B, 128, 21, [128, 77, 9, 128, 40])
-    cid, cm = syn.clip_ids(B, 77, 21, [77, 12, 40])
-    imgs = syn.images(B, 21)
-    outs = {}
-    for fix in (0, 1, 1):
-        eng.set_option("splitk_fix", fix)
-        res = list(eng.text_forward(rid, rm)) + [eng.clip_image(imgs), eng.clip_text(cid, cm)]
-        torch.cuda.synchronize()
-        outs.setdefault(fix, []).append([t.clone() for t in res])
-    ref = outs[0][0]
-    for run in outs[1]:
-        for a, b in zip(ref, run):
-            assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
-
-
 @pytest.mark.parametrize("B", [1, 4, 8])
 def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
     """Small batches with the towers enqueued by host threads side by side (option mt_enqueue:
@@ -489,59 +405,3 @@ def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
                 assert torch.equal(v, out[k]), k
     finally:
         engine.set_option("mt_enqueue", mt)
-
-
-@pytest.mark.parametrize("B", [37, 256])
-def test_tile_queue_bit_identical(engine, B):
-    """Persistent GEMMs that take their tiles after the first from per-XCD queues (option gemm_tq:
-    an agent-scope ticket per tile, the launch's last workgroup zeroes the words for the stream's
-    next launch) against the static schedule: the same tiles with the same arithmetic, so every
-    output of analyze_batch and clip_consistency is bit-identical, over repeated calls on the four
-    tower streams (a ticket word left non-zero would skip or repeat tiles in the next launch)."""
-    import mmf_amd.synthetic as syn
-    rid, rm = syn.roberta_ids(B, 128, 41, [128, 77, 9, 128, 40])
-    cid, cm = syn.clip_ids(B, 77, 41, [77, 12, 40])
-    imgs = syn.images(B, 41)
-
-    def run():
-        out = {k: v.clone() for k, v in engine.analyze_batch(rid, rm, cid, cm, imgs).items()}
-        out.update({"cons_" + k: v.clone() for k, v in engine.clip_consistency(imgs, cid, cm).items()})
-        torch.cuda.synchronize()
-        return out
-
-    tq = engine.get_option("gemm_tq")
-    try:
-        engine.set_option("gemm_tq", 0)
-        ref = run()
-        engine.set_option("gemm_tq", 1)
-        for _ in range(4):
-            out = run()
-            for k, v in ref.items():
-                assert torch.equal(v, out[k]), k
-    finally:
-        engine.set_option("gemm_tq", tq)
-
-
-@pytest.mark.parametrize("fp32", [False, True])
-@pytest.mark.parametrize("B", [13, 256])
-def test_se_image_groups_bit_identical(B, fp32):
-    """EfficientNet squeeze-excitation with 8 images per block (option se_group, every SE weight
-    fetched once per 8 images) against one image per block: the same per-image arithmetic in the
-    same order, so bit-identical logits -- a batch that is not a multiple of 8 included, fp16 and
-    fp32 towers."""
-    if not torch.cuda.is_available():
-        pytest.skip("no HIP device")
-    import mmf_amd.synthetic as syn
-    import mmf_amd.weights as W
-    from mmf_amd.engine import Engine
-    eng = Engine(0, W.synthetic_detector_state(0, effnet_gain=2 ** 0.5), None, max_batch=256)
-    eng.set_option("effnet_fp32", 1 if fp32 else 0)
-    imgs = syn.images(B, 41)
-    res = {}
-    for grp in (0, 8):
-        eng.set_option("se_group", grp)
-        lg, sc = eng.effnet_forward(imgs)
-        torch.cuda.synchronize()
-        res[grp] = (lg.clone(), sc.clone())
-    assert torch.equal(res[0][0], res[8][0]), (res[0][0] - res[8][0]).abs().max().item()
-    assert torch.equal(res[0][1], res[8][1])

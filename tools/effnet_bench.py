@@ -1,6 +1,6 @@
 """EfficientNet-B0 tower alone (B images, synthetic weights/inputs) for per-kernel profiling:
 
-    python tools/effnet_bench.py [--batch 256 --iters 10] [--ab dw_v2=0 dw_v2=1 --rounds 5] [--opt effnet_chunks=1]
+    python tools/effnet_bench.py [--batch 256 --iters 10] [--ab dw_cw32=0 dw_cw32=1 --rounds 5] [--opt effnet_chunks=1]
     rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES ... -- python tools/effnet_bench.py --iters 2
 """
 import argparse

@@ -1,6 +1,6 @@
 """Micro-benchmark of libmmf_hip's fp16 GEMM on the encoder shapes of the hot path.
 
-    python tools/gemm_bench.py [--configs auto,4,6] [--iters 20] [--round] [--effnet]
+    python tools/gemm_bench.py [--configs auto,10,11] [--iters 20] [--round] [--effnet]
 
 Prints TFLOP/s (TB/s for the EfficientNet 1x1 convolutions) per (shape, tile config), measured with
 HIP events on the stream the kernel is launched on; the process option "gemm_config"
@@ -81,7 +81,7 @@ def effnet(a, lib, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="auto,3,4,5,6")
+    ap.add_argument("--configs", default="auto,3,5,10,11")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--kscale", default="", help="comma list of K multipliers to time (fixed-cost probe)")
     ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
