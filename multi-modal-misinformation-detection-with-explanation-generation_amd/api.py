@@ -338,9 +338,11 @@ class MisinfoForensics:
                  device: str = "cuda",
                  *, roberta_tokenizer=None, clip_processor=None, detector_state=None, clip_state=None,
                  synthetic_seed: Optional[int] = None, max_batch: int = 256, max_text_len: int = 128,
-                 effnet_precision: str = "auto", verbose: bool = True):
+                 effnet_precision: str = "auto", text_precision: str = "auto", verbose: bool = True):
         if effnet_precision not in Engine.EFFNET_PRECISIONS:
             raise ValueError(f"effnet_precision must be one of {Engine.EFFNET_PRECISIONS}, got {effnet_precision!r}")
+        if text_precision not in Engine.TEXT_PRECISIONS:
+            raise ValueError(f"text_precision must be one of {tuple(Engine.TEXT_PRECISIONS)}, got {text_precision!r}")
         self.device = _require_hip(device)
         self._verbose = verbose
         self._log(f"Using device: {self.device}")
@@ -395,11 +397,14 @@ class MisinfoForensics:
         self.detector.eval()
 
         self.clip_eos_token_id = clip_eos_token_id(clip_model_dir)
-        # effnet_precision "auto" (default): the fp32-activation tower is selected at
-        # every EfficientNet (re)load when the fp16 tower's deepfake_score moves by more than 5e-4 on
-        # the calibration images (Engine.check_effnet_precision); "fp16" / "fp32" pin the tower
+        # effnet_precision / text_precision "auto" (default): at every (re)load of the component the
+        # engine measures its fast path against its precision fallback on seeded calibration inputs
+        # and keeps the fallback when a score moves by more than 5e-4 (the fp32
+        # EfficientNet tower; RoBERTa's precise mode, Engine.check_text_precision); the other values
+        # pin the mode
         self.engine = Engine(self.device.index or 0, None, clip_state, eos_token_id=self.clip_eos_token_id,
-                             max_batch=max_batch, max_text_len=max_text_len, effnet_precision=effnet_precision)
+                             max_batch=max_batch, max_text_len=max_text_len, effnet_precision=effnet_precision,
+                             text_precision=text_precision)
         self.detector.bind(self.engine)  # uploads RoBERTa + heads, EfficientNet, FusionJudge
         self.clip_state = clip_state
 

@@ -79,6 +79,9 @@ struct EncLayer {
   Lin16 qkv_f, fc1_f;
   float *qkv_u = nullptr, *fc1_u = nullptr;
   Lin16 qkv_h;  // RoBERTa: the fused QKV with rows interleaved per head, [q_h; k_h; v_h] (gemm.hip epi 3)
+  // RoBERTa precise mode (text_hilo = 2, precise.hip): [W_hi | W_hi | W_lo] along K (in = 3 K), the
+  // bias shared with the fp16 copy
+  Lin16 qkv3, o3, fc13, fc23;
 };
 
 struct EffBlock {
@@ -115,6 +118,12 @@ struct Workspace {
   // fp32 EfficientNet activations (option effnet_fp32), allocated on first use for cap_b images
   float *e32_a = nullptr, *e32_b = nullptr, *e32_exp = nullptr, *e32_dw = nullptr;
   int e32_cap_b = 0;
+  // RoBERTa precise mode (text_hilo = 2, group AG_TEXT32, allocated while the mode is selected): the
+  // fp32 qkv / FFN hidden [rows][3072], the K-concatenated operands of the stream / ctx [rows][2304]
+  // and of the FFN hidden [rows][9216]
+  float* p32 = nullptr;
+  f16_t *s3 = nullptr, *h3 = nullptr;
+  size_t t32_rows = 0;
   // split-K partials of the skinny-M GEMMs, one per tower (the towers run on concurrent streams)
   float *sk_text = nullptr, *sk_vit = nullptr, *sk_ctext = nullptr;
   size_t sk_elems = 0;
@@ -185,7 +194,10 @@ void apply_options(const Options& o, GemmArgs* g) {
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the
 // workspaces) frees exactly what it replaces.
-enum AllocGroup { AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_EFF32, AG_RESIZE, AG_COUNT };
+enum AllocGroup {
+  AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_EFF32, AG_RESIZE, AG_TEXT32,
+  AG_COUNT
+};
 
 }  // namespace
 
@@ -272,6 +284,7 @@ struct mmf_handle {
   // the split stream it selects under text_hilo = -1 (finalize_text)
   float r_stream_mag = 0.f;
   int r_hilo_auto = 0;
+  int r_precise = 0;  // the precise-mode weights (EncLayer qkv3 ...) are packed
   float *h_w1a = nullptr, *h_b1a = nullptr, *h_w2a = nullptr, *h_b2a = nullptr;
   float *h_w1m = nullptr, *h_b1m = nullptr, *h_w2m = nullptr, *h_b2m = nullptr;
   // EfficientNet
@@ -417,6 +430,25 @@ int up_f16(mmf_handle* h, f16_t** dst, const std::vector<float>& v) {
   return upload(h, dst, b);
 }
 
+// W [out][in] fp32 -> [W_hi | W_hi | W_lo] fp16 [out][3 in] (precise.hip: the K-concatenated weight)
+int up_split3(mmf_handle* h, Lin16* dst, const std::vector<float>& w, const float* bias, int out, int in) {
+  std::vector<uint16_t> b((size_t)out * 3 * in);
+  for (int n = 0; n < out; ++n)
+    for (int k = 0; k < in; ++k) {
+      const float x = w[(size_t)n * in + k];
+      const uint16_t hi = f2h_host(x);
+      uint16_t* r = b.data() + (size_t)n * 3 * in;
+      r[k] = hi;
+      r[in + k] = hi;
+      r[2 * in + k] = f2h_host(x - h2f_host(hi));
+    }
+  CHK(upload(h, &dst->w, b));
+  dst->b = const_cast<float*>(bias);
+  dst->out = out;
+  dst->in = 3 * in;
+  return 0;
+}
+
 const HostT* get(mmf_handle* h, const std::string& name, size_t numel) {
   auto it = h->staged.find(name);
   if (it == h->staged.end()) {
@@ -454,12 +486,13 @@ int load_ln(mmf_handle* h, LNp* ln, const std::string& p, int n) {
   CHK(load_f32_padded(h, &ln->g, p + ".weight", n));
   return load_f32_padded(h, &ln->b, p + ".bias", n);
 }
-int load_lin(mmf_handle* h, Lin16* l, const std::string& p, int out, int in, bool bias) {
+int load_lin(mmf_handle* h, Lin16* l, const std::string& p, int out, int in, bool bias, Lin16* split3 = nullptr) {
   GET(w, p + ".weight", (size_t)out * in);
   CHK(up_f16(h, &l->w, w->f));
   if (bias) CHK(load_f32_padded(h, &l->b, p + ".bias", out));
   l->out = out;
   l->in = in;
+  if (split3) CHK(up_split3(h, split3, w->f, l->b, out, in));
   return 0;
 }
 // LN(x) W^T + b with LN = (gamma, beta) folded (gemm.hip lazy LN): w' = fp16(w diag(gamma)),
@@ -497,7 +530,7 @@ int fold_ln_named(mmf_handle* h, Lin16* dst, float** u, const std::string& lin, 
 // fused QKV: rows [q; k; v] of [3*H][H] + bias; with ln (non-empty) also the LN-folded copy; with
 // heads also the per-head interleaved copy qkv_h (row 192 h + 64 part + d = row H part + 64 h + d)
 int load_qkv(mmf_handle* h, EncLayer* L, const std::string& q, const std::string& k, const std::string& v, int H,
-             const std::string& ln, bool heads = false) {
+             const std::string& ln, bool heads = false, bool split3 = false) {
   Lin16* l = &L->qkv;
   std::vector<float> w((size_t)3 * H * H), b((size_t)3 * H);
   const std::string names[3] = {q, k, v};
@@ -511,6 +544,7 @@ int load_qkv(mmf_handle* h, EncLayer* L, const std::string& q, const std::string
   CHK(up_f32_padded(h, &l->b, b));
   l->out = 3 * H;
   l->in = H;
+  if (split3) CHK(up_split3(h, &L->qkv3, w, l->b, 3 * H, H));
   if (heads) {
     std::vector<float> wh(w.size()), bh(b.size());
     for (int hd = 0; hd < H / 64; ++hd)
@@ -593,17 +627,23 @@ int finalize_text(mmf_handle* h) {
     h->r_stream_mag = mag;
     h->r_hilo_auto = mag > kHiloMag ? 1 : 0;
   }
+  // the precise mode's K-concatenated weights (+510 MB) are packed unless the layout is pinned to an
+  // fp16 stream (text_hilo 0 / 1): the load-time calibration (engine.py) may select the mode
+  const bool sp = h->opt.text_hilo < 0 || h->opt.text_hilo >= 2;
+  h->r_precise = 0;
   for (int i = 0; i < 12; ++i) {
     const std::string l = p + "encoder.layer." + std::to_string(i) + ".";
     EncLayer& L = h->r_layers[i];
+    L.qkv3 = L.o3 = L.fc13 = L.fc23 = Lin16{};
     CHK(load_qkv(h, &L, l + "attention.self.query", l + "attention.self.key", l + "attention.self.value", 768, "",
-                 true));
-    CHK(load_lin(h, &L.o, l + "attention.output.dense", 768, 768, true));
+                 true, sp));
+    CHK(load_lin(h, &L.o, l + "attention.output.dense", 768, 768, true, sp ? &L.o3 : nullptr));
     CHK(load_ln(h, &L.ln1, l + "attention.output.LayerNorm", 768));
-    CHK(load_lin(h, &L.fc1, l + "intermediate.dense", 3072, 768, true));
-    CHK(load_lin(h, &L.fc2, l + "output.dense", 768, 3072, true));
+    CHK(load_lin(h, &L.fc1, l + "intermediate.dense", 3072, 768, true, sp ? &L.fc13 : nullptr));
+    CHK(load_lin(h, &L.fc2, l + "output.dense", 768, 3072, true, sp ? &L.fc23 : nullptr));
     CHK(load_ln(h, &L.ln2, l + "output.LayerNorm", 768));
   }
+  h->r_precise = sp ? 1 : 0;
   for (int hd = 0; hd < 2; ++hd) {
     const std::string n = hd ? "misinfo_head" : "ai_head";
     GET(w1, n + ".0.weight", (size_t)256 * 768);
@@ -817,6 +857,13 @@ int lnorm(mmf_handle* h, const float* x, int ldx, const LNp& p, float* y32, int 
   return 0;
 }
 
+// post-LN in fp32, in place: x = LN(x + y) (precise mode; layernorm_kernel reads a row before writing it)
+int lnorm_add(mmf_handle* h, float* x, const float* y, const LNp& p, int rows, hipStream_t s) {
+  ProfScope ps(h, s, PK_LN, 9.0 * rows * 768, (double)rows * 768 * 12);
+  HIPCHK(launch_layernorm(x, 768, y, 768, p.g, p.b, 1e-5f, x, 768, nullptr, 0, rows, 768, s));
+  return 0;
+}
+
 int add_ln(mmf_handle* h, float* x, int ldx, const f16_t* y, int ldy, const LNp& p, float* s32, float* o32,
            f16_t* o16, int ldo, int rows, int C, hipStream_t s) {
   ProfScope ps(h, s, PK_LN, 9.0 * rows * C, (double)rows * C * (4 + 2 + (s32 ? 4 : 0) + (o32 ? 4 : 0) + 2));
@@ -846,10 +893,66 @@ int check_cap(mmf_handle* h, int B, int Lr, int Lc) {
   return 0;
 }
 
+int text_mode(const mmf_handle* h) { return h->opt.text_hilo < 0 ? h->r_hilo_auto : h->opt.text_hilo; }
+
+// RoBERTa precise mode (text_hilo = 2; precise.hip): fp32 stream, fp32 branch outputs, LayerNorm
+// and attention, every GEMM on ~22-bit operands through the K-concatenated [hi | lo | hi] x
+// [W_hi | W_hi | W_lo] product on the fp16 MFMA kernels.  All 12 layers run on every row; the heads
+// read the CLS rows of the final stream.  DESIGN §4 states its cost.
+int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
+                     float* scores, int score_stride, hipStream_t s) {
+  Workspace& w = h->ws;
+  const int M = B * L;
+  if (!h->r_precise) return fail(MMF_EINVAL, "text_hilo = 2: the precise-mode weights were not packed (load the text "
+                                             "model with text_hilo -1 or 2)");
+  if (!w.p32 || w.t32_rows < (size_t)M) return fail(MMF_EINVAL, "text_hilo = 2: precise workspaces not reserved");
+  float* x = w.r_x;  // the fp32 residual stream [M][768]
+  float* y = w.r_y;  // branch outputs / ctx [M][768]
+  {
+    ProfScope ps(h, s, PK_EMBED, 10.0 * M * 768, (double)M * 768 * (4 + 4 + 4));
+    HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, nullptr,
+                                w.r_xb, B, L, 768, 1, s, x));
+  }
+  HIPCHK(launch_split3(x, 768, w.s3, M, 768, s));
+  for (int i = 0; i < 12; ++i) {
+    const EncLayer& Ly = h->r_layers[i];
+    GemmArgs g = with_ws(gemm_args(w.s3, 2304, Ly.qkv3, M), w.sk_text, w.sk_elems);
+    g.c32 = w.p32;
+    g.ldc = 2304;
+    CHK(gemm(h, g, s));
+    {
+      ProfScope ps(h, s, PK_ATTN, 4.0 * B * 12 * (double)L * L * 64, (double)M * (2304 + 768) * 4);
+      HIPCHK(launch_attention32(w.p32, 2304, 768, 1536, mask, y, 768, B, L, 12, s));
+    }
+    HIPCHK(launch_split3(y, 768, w.s3, M, 768, s));
+    g = with_ws(gemm_args(w.s3, 2304, Ly.o3, M), w.sk_text, w.sk_elems);
+    g.c32 = y;
+    CHK(gemm(h, g, s));
+    CHK(lnorm_add(h, x, y, Ly.ln1, M, s));
+    HIPCHK(launch_split3(x, 768, w.s3, M, 768, s));
+    g = with_ws(gemm_args(w.s3, 2304, Ly.fc13, M), w.sk_text, w.sk_elems);
+    g.act = 1;  // GELU-erf
+    g.c32 = w.p32;
+    g.ldc = 3072;
+    CHK(gemm(h, g, s));
+    HIPCHK(launch_split3(w.p32, 3072, w.h3, M, 3072, s));
+    g = with_ws(gemm_args(w.h3, 9216, Ly.fc23, M), w.sk_text, w.sk_elems);
+    g.c32 = y;
+    CHK(gemm(h, g, s));
+    CHK(lnorm_add(h, x, y, Ly.ln2, M, s));
+    if (i < 11) HIPCHK(launch_split3(x, 768, w.s3, M, 768, s));
+  }
+  ProfScope ps(h, s, PK_HEADS, 2.0 * B * 2 * (768 * 256 + 256 * 2), (double)B * 768 * 4 + 2 * 768 * 256 * 4);
+  HIPCHK(launch_text_heads(x, L * 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,
+                           h->h_b2m, ai, mi, scores, score_stride, B, s));
+  return 0;
+}
+
 int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
              float* scores, int score_stride, hipStream_t s) {
   Workspace& w = h->ws;
-  const int hilo = h->opt.text_hilo < 0 ? h->r_hilo_auto : h->opt.text_hilo;
+  const int hilo = text_mode(h);
+  if (hilo >= 2) return run_text_precise(h, ids, mask, B, L, ai, mi, scores, score_stride, s);
   uint16_t* rlo = hilo ? w.r_lo : nullptr;
   const int M = B * L;
   {
@@ -1164,17 +1267,7 @@ EffSizes eff_sizes() {
 int run_effnet32(mmf_handle* h, const uint8_t* img, const float* xf32, int B, float* logits, float* score,
                  int score_stride, hipStream_t s, int img0 = 0) {
   Workspace& w = h->ws;
-  if (w.e32_cap_b < h->cap_b) {
-    CHK(free_group(h, AG_EFF32));
-    const EffSizes es = eff_sizes();
-    const size_t nb = (size_t)h->cap_b * 4;
-    void* p;
-    CHK(dev_alloc(h, &p, nb * es.io, AG_EFF32)); w.e32_a = (float*)p;
-    CHK(dev_alloc(h, &p, nb * es.io, AG_EFF32)); w.e32_b = (float*)p;
-    CHK(dev_alloc(h, &p, nb * es.exp, AG_EFF32)); w.e32_exp = (float*)p;
-    CHK(dev_alloc(h, &p, nb * es.dw, AG_EFF32)); w.e32_dw = (float*)p;
-    w.e32_cap_b = h->cap_b;
-  }
+  if (w.e32_cap_b < img0 + B) return fail(MMF_EINVAL, "effnet_fp32: fp32 tower workspaces not reserved");
   // a chunk starting at image img0 works in its own slice of every workspace (mmf_effnet_forward)
   const EffSizes es = eff_sizes();
   const size_t b0 = (size_t)img0;
@@ -1346,6 +1439,48 @@ int analyze_tail(mmf_handle* h, int B, float* scores5, float* text_sim, float* p
 }
 
 
+// Workspaces of the precision modes, allocated while the mode is selected and freed when it is left
+// (mmf_reserve, mmf_set_option, mmf_finalize) -- never from inside a launch sequence, which worker
+// threads may be enqueueing (option mt_enqueue): the fp32 EfficientNet tower (effnet_fp32, ~10 MB per
+// image) and the RoBERTa precise mode (text_hilo = 2, 40 KB per token row).
+int ensure_mode_ws(mmf_handle* h) {
+  if (!h->cap_b) return 0;
+  Workspace& w = h->ws;
+  const size_t rows = (size_t)h->cap_b * h->cap_lr;
+  void* p;
+  if (text_mode(h) >= 2 && h->r_precise) {
+    if (w.t32_rows < rows) {
+      CHK(free_group(h, AG_TEXT32));
+      CHK(dev_alloc(h, &p, rows * 3072 * 4, AG_TEXT32)); w.p32 = (float*)p;
+      CHK(dev_alloc(h, &p, rows * 2304 * 2, AG_TEXT32)); w.s3 = (f16_t*)p;
+      CHK(dev_alloc(h, &p, rows * 9216 * 2, AG_TEXT32)); w.h3 = (f16_t*)p;
+      w.t32_rows = rows;
+    }
+  } else if (w.t32_rows) {
+    CHK(free_group(h, AG_TEXT32));
+    w.p32 = nullptr;
+    w.s3 = w.h3 = nullptr;
+    w.t32_rows = 0;
+  }
+  if (h->opt.effnet_fp32) {
+    if (w.e32_cap_b < h->cap_b) {
+      CHK(free_group(h, AG_EFF32));
+      const EffSizes es = eff_sizes();
+      const size_t nb = (size_t)h->cap_b * 4;
+      CHK(dev_alloc(h, &p, nb * es.io, AG_EFF32)); w.e32_a = (float*)p;
+      CHK(dev_alloc(h, &p, nb * es.io, AG_EFF32)); w.e32_b = (float*)p;
+      CHK(dev_alloc(h, &p, nb * es.exp, AG_EFF32)); w.e32_exp = (float*)p;
+      CHK(dev_alloc(h, &p, nb * es.dw, AG_EFF32)); w.e32_dw = (float*)p;
+      w.e32_cap_b = h->cap_b;
+    }
+  } else if (w.e32_cap_b) {
+    CHK(free_group(h, AG_EFF32));
+    w.e32_a = w.e32_b = w.e32_exp = w.e32_dw = nullptr;
+    w.e32_cap_b = 0;
+  }
+  return 0;
+}
+
 int ensure_sims(mmf_handle* h) {
   if (!h->vault_n || !h->cap_b) return 0;
   if (h->ws.s_cap_n >= h->vault_n) return 0;
@@ -1430,7 +1565,7 @@ int mmf_finalize(mmf_handle* h, int clip_eos_token_id) {
   h->ready = ready;
   h->staged.clear();
   HIPCHK(hipDeviceSynchronize());
-  return 0;
+  return ensure_mode_ws(h);
 }
 
 int mmf_ready(mmf_handle* h) { return h ? h->ready : 0; }
@@ -1442,6 +1577,7 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   CHK(free_group(h, AG_WS));
   CHK(free_group(h, AG_SIMS));
   CHK(free_group(h, AG_EFF32));
+  CHK(free_group(h, AG_TEXT32));
   h->ws = Workspace();
   h->cap_b = h->cap_lr = h->cap_lc = 0;
   Workspace& w = h->ws;
@@ -1499,7 +1635,7 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   h->cap_lr = Lr;
   h->cap_lc = Lc;
   CHK(ensure_sims(h));
-  return 0;
+  return ensure_mode_ws(h);
 }
 
 int mmf_text_forward(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
@@ -1794,7 +1930,14 @@ int mmf_set_option(mmf_handle* h, const char* name, int value) {
   Options& o = h ? h->opt : process_options();
   for (const OptName& n : kOptNames)
     if (!strcmp(n.name, name)) {
+      if (h && !strcmp(name, "text_hilo") && value >= 2 && !h->r_precise && (h->ready & 1))
+        return fail(MMF_EINVAL, "text_hilo = 2 needs the precise-mode weights: the text model was packed with text_hilo "
+                                "%d (re-load it with -1 or 2)", o.text_hilo);
       o.*(n.field) = value;
+      if (h) {
+        (void)hipSetDevice(h->device);
+        return ensure_mode_ws(h);  // (precision modes: their workspaces follow the selection)
+      }
       return 0;
     }
   return fail(MMF_EINVAL, "unknown option '%s'", name);

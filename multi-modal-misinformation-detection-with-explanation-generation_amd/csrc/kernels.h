@@ -78,10 +78,17 @@ hipError_t launch_attention_q1(const float* q, int ldq, const f16_t* qkv, int ld
 hipError_t launch_attention(const f16_t* qkv, int ldqkv, const int32_t* mask, f16_t* out, int ldo, int B,
                             int L, int H, int causal, hipStream_t s);
 
-// RoBERTa embeddings + LayerNorm -> x fp32 [B*L][H], xb fp16 [B*L][H]
+// RoBERTa embeddings + LayerNorm -> the split stream xb (hi) + xlo (lo, nullable) [B*L][H] fp16, or,
+// with x32 non-null, the fp32 stream only (precise mode)
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
                                 const float* g, const float* b, float eps, uint16_t* xlo, f16_t* xb, int B, int L,
-                                int H, int pad_id, hipStream_t s);
+                                int H, int pad_id, hipStream_t s, float* x32 = nullptr);
+// RoBERTa precise mode (precise.hip, option text_hilo = 2): fp32 rows -> [hi | lo | hi] fp16 rows of 3C
+// (the K-concatenated GEMM operand), and fp32 attention over an fp32 qkv (q at h*64, k at koff + h*64,
+// v at voff + h*64; key-padding mask int32 [B][L] or null) -> fp32 out [B*L][ldo]
+hipError_t launch_split3(const float* x, int ldx, f16_t* out, int rows, int C, hipStream_t s);
+hipError_t launch_attention32(const float* qkv, int ld, int koff, int voff, const int32_t* mask, float* out, int ldo,
+                              int B, int L, int H, hipStream_t s);
 // RoBERTa post-LN residual stream split as hi = fp16(x) (also the GEMM operand), lo = fp16(x - hi)
 hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const float* g,
                               const float* b, float eps, int rows, int C, hipStream_t s);

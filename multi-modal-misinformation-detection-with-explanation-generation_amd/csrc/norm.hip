@@ -212,7 +212,8 @@ __global__ __launch_bounds__(256) void hilo_rows_kernel(const f16_t* hi, const u
 template <int NV>
 __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, const float* word, const float* pos,
                                                             const float* type0, const float* g, const float* b,
-                                                            float eps, uint16_t* xlo, f16_t* xb, int L, int pad) {
+                                                            float eps, uint16_t* xlo, f16_t* xb, float* x32, int L,
+                                                            int pad) {
   __shared__ int s_ids[512];
   __shared__ int s_pos[512];
   const int bi = blockIdx.x, tid = threadIdx.x;
@@ -244,7 +245,8 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
     add_row<NV>(v, pos + (size_t)s_pos[t] * C, lane);
     const size_t r = (size_t)bi * L + t;
     ln_row<NV>(v, g, b, eps, C, lane);
-    store_row_hilo<NV>(v, xb + r * C, xlo ? xlo + r * C : nullptr, lane);
+    if (x32) store_row<NV>(v, x32 + r * C, nullptr, lane);  // precise mode: the fp32 stream
+    else store_row_hilo<NV>(v, xb + r * C, xlo ? xlo + r * C : nullptr, lane);
   }
 }
 
@@ -437,11 +439,11 @@ hipError_t launch_add_ln(const f16_t* x, int ldx, const f16_t* y, int ldy, const
 
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
                                 const float* g, const float* b, float eps, uint16_t* xlo, f16_t* xb, int B, int L,
-                                int H, int pad_id, hipStream_t s) {
+                                int H, int pad_id, hipStream_t s, float* x32) {
   if (H != 768 || L > 512) return hipErrorInvalidValue;
   // 4 workgroups per sequence: one per sequence left the chip at 256 workgroups (~77 us at B = 256)
-  hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B, 4), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, xlo, xb, L,
-                     pad_id);
+  hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B, 4), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, xlo, xb, x32,
+                     L, pad_id);
   return hipGetLastError();
 }
 

@@ -27,12 +27,18 @@ class Engine:
     """MI355X replica of the MisinfoForensics models on one device."""
 
     EFFNET_PRECISIONS = ("auto", "fp16", "fp32")
+    # RoBERTa stream / operand precision -> option text_hilo (capi.cpp run_text / run_text_precise):
+    # "auto" = the LayerNorm-bound layout (-1: fp16 or split stream) unless the load-time calibration
+    # selects "precise"; the others pin the mode ("fp16" / "split" also skip packing the precise weights)
+    TEXT_PRECISIONS = {"auto": -1, "fp16": 0, "split": 1, "precise": 2}
 
     def __init__(self, device: int = 0, detector_state=None, clip_state=None, eos_token_id: int = 49407,
                  max_batch: int = 256, max_text_len: int = 128, max_clip_len: int = 77,
-                 effnet_precision: str = "auto"):
+                 effnet_precision: str = "auto", text_precision: str = "auto"):
         if effnet_precision not in self.EFFNET_PRECISIONS:
             raise ValueError(f"effnet_precision must be one of {self.EFFNET_PRECISIONS}, got {effnet_precision!r}")
+        if text_precision not in self.TEXT_PRECISIONS:
+            raise ValueError(f"text_precision must be one of {tuple(self.TEXT_PRECISIONS)}, got {text_precision!r}")
         self.lib = hip.load()
         self.device = torch.device("cuda", device)
         torch.cuda.set_device(self.device)
@@ -41,7 +47,10 @@ class Engine:
         self.h = h
         self.eos_token_id = eos_token_id
         self.effnet_precision = effnet_precision
+        self.text_precision = text_precision
         self.effnet_check = None
+        self.text_check = None
+        self.set_option("text_hilo", self.TEXT_PRECISIONS[text_precision])
         self.clip_stream_check = None
         self.vault_n = 0
         if detector_state is not None:
@@ -52,7 +61,7 @@ class Engine:
         self.reserve(max_batch, max_text_len, max_clip_len)
         if clip_state is not None:
             self.check_clip_streams()
-        self.calibrate(("effnet",) if detector_state is not None else ())
+        self.calibrate(("text", "effnet") if detector_state is not None else ())
 
     # ------------------------------------------------------------------ weights
     def load_state(self, state: Dict, prefix: str = "") -> None:
@@ -136,8 +145,48 @@ class Engine:
         """Load-time precision selection for re-packed components (called at construction and by
         the detector's sync after every re-pack: trained weights reach the engine through
         misinfo_forensics.py:175-186 / 285-303 after construction)."""
+        if "text" in components and self.ready & 1:
+            self.check_text_precision()
         if "effnet" in components and self.ready & 2:
             self.check_effnet_precision()
+
+    # RoBERTa: largest tolerated change of ai_score / misinfo_score between the fast layout and the
+    # precise mode on the calibration texts (half the north-star bar)
+    TEXT_TOL = 5e-4
+
+    def check_text_precision(self, n: int = 64) -> dict:
+        """Load-time selection of the RoBERTa precise mode.  The fp16-operand
+        design holds 1e-3 only while the LayerNorms do not amplify operand rounding: a checkpoint
+        with one channel dominating every LayerNorm (gamma ~7: DESIGN.md §4) moves the scores by
+        1.6e-3 even on the split stream.  With text_precision "auto" the fast layout (fp16 or split
+        stream, from the LayerNorm bound) and the precise mode (~22-bit GEMM operands, fp32 stream,
+        LayerNorm and attention) run on n seeded texts of 128 tokens; if any score is non-finite or
+        moves by more than TEXT_TOL, the precise mode stays selected (option text_hilo = 2)."""
+        from . import synthetic as syn
+        if self.text_precision != "auto":
+            self.text_check = {"mode": self.text_precision, "calibrated": False}
+            return self.text_check
+        self.set_option("text_hilo", -1)
+        n = max(1, n)
+        L = min(128, self.max_text_len)
+        ids, mask = syn.roberta_ids(n, L, 6007, [L, L // 2, 17, 5])
+
+        def scores():
+            return torch.cat([self.text_forward(ids[i:i + self.max_batch], mask[i:i + self.max_batch])[2].double()
+                              for i in range(0, n, self.max_batch)])
+        fast = scores()
+        fast_mode = self.get_option("text_hilo_effective")
+        self.set_option("text_hilo", 2)
+        prec = scores()
+        finite = bool(torch.isfinite(fast).all())
+        d = float((fast - prec).abs().max()) if finite else float("inf")
+        ok = finite and d <= self.TEXT_TOL
+        if ok:
+            self.set_option("text_hilo", -1)
+        names = {0: "fp16", 1: "split", 2: "precise"}
+        self.text_check = {"max_dscore": d, "fast_layout": names[fast_mode], "mode": names[fast_mode] if ok else "precise",
+                           "texts": n, "calibrated": True}
+        return self.text_check
 
     def check_effnet_precision(self, n: int = 64) -> dict:
         """Load-time guard of the fp16 EfficientNet tower (the counterpart of

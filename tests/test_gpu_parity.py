@@ -39,6 +39,52 @@ def test_text_signals(engine, golden):
     np.testing.assert_allclose(ai.cpu().numpy(), golden["ai_logits"], atol=5e-3)
 
 
+def test_text_precise_mode_vs_golden(engine, golden):
+    """RoBERTa precise mode (option text_hilo = 2, precise.hip: ~22-bit GEMM operands through the
+    K-concatenated [hi | lo | hi] x [W_hi | W_hi | W_lo] product, fp32 stream / LayerNorm /
+    attention) against the reference-run logits: fp32-level agreement, far inside the fp16 modes'
+    bar; batch 1 too (the skinny split-K path at K = 2304 / 9216)."""
+    mode = engine.get_option("text_hilo")
+    try:
+        engine.set_option("text_hilo", 2)
+        assert engine.get_option("text_hilo_effective") == 2
+        ai, mi, sc = engine.text_forward(golden["rob_ids"], golden["rob_mask"])
+        ai1, _, sc1 = engine.text_forward(golden["rob_ids"][:1], golden["rob_mask"][:1])
+        torch.cuda.synchronize()
+    finally:
+        engine.set_option("text_hilo", mode)
+    sc = sc.cpu().numpy()
+    da = np.abs(ai.cpu().numpy() - golden["ai_logits"]).max()
+    dm = np.abs(mi.cpu().numpy() - golden["misinfo_logits"]).max()
+    ds = max(np.abs(sc[:, 0] - _sm1(golden["ai_logits"])).max(), np.abs(sc[:, 1] - _sm1(golden["misinfo_logits"])).max())
+    print(f"precise mode vs golden: logits {da:.2e} / {dm:.2e}, scores {ds:.2e}")
+    assert ds < 2e-5 and da < 2e-4 and dm < 2e-4
+    np.testing.assert_allclose(sc1.cpu().numpy()[0], sc[0], atol=2e-5)
+
+
+def test_text_precise_mode_long_texts(det_sd, clip_sd):
+    """Precise mode past 128 tokens (attention32 over several 128-query blocks and 32-key chunks,
+    ragged masks) against the oracle's unpadded single-text analyze_text."""
+    import mmf_amd.synthetic as syn
+    from mmf_amd.engine import Engine
+    from oracle.pipeline import OracleForensics
+    lens = [512, 300, 129, 17]
+    ids, mask = syn.roberta_ids(len(lens), 512, 79, lens)
+    eng = Engine(0, det_sd, None, max_batch=len(lens), max_text_len=512, text_precision="precise")
+    assert eng.get_option("text_hilo_effective") == 2
+    _, _, sc = eng.text_forward(ids, mask)
+    torch.cuda.synchronize()
+    sc = sc.cpu().numpy()
+    orc = OracleForensics(det_sd, clip_sd)
+    d = 0.0
+    for i, n in enumerate(lens):
+        r = orc.analyze_text(ids[i, :n])
+        d = max(d, abs(sc[i, 0] - r["ai_score"]), abs(sc[i, 1] - r["misinfo_score"]))
+    print(f"precise mode, L <= 512: max |d score| {d:.2e}")
+    assert d < 2e-5
+    eng.close()
+
+
 def test_effnet_signal(engine, golden, golden_inputs):
     lg, sc = engine.effnet_forward(golden_inputs["imgs"])
     torch.cuda.synchronize()
