@@ -456,6 +456,47 @@ MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], c
   __syncthreads();  // the window is the next tile's second-slab stage
 }
 
+// Diagnostic build only (-DMMF_GEMM_STAMP, tools/gemm_stamps.py): per-workgroup
+// phase stamps of the persistent kernel into a buffer of its own ([workgroup][kGStampSlots]: 0 / 1 =
+// s_memrealtime at start / end, 2 = number of stamps, 3.. = s_memtime at each tile's start, after its
+// first K-step and after its K loop, then once after the last tile).  No output is computed from
+// them.  In the production build every GST macro is empty.
+#ifdef MMF_GEMM_STAMP
+constexpr int kGStampSlots = 96;
+__device__ unsigned long long* g_gemm_stamp;
+MMF_DEV unsigned long long gst_time() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define GST_INIT()                                                                                           \
+  unsigned long long* gst_ = (g_gemm_stamp && blockIdx.x < 256u) ? g_gemm_stamp + (size_t)blockIdx.x * kGStampSlots \
+                                                                 : nullptr;                                  \
+  int gst_n_ = 3;                                                                                            \
+  {                                                                                                          \
+    const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                                          \
+    if (gst_ && threadIdx.x == 0) gst_[0] = r_;                                                              \
+  }
+#define GST()                                                                                                \
+  {                                                                                                          \
+    const unsigned long long t_ = gst_time();                                                                \
+    if (gst_ && threadIdx.x == 0 && gst_n_ < kGStampSlots) gst_[gst_n_] = t_;                                \
+    ++gst_n_;                                                                                                \
+  }
+#define GST_END()                                                                                            \
+  {                                                                                                          \
+    GST()                                                                                                    \
+    const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                                          \
+    if (gst_ && threadIdx.x == 0) { gst_[1] = r_; gst_[2] = (unsigned long long)gst_n_; }                    \
+  }
+#else
+#define GST_INIT()
+#define GST()
+#define GST_END()
+#endif
+
 #ifndef MMF_GLDS_BUF
 #define MMF_GLDS_BUF 1  // descriptor LDS-DMA fills for full panels (0: 64-bit-address fills everywhere; A/B builds)
 #endif
@@ -511,6 +552,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g
 
   int t = wgid;
   if (t >= tiles) return;
+  GST_INIT()
   int tnext = 0;
   // s_setprio 1 for waves 0-3 (+0.4 % on the step, round-1 A/B; the old option gemm_prio = 2)
   if (wave < NW / 2) __builtin_amdgcn_s_setprio(1);
@@ -562,6 +604,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g
   int cur = 0;
   for (; t < tiles; t = tnext) {
     tnext = t + nwg;
+    GST()  // tile start (= the previous tile's epilogue end)
     int tm, tn;
     tile_coords(t, tilesM, tilesN, gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
@@ -718,7 +761,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g
       }
       __syncthreads();  // vmcnt(0): next stage landed; all reads of `cur` done before it is refilled
       cur ^= 1;
+#ifdef MMF_GEMM_STAMP
+      if (kt == 0) GST()  // after the first K-step
+#endif
     }
+    GST()  // K loop done
 
     // Epilogue.  The activation is a compile-time parameter (no per-element branch).  All traffic
     // is raw-buffer: out-of-range rows/columns read 0 / drop their stores, so there is no divergent
@@ -814,7 +861,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g
           // (v_permlane16_swap pairing: VALU, no ds_bpermute round trip)
           const int n8 = n0 + wn * TN + (odd ? (i + 1) * 16 + (fg - 1) * 4 : i * 16 + fg * 4);
           const uint4 o = pair_rows16(pk[0], pk[1]);
-          const uint32_t off = (m * (uint32_t)g.ldc + n8) * 2u;
+          uint32_t off = (m * (uint32_t)g.ldc + n8) * 2u;
+#ifdef MMF_EPI_SKIP
+          // measurement build only (outputs incomplete): the last MMF_EPI_SKIP of every MI row
+          // fragments are not stored -- how the epilogue time scales with the bytes it writes
+          if (j >= MI - MMF_EPI_SKIP * MI / 8) off = kOOB;
+#endif
           if (full8) {
             buf_store_u4(rc16, n8 < N ? off : kOOB, o);
           } else {  // N % 8 == 4: the last group of a row holds only 4 valid columns
@@ -867,6 +919,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g
     if (g.res32) epilogue(std::true_type{});
     else epilogue(std::false_type{});
   }
+  GST_END()
 }
 
 // persistent grid: one workgroup per CU (256 CUs), fewer when the launch has fewer tiles
@@ -1105,6 +1158,13 @@ const char* gemm_config_name(int c) {
       "gemm_glds_compute_only"};
   return (c >= 0 && c < kGemmConfigs) ? names[c] : "gemm_f16<?>";
 }
+
+#ifdef MMF_GEMM_STAMP
+// diagnostic build: where the persistent GEMM writes its stamps (nullptr = off)
+extern "C" int mmf_debug_gemm_stamp(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stamp), &buf, sizeof(buf));
+}
+#endif
 
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return hipSuccess;
