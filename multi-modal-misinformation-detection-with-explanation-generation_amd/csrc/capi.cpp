@@ -156,6 +156,8 @@ struct Options {
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
                         // GEMMs round to as many rounds as QKV: measured slower, off)
+  int clip_group = 0;   // CLIP towers layer-locked on one stream, each layer's ViT + text GEMMs of a kind as one
+                        // grouped persistent launch (run_clip_pair); 0: the towers on two streams
   int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
 };
 // (Round 5 removed the options whose variants were measured slower and stayed off: gemm_ring, gemm_wide,
@@ -173,6 +175,7 @@ const OptName kOptNames[] = {
     {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"}, {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
     {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},
+    {"clip_group", &Options::clip_group, "MMF_CLIP_GROUP"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -1075,18 +1078,89 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
 constexpr int kLazyMinRows = 256;
 bool clip_lazy(mmf_handle* h, int M) { return h->opt.lazy_ln && h->opt.clip_res16 && M >= kLazyMinRows; }
 
-int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, float* x, f16_t* xb, f16_t* qkv,
-                     f16_t* ctx, f16_t* hid, const int32_t* mask, int causal, int B, int L,
-                     const int32_t* last_rows, float* xc, f16_t* ctxc, float* skws, size_t sk_elems,
-                     float2* const* st, hipStream_t s) {
+// One CLIP tower's encoder pass: its weights, workspaces and (lazy LN) the statistics of its stream
+struct ClipEnc {
+  EncLayer* layers;
+  int H, I, heads;
+  float* x;  // residual stream (fp32, or fp16 when opt.clip_res16: x16)
+  f16_t *x16, *xb, *qkv, *ctx, *hid;
+  const int32_t* mask;
+  int causal, B, L, M;
+  const int32_t* last_rows;
+  float* xc;
+  f16_t* ctxc;
+  float* skws;
+  size_t sk_elems;
+  float2* const* st;
+  bool lazy;
+  LnStats cur;  // lazy LN: partials of the current stream
+  int sti;      // which of the two partial buffers holds them
+};
+
+ClipEnc vit_enc(mmf_handle* h, int B) {
+  Workspace& w = h->ws;
+  const int M = B * 50;
+  return ClipEnc{h->v_layers, 768, 3072, 12, w.v_x, h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.v_x) : nullptr,
+                 w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50, M, nullptr, w.v_xc, w.v_ctxc, w.sk_vit,
+                 w.sk_elems, w.v_st, clip_lazy(h, M), LnStats{w.v_st[0], 1, 768}, 0};
+}
+ClipEnc text_enc(mmf_handle* h, const int32_t* mask, int B, int L) {
+  Workspace& w = h->ws;
   const int M = B * L;
-  f16_t* x16 = h->opt.clip_res16 ? reinterpret_cast<f16_t*>(x) : nullptr;
+  return ClipEnc{h->t_layers, 512, 2048, 8, w.t_x, h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.t_x) : nullptr,
+                 w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, M, w.t_eos, w.t_xc, w.t_ctxc, w.sk_ctext,
+                 w.sk_elems, w.t_st, clip_lazy(h, M), LnStats{w.t_st[0], 1, 512}, 0};
+}
+
+// the four GEMMs of a lazy-LN layer (not the last): QKV and FFN-1 read the raw stream with LN1 / LN2
+// folded (consumers), out-proj and FFN-2 add into the stream and write its next partials (producers)
+GemmArgs lazy_qkv(ClipEnc& E, int i) {
+  const EncLayer& Ly = E.layers[i];
+  GemmArgs g = ln_consumer(E.x16, E.H, Ly.qkv_f, Ly.qkv_u, E.cur, E.M);
+  g.c16 = E.qkv;
+  return g;
+}
+GemmArgs lazy_producer(mmf_handle* h, ClipEnc& E, const f16_t* A, int lda, const Lin16& l) {
+  LnStats nxt;
+  E.sti ^= 1;
+  GemmArgs g = ln_producer(h->opt, A, lda, l, E.x16, E.M, E.st[E.sti], &nxt);
+  E.cur = nxt;
+  return g;
+}
+GemmArgs lazy_o(mmf_handle* h, ClipEnc& E, int i) { return lazy_producer(h, E, E.ctx, E.H, E.layers[i].o); }
+GemmArgs lazy_fc1(ClipEnc& E, int i) {
+  const EncLayer& Ly = E.layers[i];
+  GemmArgs g = ln_consumer(E.x16, E.H, Ly.fc1_f, Ly.fc1_u, E.cur, E.M);
+  g.act = 2;  // quick_gelu
+  g.c16 = E.hid;
+  return g;
+}
+GemmArgs lazy_fc2(mmf_handle* h, ClipEnc& E, int i) { return lazy_producer(h, E, E.hid, E.I, E.layers[i].fc2); }
+
+int clip_attn(mmf_handle* h, const ClipEnc& E, hipStream_t s) {
+  return attn(h, E.qkv, 3 * E.H, E.mask, E.ctx, E.H, E.B, E.L, E.heads, E.causal, s);
+}
+
+// pre-LN CLIP encoder layers [i0, i1) over E.x (residual stream, in place: fp32, or fp16 when
+// opt.clip_res16) with xb = LN1_0(x) already computed (materialised mode) or its statistics in
+// st[0] (lazy mode)
+int run_clip_encoder(mmf_handle* h, ClipEnc& E, int i0, int i1, hipStream_t s) {
+  const int M = E.M, H = E.H, I = E.I, B = E.B, L = E.L, heads = E.heads;
+  float* const x = E.x;
+  f16_t* const x16 = E.x16;
+  f16_t *const xb = E.xb, *const qkv = E.qkv, *const ctx = E.ctx, *const hid = E.hid;
+  float* const xc = E.xc;
+  f16_t* const ctxc = E.ctxc;
+  float* const skws = E.skws;
+  const size_t sk_elems = E.sk_elems;
+  const int32_t* const mask = E.mask;
+  const int32_t* const last_rows = E.last_rows;
+  const int causal = E.causal;
+  EncLayer* const layers = E.layers;
   // lazy LN (gemm.hip; the caller's embedding wrote st[0] with the stream's statistics): the QKV /
   // FFN-1 GEMMs read the raw stream x16 with LN1 / LN2 folded, out-proj / FFN-2 add into it
-  const bool lazy = clip_lazy(h, M);
-  LnStats cur{st[0], 1, H};
-  int sti = 0;
-  for (int i = 0; i < 12; ++i) {
+  const bool lazy = E.lazy;
+  for (int i = i0; i < i1; ++i) {
     const EncLayer& Ly = layers[i];
     GemmArgs g;
     if (i == 11 && (h->opt.last_q1 & 2)) {
@@ -1108,7 +1182,7 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
         kvf.w += (size_t)H * H;
         kvf.b += H;  // (c and u are padded by 256 past 3H: the 256-column DMA stays in bounds)
         kvf.out = 2 * H;
-        g = ln_consumer(x16, H, kvf, Ly.qkv_u + H, cur, M);
+        g = ln_consumer(x16, H, kvf, Ly.qkv_u + H, E.cur, M);
       } else {
         Lin16 kv = Ly.qkv;
         kv.w += (size_t)H * H;
@@ -1125,10 +1199,10 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
                                    heads, s));
       }
     } else {
-      g = lazy ? ln_consumer(x16, H, Ly.qkv_f, Ly.qkv_u, cur, M) : with_ws(gemm_args(xb, H, Ly.qkv, M), skws, sk_elems);
-      g.c16 = qkv;
+      g = lazy ? lazy_qkv(E, i) : with_ws(gemm_args(xb, H, Ly.qkv, M), skws, sk_elems);
+      if (!lazy) g.c16 = qkv;
       CHK(gemm(h, g, s));
-      CHK(attn(h, qkv, 3 * H, mask, ctx, H, B, L, heads, causal, s));
+      CHK(clip_attn(h, E, s));
     }
     if (i == 11) {
       if (!(h->opt.last_q1 & 2)) HIPCHK(launch_gather_rows2(ctx, x16 ? nullptr : x, x16, last_rows, L, H, ctxc, xc, B, s));
@@ -1148,17 +1222,9 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
       break;
     }
     if (lazy) {
-      LnStats nxt;
-      sti ^= 1;
-      CHK(gemm(h, ln_producer(h->opt, ctx, H, Ly.o, x16, M, st[sti], &nxt), s));
-      cur = nxt;
-      g = ln_consumer(x16, H, Ly.fc1_f, Ly.fc1_u, cur, M);
-      g.act = 2;  // quick_gelu
-      g.c16 = hid;
-      CHK(gemm(h, g, s));
-      sti ^= 1;
-      CHK(gemm(h, ln_producer(h->opt, hid, I, Ly.fc2, x16, M, st[sti], &nxt), s));
-      cur = nxt;
+      CHK(gemm(h, lazy_o(h, E, i), s));
+      CHK(gemm(h, lazy_fc1(E, i), s));
+      CHK(gemm(h, lazy_fc2(h, E, i), s));
       continue;
     }
     // out-proj / FFN-2 write their fp16 branch output y (out-proj into `hid`, free until FFN-1;
@@ -1183,7 +1249,26 @@ int run_clip_encoder(mmf_handle* h, EncLayer* layers, int H, int I, int heads, f
   return 0;
 }
 
-int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStream_t s) {
+// two lazy-LN GEMMs of one layer (the ViT's and the CLIP text tower's) as one persistent launch
+// (option clip_group, gemm.hip gemm_glds_group_kernel), or apart when their tiles differ
+int gemm2(mmf_handle* h, GemmArgs a, GemmArgs b, hipStream_t s) {
+  apply_options(h->opt, &a);
+  apply_options(h->opt, &b);
+  // clip_group 2: consumers on 256x192 tiles (their grouped 256x256 instantiations spill)
+  if (h->opt.clip_group == 2 && a.epi == 1) a.force_cfg = b.force_cfg = 10 + 1;
+  if (!gemm_group_ok(a, b)) {
+    CHK(gemm(h, a, s));
+    return gemm(h, b, s);
+  }
+  const double fl = 2.0 * ((double)a.M * a.N * a.K + (double)b.M * b.N * b.K);
+  const double by = 2.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)b.M * b.K + (double)b.N * b.K) +
+                    2.0 * ((double)a.M * a.N + (double)b.M * b.N) * (a.epi == 2 ? 2 : 1);
+  ProfScope ps(h, s, (gemm_config(a) * kGemmEpis + a.epi) * kGemmActs + a.act, fl, by);
+  HIPCHK(launch_gemm_group(a, b, s));
+  return 0;
+}
+
+int clip_image_embed(mmf_handle* h, const uint8_t* img, int B, hipStream_t s) {
   Workspace& w = h->ws;
   {
     ProfScope ps(h, s, PK_IM2COL, 2.0 * B * 49 * 3072, (double)B * 49 * 3072 * (1 + 2));
@@ -1196,28 +1281,36 @@ int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStre
   GemmArgs g = gemm_args(w.v_col, 3072, pe, B * 49);
   g.c32 = w.v_patch;
   CHK(gemm(h, g, s));
-  {
-    ProfScope ps(h, s, PK_EMBED, 16.0 * B * 50 * 768, (double)B * 50 * 768 * (4 + 4 + 2));
-    HIPCHK(launch_clip_vision_assemble(w.v_patch, h->v_cls, h->v_pos, h->v_pre.g, h->v_pre.b, h->v_layers[0].ln1.g,
-                                       h->v_layers[0].ln1.b, 1e-5f, h->opt.clip_res16 ? nullptr : w.v_x,
-                                       h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.v_x) : nullptr, w.v_xb,
-                                       clip_lazy(h, B * 50) ? w.v_st[0] : nullptr, B, s));
-  }
-  CHK(run_clip_encoder(h, h->v_layers, 768, 3072, 12, w.v_x, w.v_xb, w.v_qkv, w.v_ctx, w.v_h, nullptr, 0, B, 50,
-                       nullptr, w.v_xc, w.v_ctxc, w.sk_vit, w.sk_elems, w.v_st, s));
+  ProfScope ps(h, s, PK_EMBED, 16.0 * B * 50 * 768, (double)B * 50 * 768 * (4 + 4 + 2));
+  HIPCHK(launch_clip_vision_assemble(w.v_patch, h->v_cls, h->v_pos, h->v_pre.g, h->v_pre.b, h->v_layers[0].ln1.g,
+                                     h->v_layers[0].ln1.b, 1e-5f, h->opt.clip_res16 ? nullptr : w.v_x,
+                                     h->opt.clip_res16 ? reinterpret_cast<f16_t*>(w.v_x) : nullptr, w.v_xb,
+                                     clip_lazy(h, B * 50) ? w.v_st[0] : nullptr, B, s));
+  return 0;
+}
+
+int clip_image_tail(mmf_handle* h, int B, float* emb, hipStream_t s) {
+  Workspace& w = h->ws;
   HIPCHK(launch_gather_ln(w.v_xc, nullptr, 1, h->v_post.g, h->v_post.b, 1e-5f, w.v_cls, nullptr, B, 768, s));
   Lin16 pj;
   pj.w = h->v_proj;
   pj.out = 512;
   pj.in = 768;
-  g = with_ws(gemm_args(w.v_cls, 768, pj, B), w.sk_vit, w.sk_elems);
+  GemmArgs g = with_ws(gemm_args(w.v_cls, 768, pj, B), w.sk_vit, w.sk_elems);
   g.c32 = emb;
   CHK(gemm(h, g, s));
   HIPCHK(launch_l2norm(emb, B, 512, s));
   return 0;
 }
 
-int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* emb, hipStream_t s) {
+int run_clip_image(mmf_handle* h, const uint8_t* img, int B, float* emb, hipStream_t s) {
+  CHK(clip_image_embed(h, img, B, s));
+  ClipEnc E = vit_enc(h, B);
+  CHK(run_clip_encoder(h, E, 0, 12, s));
+  return clip_image_tail(h, B, emb, s);
+}
+
+int clip_text_embed(mmf_handle* h, const int32_t* ids, int B, int L, hipStream_t s) {
   Workspace& w = h->ws;
   {
     ProfScope ps(h, s, PK_EMBED, 10.0 * B * L * 512, (double)B * L * 512 * (4 + 4 + 4 + 2));
@@ -1227,8 +1320,11 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
                                   clip_lazy(h, B * L) ? w.t_st[0] : nullptr, B, L, 512, s));
   }
   HIPCHK(launch_eos_index(ids, w.t_eos, B, L, h->eos_id, s));
-  CHK(run_clip_encoder(h, h->t_layers, 512, 2048, 8, w.t_x, w.t_xb, w.t_qkv, w.t_ctx, w.t_h, mask, 1, B, L, w.t_eos,
-                       w.t_xc, w.t_ctxc, w.sk_ctext, w.sk_elems, w.t_st, s));
+  return 0;
+}
+
+int clip_text_tail(mmf_handle* h, int B, float* emb, hipStream_t s) {
+  Workspace& w = h->ws;
   HIPCHK(launch_gather_ln(w.t_xc, nullptr, 1, h->t_final.g, h->t_final.b, 1e-5f, w.t_pool, nullptr, B, 512, s));
   Lin16 pj;
   pj.w = h->t_proj;
@@ -1239,6 +1335,41 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
   CHK(gemm(h, g, s));
   HIPCHK(launch_l2norm(emb, B, 512, s));
   return 0;
+}
+
+int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* emb, hipStream_t s) {
+  CHK(clip_text_embed(h, ids, B, L, s));
+  ClipEnc E = text_enc(h, mask, B, L);
+  CHK(run_clip_encoder(h, E, 0, 12, s));
+  return clip_text_tail(h, B, emb, s);
+}
+
+// Both CLIP towers layer-locked on ONE stream (option clip_group, both towers lazy-LN): the ViT's and
+// the text tower's GEMM of each kind in layers 0-10 run as one grouped persistent launch (their
+// sub-round grids -- producers 200 + 231 tiles on 256 CUs -- pack into one), the two attentions
+// back to back; the compact last layers and the heads per tower.  Each tower's arithmetic is its
+// own launch's, so the embeddings are bit-identical to the two-stream path.
+bool clip_group_ok(mmf_handle* h, int B, int L) {
+  return h->opt.clip_group && clip_lazy(h, B * 50) && clip_lazy(h, B * L);
+}
+
+int run_clip_pair(mmf_handle* h, const uint8_t* img, const int32_t* ids, const int32_t* mask, int B, int L,
+                  float* iemb, float* temb, hipStream_t s) {
+  CHK(clip_image_embed(h, img, B, s));
+  CHK(clip_text_embed(h, ids, B, L, s));
+  ClipEnc V = vit_enc(h, B), T = text_enc(h, mask, B, L);
+  for (int i = 0; i < 11; ++i) {
+    CHK(gemm2(h, lazy_qkv(V, i), lazy_qkv(T, i), s));
+    CHK(clip_attn(h, V, s));
+    CHK(clip_attn(h, T, s));
+    CHK(gemm2(h, lazy_o(h, V, i), lazy_o(h, T, i), s));
+    CHK(gemm2(h, lazy_fc1(V, i), lazy_fc1(T, i), s));
+    CHK(gemm2(h, lazy_fc2(h, V, i), lazy_fc2(h, T, i), s));
+  }
+  CHK(run_clip_encoder(h, V, 11, 12, s));
+  CHK(run_clip_encoder(h, T, 11, 12, s));
+  CHK(clip_image_tail(h, B, iemb, s));
+  return clip_text_tail(h, B, temb, s);
 }
 
 // EfficientNet-B0 activation elements per image: block input/output, expanded, depthwise output,
@@ -1728,6 +1859,11 @@ int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, 
   float* ie = img_emb ? img_emb : h->ws.v_emb;
   float* te = txt_emb ? txt_emb : h->ws.t_emb;
   CHK(ensure_towers(h));
+  if (clip_group_ok(h, B, L)) {  // both towers layer-locked on this stream, grouped GEMM launches
+    CHK(run_clip_pair(h, img, ids, mask, B, L, ie, te, s));
+    HIPCHK(launch_rowdot(ie, te, sim, 1, B, 512, s));
+    return 0;
+  }
   const int concurrent = h->opt.concurrent && !h->prof;
   hipStream_t st = s;
   if (concurrent) {  // the text tower beside the vision tower (disjoint workspaces)
@@ -1851,6 +1987,8 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   // diag_skip (diagnostic only, never set by the API or bench.py): towers left out to measure each
   // tower's marginal cost in the concurrent step (bit 1 text, 2 EfficientNet, 4 CLIP text, 8 ViT)
   const int skip = h->opt.diag_skip;
+  // clip_group: the CLIP pair layer-locked on the ViT's stream (run_clip_pair), the text tower's stream idle
+  const bool pair = clip_group_ok(h, B, Lc) && !(skip & 12);
   if (concurrent && h->opt.mt_enqueue > 0 && B <= h->opt.mt_enqueue) {
     // small batches: three host threads enqueue the text, CLIP-text and EfficientNet towers while
     // this thread enqueues the ViT, so every chain starts at once (each stream keeps its own order)
@@ -1859,11 +1997,13 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
       h->pool->start(h->device);
     }
     float* t_emb = w.t_emb;
-    const bool on[3] = {!(skip & 1), !(skip & 4), !(skip & 2)};
+    const bool on[3] = {!(skip & 1), !(skip & 4) && !pair, !(skip & 2)};
     if (on[0]) h->pool->submit(0, [=] { return run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text); });
     if (on[1]) h->pool->submit(1, [=] { return run_clip_text(h, clip_ids, clip_mask, B, Lc, t_emb, st_ctxt); });
     if (on[2]) h->pool->submit(2, [=] { return run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff, 0); });
-    const int rc = (skip & 8) ? 0 : run_clip_image(h, img_clip, B, w.v_emb, s);
+    const int rc = pair       ? run_clip_pair(h, img_clip, clip_ids, clip_mask, B, Lc, w.v_emb, t_emb, s)
+                   : (skip & 8) ? 0
+                                : run_clip_image(h, img_clip, B, w.v_emb, s);
     int wrc = 0;
     std::string werr;
     for (int i = 0; i < 3; ++i) {
@@ -1879,9 +2019,10 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
     if (wrc) return fail(wrc, "%s", werr.c_str());
   } else {
     if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
-    if (!(skip & 4)) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
+    if (!(skip & 4) && !pair) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
     if (!(skip & 2)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
-    if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
+    if (pair) CHK(run_clip_pair(h, img_clip, clip_ids, clip_mask, B, Lc, w.v_emb, w.t_emb, s));
+    else if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
   }
   if (concurrent) {
     for (int i = 0; i < 3; ++i) {

@@ -506,420 +506,40 @@ MMF_DEV unsigned long long gst_time() {
 template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
                                                                        int gm) {
-  // Persistent: one 512-thread workgroup per CU walks tiles t = i*gridDim + wgid.  The first
-  // K-slab of the NEXT tile is DMA'd into the free LDS stage during the current tile's last
-  // K-step, so only the very first tile pays the load latency and each epilogue's stores drain
-  // underneath the next tile's first MFMAs.
-  constexpr int NW = WGM * WGN;
-  constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
-  constexpr int STAGE = (BM + BN) * BK;
-  static_assert(NW == 8 && BM == 256, "8 waves, 256-row tiles");
-  // EPI 3 (attention epilogue, RoBERTa QKV): a 40 KB gap between the two stages, so that the stage
-  // the last K-step freed plus the gap hold q (32 KB) and k | v (64 KB) of the tile's two sequences
-  constexpr bool ATT = EPI == 3;
-  static_assert(!ATT || (BM == 256 && BN == 192 && WGM == 4 && WGN == 2 && PIPE2), "attention epilogue: 256x192");
-  constexpr int XGAP = ATT ? 20480 : 0;  // f16 elements
-  constexpr int SOFF = STAGE + XGAP;     // stage 1's offset
-  __shared__ __attribute__((aligned(16))) f16_t lds[2 * STAGE + XGAP];
-  constexpr bool ROWST = EPI == 1;  // reads row statistics
-  static_assert(EPI == 0 || BM == 256, "lazy-LN epilogues assume 256-row tiles");
-  __shared__ __attribute__((aligned(16))) float2 lds_rows[ROWST ? BM * kLnPMax : 2];
-  // column vectors of a consumer tile: u | bias (bias through LDS frees the 4*NI bias registers the
-  // plain path holds across the K loop)
-  constexpr int kBiasCol = 256;
-  __shared__ __attribute__((aligned(16))) float lds_cols[(ROWST || ATT) ? 512 : 4];  // (ATT: key mask bias)
-  __shared__ __attribute__((aligned(16))) float2 lds_stat[ROWST ? BM : 2];  // (mean, rstd) per tile row
+#define MMF_GLDS_FIRST_TILE wgid
+#include "gemm_glds_body.inc"
+#undef MMF_GLDS_FIRST_TILE
+}
 
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int M = g.M, N = g.N;
-  const int nk = g.K / BK;
-  const int fr = lane & 15, fg = lane >> 4;
-  const bool has_res = g.res32 || g.res16;
-  const bool full8 = (N & 7) == 0;
-  // byte extents of the epilogue operands (run_glds keeps them, and every offset formed below
-  // for a row < M + BM, under 2^31)
-  const uint32_t out_elems = (uint32_t)(M - 1) * g.ldc + N;
-  const rsrc_t rbias = make_rsrc(g.bias, (uint32_t)N * 4u);
-  const rsrc_t rres = make_rsrc(g.res32 ? (const void*)g.res32 : (const void*)g.res16,
-                                ((uint32_t)(M - 1) * g.ldr + N) * (g.res32 ? 4u : 2u));
-  const rsrc_t rc32 = make_rsrc(g.c32, out_elems * 4u);
-  const rsrc_t rc16 = make_rsrc(g.c16, out_elems * 2u);
+// One problem of a grouped launch: its tiles follow `skip` tiles of the previous problem in the global
+// order wgid, wgid + nwg, ... (gemm_glds_group_kernel).  The LDS arrays are function-scope __shared__
+// variables of this function, so both passes of the grouped kernel share one allocation.
+template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2, int EPI>
+MMF_DEV void glds_run(GemmArgs g, int tilesN, int tiles, int tilesM, int gm, int skip) {
+  constexpr int DBG = 0;
+#define MMF_GLDS_FIRST_TILE (wgid >= skip ? wgid - skip : wgid + (skip - wgid + nwg - 1) / nwg * nwg - skip)
+#include "gemm_glds_body.inc"
+#undef MMF_GLDS_FIRST_TILE
+}
 
-  int t = wgid;
-  if (t >= tiles) return;
-  GST_INIT()
-  int tnext = 0;
-  // s_setprio 1 for waves 0-3 (+0.4 % on the step, round-1 A/B; the old option gemm_prio = 2)
-  if (wave < NW / 2) __builtin_amdgcn_s_setprio(1);
-  // descriptor fills (glds_tile_buf) for every full row / column panel whose operand's byte extent
-  // fits 32 bits: the per-lane source offset is one loop-invariant
-  // VGPR and the panel base rides in the scalar soffset, so a K-step's DMA issue costs no VALU
-  // (glds_tile: a clamped row and a 64-bit address per piece, ~6 VALU each, every K-step)
-  const bool bufA = MMF_GLDS_BUF && (size_t)M * g.lda * 2 < ((size_t)1 << 32);
-  const bool bufW = MMF_GLDS_BUF && (size_t)N * g.ldw * 2 < ((size_t)1 << 32);
-  const rsrc_t ra = make_rsrc(g.A, bufA ? (uint32_t)((size_t)M * g.lda * 2) : 0u);
-  const rsrc_t rw = make_rsrc(g.W, bufW ? (uint32_t)((size_t)N * g.ldw * 2) : 0u);
-  const uint32_t lchunk = (uint32_t)(((lane & 7) ^ (lane >> 3)) * 16);
-  const uint32_t aoff = (uint32_t)(lane >> 3) * (uint32_t)g.lda * 2u + lchunk;
-  const uint32_t woff = (uint32_t)(lane >> 3) * (uint32_t)g.ldw * 2u + lchunk;
-  auto stage = [&](int buf, int tile, int kt) {
-    if constexpr (DBG == 2) return;
-    int tm_, tn_;
-    tile_coords(tile, tilesM, tilesN, gm, tm_, tn_);
-    f16_t* nb = lds + buf * SOFF;
-    if (bufA && tm_ * BM + BM <= M) glds_tile_buf<BM, NW>(ra, (uint32_t)g.lda * 2u, tm_ * BM, kt * BK, aoff, nb, wave);
-    else glds_tile<BM, NW>(g.A, g.lda, tm_ * BM, M, kt * BK, nb, wave, lane);
-    if (bufW && tn_ * BN + BN <= N)
-      glds_tile_buf<BN, NW>(rw, (uint32_t)g.ldw * 2u, tn_ * BN, kt * BK, woff, nb + BM * BK, wave);
-    else glds_tile<BN, NW>(g.W, g.ldw, tn_ * BN, N, kt * BK, nb + BM * BK, wave, lane);
-  };
-  // lazy-LN epilogue operands of tile (m0_, n0_) -> LDS (issued in the second K-step: every wave
-  // has left the previous tile's epilogue by then; the K-step barriers' vmcnt(0) covers them)
-  auto epi_dma = [&](int m0_, int n0_) {
-    typedef __attribute__((address_space(3))) char lds_char_t;
-    if constexpr (ROWST) {  // the 256 rows' partials: 256 * P * 8 B, contiguous, whole KBs
-      const uint32_t bytes = (uint32_t)BM * g.ln_in_P * 8u;
-      const char* src = reinterpret_cast<const char*>(g.ln_in) + (size_t)m0_ * g.ln_in_P * 8;
-      for (uint32_t off = (uint32_t)wave * 1024u; off < bytes; off += NW * 1024u)
-        __builtin_amdgcn_global_load_lds((const void*)(src + off + lane * 16),
-                                         (lds_void_t*)((lds_char_t*)lds_rows + off), 16, 0, 0);
-    }
-    if constexpr (EPI == 1) {  // u[n0 .. n0 + 256)
-      if (wave == NW - 1)
-        __builtin_amdgcn_global_load_lds((const void*)(g.ln_u + n0_ + lane * 4), (lds_void_t*)lds_cols, 16, 0, 0);
-    }
-    if constexpr (ROWST) {  // bias[n0 .. n0 + 256) (buffers padded by 256)
-      if (wave == NW - 3)
-        __builtin_amdgcn_global_load_lds((const void*)(g.bias + n0_ + lane * 4),
-                                         (lds_void_t*)((lds_char_t*)lds_cols + kBiasCol * 4), 16, 0, 0);
-    }
-  };
-  stage(0, t, 0);
-  __syncthreads();
-  int cur = 0;
-  for (; t < tiles; t = tnext) {
-    tnext = t + nwg;
-    GST()  // tile start (= the previous tile's epilogue end)
-    int tm, tn;
-    tile_coords(t, tilesM, tilesN, gm, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-    f32x4 acc[NI][MI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 bias_r[ROWST ? 1 : NI];  // this lane's epilogue bias columns, fetched under the K loop
-    if constexpr (!ROWST) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i) bias_r[i] = buf_load_f4(rbias, (uint32_t)(n0 + wn * TN + i * 16 + fg * 4) * 4u);
-    }
-    // bias of fragment column group i (ROWST: from LDS)
-    auto bias_of = [&](int i) -> float4 {
-      if constexpr (ROWST) return *reinterpret_cast<const float4*>(lds_cols + kBiasCol + wn * TN + i * 16 + fg * 4);
-      else return bias_r[i];
-    };
-
-    for (int kt = 0; kt < nk; ++kt) {
-      if constexpr (ROWST) {
-        if (kt == 1) epi_dma(m0, n0);
-        if (kt == 2) {
-          // the DMA'd partials -> (mean, rstd) of the tile's 256 rows (threads 0-255, one row each,
-          // two passes over the LDS partials with a rolled loop: few live registers here, where the
-          // K loop's accumulators are live), before this K-step's fragment reads; the epilogue
-          // reads them after the K loop's later barriers
-          if (tid < BM && BN == 192) {
-            // 256x192 tiles have register room: all kLnPMax partial slots read at once, one LDS
-            // latency.  Slots p >= P belong to the next rows or lie past the DMA'd block (any bit
-            // pattern, NaN included), so they are SELECTED out, never weighted by 0.
-            const int P = g.ln_in_P, tnin = g.ln_in_tn, C = EPI == 1 ? g.K : N;
-            const float2* pr = lds_rows + tid * P;
-            float2 pv[kLnPMax];
-            float nv[kLnPMax];
-#pragma unroll
-            for (int pi = 0; pi < kLnPMax; ++pi) {
-              const float2 v = pr[pi];
-              pv[pi] = pi < P ? v : make_float2(0.f, 0.f);
-              nv[pi] = pi < P ? (float)min(C - pi * tnin, tnin) : 0.f;
-            }
-            // explicit fmaf, the same operation sequence as the rolled loop below: a zero slot adds
-            // an exact 0, so both tile widths give bit-identical statistics (the consumer's tile
-            // width depends on M, and rows must not change with the batch they run in)
-            float s1 = 0.f;
-#pragma unroll
-            for (int pi = 0; pi < kLnPMax; ++pi) s1 = fmaf(nv[pi], pv[pi].x, s1);
-            const float mean = s1 / (float)C;
-            float s2 = 0.f;
-#pragma unroll
-            for (int pi = 0; pi < kLnPMax; ++pi) {
-              const float d = pv[pi].x - mean;
-              s2 += fmaf(nv[pi] * d, d, pv[pi].y);
-            }
-            lds_stat[tid] = make_float2(mean, rsqrtf(s2 / (float)C + g.ln_eps));
-          } else if (tid < BM) {
-            const int P = g.ln_in_P, tnin = g.ln_in_tn, C = EPI == 1 ? g.K : N;
-            const float2* pr = lds_rows + tid * P;
-            float s1 = 0.f;
+// Grouped launch (option clip_group; the ViT and CLIP-text GEMMs of one layer, which share a tile
+// instantiation): one persistent grid over problem 0's tiles, then problem 1's, in one global order
+// t = 0 .. tiles0 + tiles1 - 1 (workgroup w takes w, w + nwg, ...), so the two sub-round launches of
+// the separate towers (ViT 200 + text 231 producer tiles on 256 CUs) pack into one.  Problem 0 is the
+// one with the longer K (longest tiles first).  Each tile is computed exactly as in its own launch.
+struct GemmPair {
+  GemmArgs g[2];
+  int tilesN[2], tiles[2], tilesM[2];
+};
+template <int BM, int BN, int WGM, int WGN, int ACT, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_group_kernel(GemmPair pr) {
+  // one copy of the tile loop (two inlined copies spill 50-90 VGPRs at 256x256): the problem's
+  // arguments are read per pass
 #pragma unroll 1
-            for (int pi = 0; pi < P; ++pi) s1 = fmaf((float)min(C - pi * tnin, tnin), pr[pi].x, s1);
-            const float mean = s1 / (float)C;
-            float s2 = 0.f;
-#pragma unroll 1
-            for (int pi = 0; pi < P; ++pi) {
-              const float2 v = pr[pi];
-              const float d = v.x - mean;
-              s2 += fmaf((float)min(C - pi * tnin, tnin) * d, d, v.y);
-            }
-            lds_stat[tid] = make_float2(mean, rsqrtf(s2 / (float)C + g.ln_eps));
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (kt + 1 < nk) {
-        stage(cur ^ 1, t, kt + 1);
-      } else {
-        if (tnext < tiles) stage(cur ^ 1, tnext, 0);
-      }
-      const f16_t* Xs = lds + cur * SOFF;
-      const f16_t* Ws = Xs + BM * BK;
-      if constexpr (DBG == 1) {
-      } else if constexpr (PIPE2) {
-        // half-step pipeline: the second K-half's fragment reads are issued between the first
-        // half's MFMAs (1 read per 2 MFMAs), so only the first half's reads are exposed after the
-        // barrier
-        f16x8 w0[NI], x0[MI], w1[NI], x1[MI];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) w0[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, fg)));
-#pragma unroll
-        for (int j = 0; j < MI; ++j) x0[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, fg)));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-          w1[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, 4 + fg)));
-#pragma unroll
-        for (int j = 0; j < MI; ++j)
-          x1[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, 4 + fg)));
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(w0[i], x0[j], acc[i][j]);
-#pragma unroll
-        for (int q = 0; q < NI + MI; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, NI * MI - 2 * (NI + MI), 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(w1[i], x1[j], acc[i][j]);
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (BN == 192) {
-        // 256x192 (wave tile 64x96): all 20 fragment reads of the K-step first, then its 48 MFMAs,
-        // then the barrier -- pinned with sched_barriers (hipcc otherwise interleaves 2 reads +
-        // lgkmcnt(0) per 8 MFMAs and sinks MFMAs below the barrier's vmcnt(0)).  Measured: these
-        // GEMMs 3 % faster; the same schedule on the 256x256 tiles (24 reads, 64 MFMAs) 3-10 %
-        // slower, so they keep the compiler's interleave below.
-        f16x8 wf[2][NI], xf[2][MI];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-            wf[ks][i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
-#pragma unroll
-          for (int j = 0; j < MI; ++j)
-            xf[ks][j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(wf[ks][i], xf[ks][j], acc[i][j]);
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          f16x8 wf[NI], xf[MI];
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-            wf[i] = as_f16x8(*reinterpret_cast<const uint4*>(Ws + swz(wn * TN + i * 16 + fr, ks * 4 + fg)));
-#pragma unroll
-          for (int j = 0; j < MI; ++j)
-            xf[j] = as_f16x8(*reinterpret_cast<const uint4*>(Xs + swz(wm * TM + j * 16 + fr, ks * 4 + fg)));
-#pragma unroll
-          for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int j = 0; j < MI; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
-        }
-      }
-      __syncthreads();  // vmcnt(0): next stage landed; all reads of `cur` done before it is refilled
-      cur ^= 1;
-#ifdef MMF_GEMM_STAMP
-      if (kt == 0) GST()  // after the first K-step
-#endif
-    }
-    GST()  // K loop done
-
-    // Epilogue.  The activation is a compile-time parameter (no per-element branch).  All traffic
-    // is raw-buffer: out-of-range rows/columns read 0 / drop their stores, so there is no divergent
-    // branch and no load that has to wait on the stores issued before it -- bias columns were
-    // fetched at tile start and residual rows are loaded one fragment row AHEAD of the stores (one
-    // vmcnt counter covers loads and stores in issue order).
-    // lazy LN: (mean, rstd) of fragment row j -> lds_stat[wm * TM + j * 16 + fr] (computed at kt = 2)
-    if constexpr (ATT) {
-      attention_epilogue(g, acc, bias_r, lds + ((cur ^ 1) ? SOFF + STAGE - 49152 : 0), lds_cols, m0, tn, M, wm, wn,
-                         wave, tid, fr, fg);
-      continue;
-    }
-    if constexpr (EPI == 2) {
-      // producer: out = acc + bias + residual, stored fp16 (in place over the residual is allowed:
-      // each element is read before it is written, by one lane), then this wave's partial
-      // (mean, M2) of the STORED values over its TN columns of each row
-      const int Pout = (N + TN - 1) / TN, pidx = tn * WGN + wn;
-      const int nval = min(max(N - (n0 + wn * TN), 0), TN);
-      // every residual fragment of the tile requested up front: one HBM latency per tile instead
-      // of one per fragment row
-      uint2 rall[MI][NI];
-#pragma unroll
-      for (int j = 0; j < MI; ++j) {
-        const uint32_t m = m0 + wm * TM + j * 16 + fr;
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-          rall[j][i] = buf_load_u2(rres, (m * (uint32_t)g.ldr + (n0 + wn * TN + i * 16 + fg * 4)) * 2u);
-      }
-#pragma unroll
-      for (int j = 0; j < MI; ++j) {
-        const uint2* rcur = rall[j];
-        const uint32_t m = m0 + wm * TM + j * 16 + fr;
-        uint2 pk[NI];
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int nl = wn * TN + i * 16 + fg * 4, n = n0 + nl;
-          const float rv[4] = {lo_h(rcur[i].x), hi_h(rcur[i].x), lo_h(rcur[i].y), hi_h(rcur[i].y)};
-          const float4 bi = bias_of(i);
-          pk[i] = make_uint2(pack2h(acc[i][j][0] + bi.x + rv[0], acc[i][j][1] + bi.y + rv[1]),
-                             pack2h(acc[i][j][2] + bi.z + rv[2], acc[i][j][3] + bi.w + rv[3]));
-          const uint32_t e = n < N ? m * (uint32_t)g.ldc + n : (kOOB >> 2);
-          buf_store_u2(rc16, e * 2u, pk[i]);
-          if (n < N) sum += (lo_h(pk[i].x) + hi_h(pk[i].x)) + (lo_h(pk[i].y) + hi_h(pk[i].y));
-        }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        const float mean = sum / (float)(nval > 0 ? nval : 1);
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const float d0 = lo_h(pk[i].x) - mean, d1 = hi_h(pk[i].x) - mean;
-          const float d2 = lo_h(pk[i].y) - mean, d3 = hi_h(pk[i].y) - mean;
-          if (n0 + wn * TN + i * 16 + fg * 4 < N) q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-        }
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        if (fg == 0 && (int)m < M && nval > 0) g.ln_out[(size_t)m * Pout + pidx] = make_float2(mean, q);
-      }
-      continue;
-    }
-    if (!has_res && !g.c32) {
-      // fp16-only output: lanes l and l^16 own adjacent 4-column groups of one row; swap one
-      // fragment of each pair so every lane stores 16 contiguous bytes (half the store issues)
-#pragma unroll
-      for (int j = 0; j < MI; ++j) {
-        const uint32_t m = m0 + wm * TM + j * 16 + fr;
-        float2 st = make_float2(0.f, 1.f);
-        if constexpr (EPI == 1) st = lds_stat[wm * TM + j * 16 + fr];
-#pragma unroll
-        for (int i = 0; i < NI; i += 2) {
-          uint2 pk[2];
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            float v[4] = {acc[i + h2][j][0], acc[i + h2][j][1], acc[i + h2][j][2], acc[i + h2][j][3]};
-            if constexpr (EPI == 1) {  // r (acc - mean u), then + c (the folded bias)
-              const float4 u = *reinterpret_cast<const float4*>(lds_cols + wn * TN + (i + h2) * 16 + fg * 4);
-              v[0] = st.y * (v[0] - st.x * u.x);
-              v[1] = st.y * (v[1] - st.x * u.y);
-              v[2] = st.y * (v[2] - st.x * u.z);
-              v[3] = st.y * (v[3] - st.x * u.w);
-            }
-            const float4 bi = bias_of(i + h2);
-            v[0] += bi.x;
-            v[1] += bi.y;
-            v[2] += bi.z;
-            v[3] += bi.w;
-            if (ACT != ACT_NONE) act4<ACT>(v);
-            pk[h2] = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
-          }
-          const bool odd = fg & 1;
-          // even fg: cols (16i + 4fg) .. +7 of fragment i; odd fg: cols (16(i+1) + 4(fg-1)) .. +7
-          // (v_permlane16_swap pairing: VALU, no ds_bpermute round trip)
-          const int n8 = n0 + wn * TN + (odd ? (i + 1) * 16 + (fg - 1) * 4 : i * 16 + fg * 4);
-          const uint4 o = pair_rows16(pk[0], pk[1]);
-          uint32_t off = (m * (uint32_t)g.ldc + n8) * 2u;
-#ifdef MMF_EPI_SKIP
-          // measurement build only (outputs incomplete): the last MMF_EPI_SKIP of every MI row
-          // fragments are not stored -- how the epilogue time scales with the bytes it writes
-          if (j >= MI - MMF_EPI_SKIP * MI / 8) off = kOOB;
-#endif
-          if (full8) {
-            buf_store_u4(rc16, n8 < N ? off : kOOB, o);
-          } else {  // N % 8 == 4: the last group of a row holds only 4 valid columns
-            buf_store_u4(rc16, n8 + 8 <= N ? off : kOOB, o);
-            buf_store_u2(rc16, (n8 + 8 > N && n8 < N) ? off : kOOB, make_uint2(o.x, o.y));
-          }
-        }
-      }
-      continue;
-    }
-    // general epilogue, instantiated per residual dtype so that no load sits under a branch
-    auto epilogue = [&](auto res_is_f32) {
-      constexpr bool R32 = decltype(res_is_f32)::value;
-      float4 rcur[NI], rnext[NI];
-      auto load_res = [&](float4* r, int j) {
-        const uint32_t m = m0 + wm * TM + j * 16 + fr;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const uint32_t e = m * (uint32_t)g.ldr + (n0 + wn * TN + i * 16 + fg * 4);
-          if constexpr (R32) {
-            r[i] = buf_load_f4(rres, e * 4u);
-          } else {
-            const uint2 rr = buf_load_u2(rres, e * 2u);  // zeros when there is no residual
-            r[i] = make_float4(lo_h(rr.x), hi_h(rr.x), lo_h(rr.y), hi_h(rr.y));
-          }
-        }
-      };
-      load_res(rcur, 0);
-#pragma unroll
-      for (int j = 0; j < MI; ++j) {
-        if (j + 1 < MI) load_res(rnext, j + 1);
-        const uint32_t m = m0 + wm * TM + j * 16 + fr;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int n = n0 + wn * TN + i * 16 + fg * 4;
-          const float4 bi = bias_of(i);
-          float v[4] = {acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w};
-          if (ACT != ACT_NONE) {
-            act4<ACT>(v);
-          }
-          v[0] += rcur[i].x; v[1] += rcur[i].y; v[2] += rcur[i].z; v[3] += rcur[i].w;
-          const uint32_t e = n < N ? m * (uint32_t)g.ldc + n : (kOOB >> 2);
-          if (g.c32) buf_store_f4(rc32, e * 4u, make_float4(v[0], v[1], v[2], v[3]));
-          if (g.c16) buf_store_u2(rc16, e * 2u, make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3])));
-        }
-#pragma unroll
-        for (int i = 0; i < NI; ++i) rcur[i] = rnext[i];
-      }
-    };
-    if (g.res32) epilogue(std::true_type{});
-    else epilogue(std::false_type{});
+  for (int p = 0; p < 2; ++p) {
+    if (p) __syncthreads();  // (the next problem's prologue refills the stages)
+    glds_run<BM, BN, WGM, WGN, ACT, true, EPI>(pr.g[p], pr.tilesN[p], pr.tiles[p], pr.tilesM[p], 0, p ? pr.tiles[0] : 0);
   }
-  GST_END()
 }
 
 // persistent grid: one workgroup per CU (256 CUs), fewer when the launch has fewer tiles
@@ -981,6 +601,27 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   }
 #undef MMF_EPI_CASE
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t run_glds_group(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  GemmPair pr;
+  pr.g[0] = a0;
+  pr.g[1] = a1;
+  for (int i = 0; i < 2; ++i) {
+    pr.tilesM[i] = (pr.g[i].M + BM - 1) / BM;
+    pr.tilesN[i] = (pr.g[i].N + BN - 1) / BN;
+    pr.tiles[i] = pr.tilesM[i] * pr.tilesN[i];
+  }
+  const int tiles = pr.tiles[0] + pr.tiles[1];
+  const dim3 grid(tiles < 256 ? tiles : 256), blk(64 * WGM * WGN);
+#define MMF_GRP_CASE(EPI, ACT) hipLaunchKernelGGL((gemm_glds_group_kernel<BM, BN, WGM, WGN, ACT, EPI>), grid, blk, 0, s, pr)
+  if (a0.epi == 1 && a0.act == ACT_NONE) MMF_GRP_CASE(1, ACT_NONE);
+  else if (a0.epi == 1 && a0.act == ACT_QUICK_GELU) MMF_GRP_CASE(1, ACT_QUICK_GELU);
+  else if (a0.epi == 2 && a0.act == ACT_NONE && BN == 192) MMF_GRP_CASE(2, ACT_NONE);
+  else return hipErrorNotSupported;
+#undef MMF_GRP_CASE
   return hipGetLastError();
 }
 
@@ -1157,6 +798,25 @@ const char* gemm_config_name(int c) {
       "gemm_glds_pipe2<256,256,2,4>", "(removed)", "(removed)", "(removed)", "gemm_glds_dma_only",
       "gemm_glds_compute_only"};
   return (c >= 0 && c < kGemmConfigs) ? names[c] : "gemm_f16<?>";
+}
+
+// two lazy-LN GEMMs of one tile instantiation in one persistent launch (gemm_glds_group_kernel); the
+// longer-K problem first.  hipErrorNotSupported when they differ in tile, epilogue or activation
+// (the caller then launches them apart).
+bool gemm_group_ok(const GemmArgs& a, const GemmArgs& b) {
+  if (a.epi == 0 || a.epi != b.epi || a.act != b.act || a.epi == 3) return false;
+  if (a.act != ACT_NONE && a.act != ACT_QUICK_GELU) return false;
+  if (a.epi == 2 && a.act != ACT_NONE) return false;
+  return gemm_config(a) == gemm_config(b);
+}
+
+hipError_t launch_gemm_group(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
+  if (!gemm_group_ok(a, b)) return hipErrorNotSupported;
+  if (!epi_ok(a) || !epi_ok(b)) return hipErrorInvalidValue;
+  const int ca = gemm_config(a);
+  const GemmArgs& a0 = a.K >= b.K ? a : b;
+  const GemmArgs& a1 = a.K >= b.K ? b : a;
+  return ca == 11 ? run_glds_group<256, 256, 2, 4>(a0, a1, s) : run_glds_group<256, 192, 4, 2>(a0, a1, s);
 }
 
 #ifdef MMF_GEMM_STAMP

@@ -47,6 +47,11 @@ int gemm_ln_tn(const GemmArgs& a);
 // results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
 int gemm_splitk_factor(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
+// two lazy-LN GEMMs (epi 1 or 2) of the same tile instantiation as ONE persistent launch
+// (option clip_group: the ViT and CLIP-text GEMMs of a layer); hipErrorNotSupported if they differ
+// two lazy-LN GEMMs (same tile, epilogue and activation: gemm_group_ok) as one persistent launch
+bool gemm_group_ok(const GemmArgs& a, const GemmArgs& b);
+hipError_t launch_gemm_group(const GemmArgs& a, const GemmArgs& b, hipStream_t s);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks
 constexpr int kGemmConfigs = 17;  // numbering of the tile instantiations (0 .. 16; gemm.hip config_exists)
 const char* gemm_config_name(int c);

@@ -451,3 +451,34 @@ def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
                 assert torch.equal(v, out[k]), k
     finally:
         engine.set_option("mt_enqueue", mt)
+
+
+@pytest.mark.parametrize("B", [37, 256])
+def test_clip_group_bit_identical(engine, B):
+    """Option clip_group (round 5): both CLIP towers layer-locked on one stream,
+    each layer's ViT and CLIP-text GEMMs of a kind as one grouped persistent launch
+    (gemm_glds_group_kernel).  Every tile is computed as in its own launch, so the embeddings, the
+    consistency scores and all of analyze_batch's outputs are bit-identical to the two-stream path;
+    ragged captions exercise the causal masks.  B = 256 is BASELINE configs[3]."""
+    import mmf_amd.synthetic as syn
+    rid, rm = syn.roberta_ids(B, 128, 77, [128, 64, 9])
+    cid, cm = syn.clip_ids(B, 77, 77, [77, 33, 6, 50])
+    imgs = syn.images(B, 77)
+
+    def run():
+        out = {k: v.clone() for k, v in engine.analyze_batch(rid, rm, cid, cm, imgs).items()}
+        out.update({"cons_" + k: v.clone() for k, v in engine.clip_consistency(imgs, cid, cm).items()})
+        torch.cuda.synchronize()
+        return out
+    old = engine.get_option("clip_group")
+    try:
+        engine.set_option("clip_group", 0)
+        ref = run()
+        for grp in (1, 2):  # (2: the grouped consumers on 256x192 tiles)
+            engine.set_option("clip_group", grp)
+            for _ in range(2):
+                out = run()
+                for k, v in ref.items():
+                    assert torch.equal(v, out[k]), (grp, k)
+    finally:
+        engine.set_option("clip_group", old)

@@ -37,7 +37,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--what", default="clip,text,effnet", help="comma list of clip, text, effnet, step")
     a = ap.parse_args()
+    what = set(a.what.split(","))
     import mmf_amd.synthetic as syn
     import mmf_amd.weights as W
     from mmf_amd.engine import Engine
@@ -59,17 +61,34 @@ def main():
     def add(k, v):
         res.setdefault(k, []).append(round(v, 3))
     for r in range(a.rounds):
-        eng.set_option("concurrent", 1)
-        add("clip_concurrent_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
-        eng.set_option("concurrent", 0)
-        add("clip_serial_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
-        eng.set_option("concurrent", 1)
-        add("vit_alone_ms", timed(lambda: eng.clip_image(img), a.steps))
-        add("clip_text_alone_ms", timed(lambda: eng.clip_text(cid, cm), a.steps))
-        for mode in (0, 1, 2):
-            eng.set_option("text_hilo", mode)
-            add(f"roberta_text_hilo{mode}_ms", timed(lambda: eng.text_forward(rid, rm), a.steps))
-        eng.set_option("text_hilo", -1)
+        if "clip" in what:
+            eng.set_option("concurrent", 1)
+            add("clip_concurrent_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
+            for grp in (1, 2):
+                eng.set_option("clip_group", grp)
+                add(f"clip_grouped{grp}_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
+            eng.set_option("clip_group", 0)
+            eng.set_option("concurrent", 0)
+            add("clip_serial_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
+            eng.set_option("concurrent", 1)
+            add("vit_alone_ms", timed(lambda: eng.clip_image(img), a.steps))
+            add("clip_text_alone_ms", timed(lambda: eng.clip_text(cid, cm), a.steps))
+        if "step" in what:
+            ab_out = eng.alloc_outputs(B)
+            for grp in (0, 1, 2):
+                eng.set_option("clip_group", grp)
+                add(f"analyze_b256_clip_group{grp}_ms", timed(lambda: eng.analyze_batch(rid, rm, cid, cm, img, out=ab_out), a.steps))
+            eng.set_option("clip_group", 0)
+        if "text" in what:
+            for mode in (0, 1, 2):
+                eng.set_option("text_hilo", mode)
+                add(f"roberta_text_hilo{mode}_ms", timed(lambda: eng.text_forward(rid, rm), a.steps))
+            eng.set_option("text_hilo", -1)
+    if "effnet" not in what:
+        print(json.dumps({k: {"rounds": v, "min": min(v), "median": sorted(v)[len(v) // 2]} for k, v in res.items()},
+                         indent=1), flush=True)
+        eng.close()
+        return
     eng.reserve(512, 128, 77)
     img5 = torch.from_numpy(syn.images(512, 99)).to(dev)
     for r in range(a.rounds):
