@@ -416,7 +416,7 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : 3) void expand_dw_ke
                                                         const f16_t* __restrict__ we, const float* __restrict__ be,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         f16_t* __restrict__ out, float* __restrict__ pool_part, int H,
-                                                        int W, int C, int CW_, int T_, int tiles_x) {
+                                                        int W, int C, int CW_, int T_, int tiles_x, int gpb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
   constexpr int PAD = (K - 1) / 2, KP = KS * 32;
   constexpr int CW = 48, NF = CW / 16;  // the host launches 48-channel groups only
@@ -479,8 +479,11 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : 3) void expand_dw_ke
       pbe = be[c0 + tid];
     }
   };
-  if (MMF_EDW_PF) fetch_w(0);
-  for (int c0 = 0; c0 < C; c0 += CW) {
+  // this block's channel groups: gpb of them from blockIdx.y * gpb (launch_expand_dw splits the groups
+  // over blocks when the launch has too few tiles to fill the chip)
+  const int cbeg = blockIdx.y * gpb * CW, cend = min(C, cbeg + gpb * CW);
+  if (MMF_EDW_PF) fetch_w(cbeg);
+  for (int c0 = cbeg; c0 < cend; c0 += CW) {
     if (!MMF_EDW_PF) fetch_w(c0);
 #pragma unroll
     for (int j = 0; j < NPE; ++j) {
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : 3) void expand_dw_ke
     }
     __syncthreads();
     EST()
-    if (MMF_EDW_PF && c0 + CW < C) fetch_w(c0 + CW);
+    if (MMF_EDW_PF && c0 + CW < cend) fetch_w(c0 + CW);
 
     // ---- expand the input tile (+halo) into LDS: every MFMA of a fragment row issued before its
     // epilogues (the group's weight fragments and bias held in registers) ----
@@ -968,6 +971,10 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
   return hipErrorInvalidValue;
 }
 
+#ifndef MMF_EDW_SPLIT_BELOW
+#define MMF_EDW_SPLIT_BELOW 8192  // fused fronts with fewer (tile, image) blocks split their channel groups (0: never; B = 512: 3.502 -> 3.475 ms)
+#endif
+
 bool expand_dw_applicable(int cin, int cexp) { return cin <= 64 && (cin % 8) == 0 && (cexp % 48) == 0; }
 
 hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const float* be, const float* w,
@@ -982,11 +989,18 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
   const size_t smem =
       (size_t)dw_tile_bytes(IT, CW, false) + (size_t)(k * k * CW + CW + PX * CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
   const size_t smem_ct = (size_t)dw_tile_bytes(IT, CW, true) + (size_t)(k * k * CW + CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
-  const dim3 grid(ntiles, 1, B), blk(256);
+  // launches with few tiles (the 28^2 / 14^2 stages) split their channel groups over blocks: one
+  // block per (tile, group) instead of a block walking every group, so the chip fills (each block
+  // re-reads its Cin-channel input tile from L2; every output and pool partial is computed as before)
+  const int groups = C / CW;
+  const long blocks = (long)ntiles * B;
+  const int split = blocks < MMF_EDW_SPLIT_BELOW ? groups : 1;
+  const int gpb = (groups + split - 1) / split;
+  const dim3 grid(ntiles, (groups + gpb - 1) / gpb, B), blk(256);
 #define MMF_EDWCT(KK, SS, QS, TT, RR)                                                                       \
   if (k == KK && stride == SS && KS == QS && T == TT) {                                                       \
     hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, TT, RR>), grid, blk, smem_ct, s, x, cin, we, be, w, bias, out, \
-                       pool_part, H, W, C, CW, T, tiles_x);                                                   \
+                       pool_part, H, W, C, CW, T, tiles_x, gpb);                                              \
     return hipGetLastError();                                                                                 \
   }
   if (ct) {
@@ -1000,7 +1014,7 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
 #define MMF_EDW(KK, SS, QS)                                                                                      \
   if (k == KK && stride == SS && KS == QS) {                                                                     \
     hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, 0, 1>), grid, blk, smem, s, x, cin, we, be, w, bias, out,    \
-                       pool_part, H, W, C, CW, T, tiles_x);                                                      \
+                       pool_part, H, W, C, CW, T, tiles_x, gpb);                                                 \
     return hipGetLastError();                                                                                    \
   }
   // runtime-geometry kernels (shapes past B0's, or ct = 0)
