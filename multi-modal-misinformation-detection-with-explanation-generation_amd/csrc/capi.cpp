@@ -159,6 +159,9 @@ struct Options {
   int clip_group = 0;   // CLIP towers layer-locked on one stream, each layer's ViT + text GEMMs of a kind as one
                         // grouped persistent launch (run_clip_pair); 0: the towers on two streams
   int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
+  int after_text = 12;  // towers of the concurrent B > mt_enqueue step that start only once RoBERTa is done
+                        // (bitmask as diag_skip: 2 EfficientNet, 4 CLIP text, 8 ViT)
+  int after_layer = 12; // ... or once RoBERTa has enqueued its layers 0 .. after_layer - 1 (12: the whole tower)
 };
 // (Round 5 removed the options whose variants were measured slower and stayed off: gemm_ring, gemm_wide,
 // gemm_w4, dw_v2, dw_persist, ln_prod256, cu_split, fuse_expand32, qkv_attn_gm, splitk_fix, gemm_tq,
@@ -175,7 +178,8 @@ const OptName kOptNames[] = {
     {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"}, {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
     {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},
-    {"clip_group", &Options::clip_group, "MMF_CLIP_GROUP"},
+    {"clip_group", &Options::clip_group, "MMF_CLIP_GROUP"}, {"after_text", &Options::after_text, "MMF_AFTER_TEXT"},
+    {"after_layer", &Options::after_layer, "MMF_AFTER_LAYER"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -324,6 +328,7 @@ struct mmf_handle {
   // fork/join streams of mmf_analyze_batch (text, effnet, clip-text towers beside the caller's)
   hipStream_t tower[3] = {nullptr, nullptr, nullptr};
   hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t text_ev = nullptr;  // RoBERTa tower done (option after_text)
   // option mt_enqueue (lazily started).  Invariant: while the workers enqueue, no tower writes to the
   // handle -- every per-launch choice is read from `opt` (set between calls, never during one) and
   // every workspace is reserved before the call (mmf_reserve); the towers' launch sequences only read
@@ -348,6 +353,7 @@ struct mmf_handle {
       if (join_ev[i]) (void)hipEventDestroy(join_ev[i]);
     }
     if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (text_ev) (void)hipEventDestroy(text_ev);
   }
 };
 
@@ -952,10 +958,14 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
 }
 
 int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
-             float* scores, int score_stride, hipStream_t s) {
+             float* scores, int score_stride, hipStream_t s, hipEvent_t mid_ev = nullptr, int mid_layer = 12) {
   Workspace& w = h->ws;
   const int hilo = text_mode(h);
-  if (hilo >= 2) return run_text_precise(h, ids, mask, B, L, ai, mi, scores, score_stride, s);
+  if (hilo >= 2) {
+    CHK(run_text_precise(h, ids, mask, B, L, ai, mi, scores, score_stride, s));
+    if (mid_ev) HIPCHK(hipEventRecord(mid_ev, s));
+    return 0;
+  }
   uint16_t* rlo = hilo ? w.r_lo : nullptr;
   const int M = B * L;
   {
@@ -965,6 +975,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   }
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = h->r_layers[i];
+    if (mid_ev && i == mid_layer) HIPCHK(hipEventRecord(mid_ev, s));  // option after_layer
     // last layer: only the CLS row feeds the heads (misinfo_forensics.py:95), so the rows below
     // run on B compact CLS rows (strided A / residual reads) instead of B*L rows
     const bool last = (i == 11);
@@ -1544,6 +1555,7 @@ int ensure_towers(mmf_handle* h) {
     HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
   }
   HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->text_ev, hipEventDisableTiming));
   return 0;
 }
 
@@ -2018,11 +2030,27 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
     CHK(rc);
     if (wrc) return fail(wrc, "%s", werr.c_str());
   } else {
-    if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
+    // option after_text: the chosen towers' streams wait for the RoBERTa tower (its persistent GEMMs
+    // then own every CU instead of sharing them with the other towers' launches)
+    const int after = concurrent && !(skip & 1) ? h->opt.after_text : 0;
+    const int mid = after && h->opt.after_layer >= 0 && h->opt.after_layer < 12 ? h->opt.after_layer : 12;
+    if (!(skip & 1))
+      CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text, mid < 12 ? h->text_ev : nullptr,
+                   mid));
+    if (after) {
+      if (mid == 12) HIPCHK(hipEventRecord(h->text_ev, st_text));
+      if (after & 2) HIPCHK(hipStreamWaitEvent(st_eff, h->text_ev, 0));
+      if (after & 4) HIPCHK(hipStreamWaitEvent(st_ctxt, h->text_ev, 0));
+      if (after & 8) HIPCHK(hipStreamWaitEvent(s, h->text_ev, 0));
+    }
+    // after_text bit 16 / 32: the EfficientNet tower chained behind the CLIP-text / ViT tower on that
+    // tower's stream instead of on a stream of its own
+    const hipStream_t st_e = (after & 16) ? st_ctxt : (after & 32) ? s : st_eff;
     if (!(skip & 4) && !pair) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
-    if (!(skip & 2)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
+    if (!(skip & 2) && !(after & 32)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_e));
     if (pair) CHK(run_clip_pair(h, img_clip, clip_ids, clip_mask, B, Lc, w.v_emb, w.t_emb, s));
     else if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
+    if (!(skip & 2) && (after & 32)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_e));
   }
   if (concurrent) {
     for (int i = 0; i < 3; ++i) {
