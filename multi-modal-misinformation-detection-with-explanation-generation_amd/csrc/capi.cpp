@@ -139,6 +139,7 @@ struct Options {
   int concurrent = 1;   // towers of mmf_analyze_batch on concurrent streams
   int fuse_stem = 1;    // stem fused into the stage-1 depthwise conv
   int fuse_expand = 1;  // 1x1 expand fused into the depthwise conv (stages 2-4)
+  int fuse_expand_cin = 96;  // ... and for 3 x 3 blocks of up to this many input channels (<= 96; 96: + stages 4.2 / 4.3)
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
@@ -169,7 +170,7 @@ struct Options {
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
-    {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"},
+    {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"}, {"fuse_expand_cin", &Options::fuse_expand_cin, "MMF_FUSE_EXPAND_CIN"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
     {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
@@ -1500,7 +1501,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
     int nch = 0;
     const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
     // option fuse_expand = 0: separate expand launch (A/B)
-    const bool fuse = b.expand != 1 && expand_dw_applicable(b.cin, b.cexp) && h->opt.fuse_expand;
+    const bool fuse = b.expand != 1 && h->opt.fuse_expand && expand_dw_applicable(b.cin, b.cexp, b.k, h->opt.fuse_expand_cin);
     if (&b == &b0 && fuse_stem) {
       // stem output recomputed per 18x18 halo tile: 1.27x the stem MACs, image patch read once
       ProfScope ps(h, s, PK_DW, 2.0 * B * 112 * 112 * 32 * (9 + 27 * 1.27),

@@ -412,7 +412,7 @@ template <int K, int S, int KS, int TT, int R>
 #ifndef MMF_EDW_MINB1
 #define MMF_EDW_MINB1 4  // resident blocks per CU hipcc budgets registers for (KS = 1: stage 3.1 148 -> 128 VGPRs, 4 blocks/CU; -0.9 %)
 #endif
-__global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : 3) void expand_dw_kernel(const f16_t* __restrict__ x, int Cin,
+__global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) void expand_dw_kernel(const f16_t* __restrict__ x, int Cin,
                                                         const f16_t* __restrict__ we, const float* __restrict__ be,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         f16_t* __restrict__ out, float* __restrict__ pool_part, int H,
@@ -975,14 +975,20 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
 #define MMF_EDW_SPLIT_BELOW 8192  // fused fronts with fewer (tile, image) blocks split their channel groups (0: never; B = 512: 3.502 -> 3.475 ms)
 #endif
 
-bool expand_dw_applicable(int cin, int cexp) { return cin <= 64 && (cin % 8) == 0 && (cexp % 48) == 0; }
+// Cin <= 64 (stages 2 - 4.1, KS <= 2), and 3 x 3 blocks of Cin <= min(max_cin, 96) (stages 4.2 / 4.3:
+// Cin 80, KS = 3; their two launches 28 + 33 -> 45 us per 256 images).  The 5 x 5 blocks of Cin 80 / 112
+// (stages 5.1 - 6.1, KS = 3 / 4) measured a tie or slower fused (230-256 VGPRs: two waves per SIMD).
+bool expand_dw_applicable(int cin, int cexp, int k, int max_cin) {
+  const bool ok_cin = cin <= 64 || (k == 3 && cin <= max_cin && cin <= 96);
+  return ok_cin && (cin % 8) == 0 && (cexp % 48) == 0;
+}
 
 hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const float* be, const float* w,
                             const float* bias, f16_t* out, float* pool_part, int B, int H, int W, int C, int k,
                             int stride, int* nchunks_out, hipStream_t s, int ct) {
   int T, CW, tiles_x, ntiles;
   dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
-  if (!expand_dw_applicable(cin, C) || CW != 48) return hipErrorInvalidValue;
+  if (!expand_dw_applicable(cin, C, k, 96) || CW != 48) return hipErrorInvalidValue;
   *nchunks_out = ntiles;
   const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8), KS = (cin + 31) / 32;
   if (IT > 19) return hipErrorInvalidValue;  // the kernel's MAXRF prefetch depth
@@ -1009,6 +1015,7 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
     MMF_EDWCT(5, 1, 2, 14, MMF_R_E32)
     MMF_EDWCT(5, 2, 1, 7, MMF_R_E31)
     MMF_EDWCT(3, 2, 2, 7, MMF_R_E41)
+    MMF_EDWCT(3, 1, 3, 14, MMF_R_D14)  // stages 4.2 / 4.3 (Cin 80)
   }
 #undef MMF_EDWCT
 #define MMF_EDW(KK, SS, QS)                                                                                      \
@@ -1019,6 +1026,7 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
   }
   // runtime-geometry kernels (shapes past B0's, or ct = 0)
   MMF_EDW(3, 2, 1) MMF_EDW(3, 1, 1) MMF_EDW(5, 2, 1) MMF_EDW(5, 1, 2) MMF_EDW(3, 2, 2)
+  MMF_EDW(3, 1, 3)
 #undef MMF_EDW
   return hipErrorInvalidValue;
 }

@@ -164,7 +164,7 @@ hipError_t launch_gap_classifier(const f16_t* x, int HW, int C, const float* w, 
 hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);
 // fused MBConv front: expand 1x1 (we fp16 [C][cin], be fp32, BN folded) + SiLU computed per input
 // tile into LDS, then the depthwise conv of launch_dwconv (same outputs, same pool partials)
-bool expand_dw_applicable(int cin, int cexp);
+bool expand_dw_applicable(int cin, int cexp, int k, int max_cin);
 hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const float* be, const float* w,
                             const float* bias, f16_t* out, float* pool_part, int B, int H, int W, int C, int k,
                             int stride, int* nchunks_out, hipStream_t s, int ct = 1);
