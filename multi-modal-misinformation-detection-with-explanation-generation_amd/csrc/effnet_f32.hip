@@ -196,6 +196,130 @@ __global__ __launch_bounds__(256) void pw32m_kernel(const float* __restrict__ A,
   }
 }
 
+// Small-K / narrow-N form of the same contraction (pw32_mfma = 3, K <= 64 and N <= 256: the expands of
+// stages 2.1 - 4.1 and the stage-1 project, which write 6-10x the bytes they read): one block owns 64
+// WHOLE output rows (every column), so its output is one contiguous run of 64 N floats.  Wave w computes
+// rows 16 w .. 16 w + 15 over all NF = ceil(N / 16) column blocks on the fp32-input MFMA with the K
+// chunks, LDS images and step order of pw32m_kernel -- every output element is the same ascending-k
+// fmaf chain, then + bias, activation, + residual in the same order: BIT-IDENTICAL -- and the finished
+// (bias + activation) tile goes to LDS in its global row-major layout, from where the block stores it
+// (residual added on the way) as consecutive 16-B lanes: full-line writes instead of pw32m's 64-B row
+// pieces per 16 rows (the write rate, not the arithmetic, bounds these launches).
+template <int NF, int D>
+__global__ __launch_bounds__(256) void pw32r_kernel(const float* __restrict__ A, const float* __restrict__ Wt,
+                                                    const float* __restrict__ bias, const float* __restrict__ ascale,
+                                                    int rows_per_image, const float* __restrict__ res,
+                                                    float* __restrict__ C, int M, int N, int K, int act, int NC) {
+  constexpr int NT = NF * 16, AS = QB * QK, WS = NT * QK;
+  extern __shared__ __attribute__((aligned(16))) float r_smem[];
+  // column tile: columns n0 .. n0 + nc of every row (NC = N, one tile, below 256 columns; wider
+  // launches split N into equal multiples of 16)
+  const int n0 = blockIdx.y * NC, nc = min(NC, N - n0);
+  float* As = r_smem;           // [2][QB * QK]
+  float* Ws = r_smem + 2 * AS;  // [2][NT * QK]
+  float* Cs = r_smem;           // [QB][nc] (aliases As / Ws once the K loop is done)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int m0 = blockIdx.x * QB;
+  // loaders: A chunk 64 x 16 = one float4 per thread (row lr, k quad lc); W chunk NT x 16 = NF / 4
+  // float4 per thread (rows wr0 + 64 q)
+  const int lr = tid >> 2, lc = tid & 3;
+  const int am = m0 + lr;
+  const float* sc = (ascale && am < M) ? ascale + (size_t)(am / rows_per_image) * K : nullptr;
+  constexpr int WQ = (NT * 4 + 255) / 256;  // float4 of the W chunk per thread
+  auto gload = [&](int k0, float4& a, float4 (&w)[WQ]) {
+    const int k = k0 + lc * 4;  // K % 4 == 0: a quad is in or out whole
+    a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (am < M && k < K) {
+      a = *reinterpret_cast<const float4*>(A + (size_t)am * K + k);
+      if (sc) {
+        const float4 s4 = *reinterpret_cast<const float4*>(sc + k);
+        a.x *= s4.x; a.y *= s4.y; a.z *= s4.z; a.w *= s4.w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int wr = lr + 64 * q;
+      w[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (wr < nc && k < K) w[q] = *reinterpret_cast<const float4*>(Wt + (size_t)(n0 + wr) * K + k);
+    }
+  };
+  auto lstore = [&](int buf, const float4& a, const float4 (&w)[WQ]) {  // k = 4 lc + e -> [row][g = e][s = lc]
+    const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) As[buf * AS + q_off(lr, e) + lc] = av[e];
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int wr = lr + 64 * q;
+      if (wr < NT) {
+        const float wv[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Ws[buf * WS + q_off(wr, e) + lc] = wv[e];
+      }
+    }
+  };
+  f32x4 acc[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nch = (K + QK - 1) / QK;
+  // register slots: chunk c is requested D - 1 chunks before the one that stores it to LDS (pw32m's
+  // scheme; D = 2 for the K <= 64 launches, deeper for the long-K projects)
+  float4 ra[D], rw[D][WQ];
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d)
+    if (d < nch) gload(d * QK, ra[d], rw[d]);
+  lstore(0, ra[0], rw[0]);
+  __syncthreads();
+  for (int c0 = 0; c0 < nch; c0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int c = c0 + d;
+      if (c >= nch) break;
+      const int buf = c & 1;
+      if (c + D - 1 < nch) gload((c + D - 1) * QK, ra[(d + D - 1) % D], rw[(d + D - 1) % D]);
+      const float4 xf = *reinterpret_cast<const float4*>(&As[buf * AS + q_off(wave * 16 + fr, fg)]);
+      const float xfs[4] = {xf.x, xf.y, xf.z, xf.w};
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        const float4 wf = *reinterpret_cast<const float4*>(&Ws[buf * WS + q_off(i * 16 + fr, fg)]);
+        const float wfs[4] = {wf.x, wf.y, wf.z, wf.w};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wfs[st], xfs[st], acc[i], 0, 0, 0);
+      }
+      if (c + 1 < nch) lstore(buf ^ 1, ra[(d + 1) % D], rw[(d + 1) % D]);
+      __syncthreads();
+    }
+  }
+  // lane: C[m][n .. n + 3] of each 16 x 16 block (operands swapped) -> + bias, activation -> LDS tile
+  const int ml = wave * 16 + fr;
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int n = i * 16 + fg * 4;
+    if (n < nc) {  // N % 4 == 0, NC % 16 == 0
+      const float4 bv = *reinterpret_cast<const float4*>(bias + n0 + n);
+      float o[4] = {acc[i][0] + bv.x, acc[i][1] + bv.y, acc[i][2] + bv.z, acc[i][3] + bv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act_precise(o[e], act);
+      *reinterpret_cast<float4*>(&Cs[ml * nc + n]) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  __syncthreads();
+  // the block's rows: nc contiguous floats each (one contiguous run of C when nc = N), stored (and the
+  // residual read) as consecutive 16-B lanes
+  const int rows = min(QB, M - m0), q4 = nc / 4;
+  const float4* cs4 = reinterpret_cast<const float4*>(Cs);
+  for (int idx = tid; idx < rows * q4; idx += 256) {
+    const int r = idx / q4, cq = idx - r * q4;
+    const size_t g = (size_t)(m0 + r) * N + n0 + 4 * cq;
+    float4 v = cs4[idx];
+    if (res) {
+      const float4 rv = *reinterpret_cast<const float4*>(res + g);
+      v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+    }
+    *reinterpret_cast<float4*>(C + g) = v;
+  }
+}
+
 #ifndef MMF_DW32_R
 #define MMF_DW32_R 7  // outputs per thread along x (every EfficientNet-B0 width is a multiple of 7)
 #endif
@@ -328,6 +452,30 @@ hipError_t launch_pw32(const float* A, const float* W, const float* bias, const 
   if (M <= 0 || N <= 0 || K <= 0 || (N % 4) || (K % 4) || (ascale && rows_per_image <= 0) ||
       (act != ACT_NONE && act != ACT_SILU))
     return hipErrorInvalidValue;
+  if (mfma >= 3 && N <= 256 && (K <= 64 || mfma >= 4)) {
+    // mfma = 3: the whole-row tile kernel for the small-K, write-bound launches; 4 (default): also
+    // for every long-K launch of N <= 256 (the projects: A read once instead of once per 64-column
+    // tile).  The wider launches (N 320 ... 1280) stay on pw32m: split into <= 256-column tiles of
+    // this kernel they measured slower (B = 512 tower 11.39 -> 11.86 ms)
+    const int ntl = (N + 255) / 256;
+    const int NC = ((N + ntl - 1) / ntl + 15) / 16 * 16;
+    const int NF = NC / 16;
+    const size_t lds = std::max((size_t)(2 * QB * QK + 2 * NF * 16 * QK), (size_t)QB * NC) * 4;
+    const dim3 grid((M + QB - 1) / QB, (N + NC - 1) / NC);
+    const bool deep = K >= 4 * QK;
+    switch (NF) {
+#define MMF_PW32R(F)                                                                                              \
+  case F:                                                                                                         \
+    if (deep) hipLaunchKernelGGL((pw32r_kernel<F, 4>), grid, dim3(256), lds, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act, NC); \
+    else hipLaunchKernelGGL((pw32r_kernel<F, 2>), grid, dim3(256), lds, s, A, W, bias, ascale, rows_per_image, res, C, M, N, K, act, NC); \
+    break;
+      MMF_PW32R(1) MMF_PW32R(2) MMF_PW32R(3) MMF_PW32R(4) MMF_PW32R(5) MMF_PW32R(6) MMF_PW32R(7) MMF_PW32R(8)
+      MMF_PW32R(9) MMF_PW32R(10) MMF_PW32R(11) MMF_PW32R(12) MMF_PW32R(13) MMF_PW32R(14) MMF_PW32R(15) MMF_PW32R(16)
+#undef MMF_PW32R
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (mfma) {
     // mfma = 1: loads one chunk ahead (round 3); 2: three chunks ahead where K has >= 4 chunks and
     // the grid leaves < 4 workgroups per CU (the 7^2-stage projects, K = 672 / 1152: 134 -> 107 and
