@@ -20,6 +20,6 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write -o run -- 
 # reduce on the box (raw PMC csvs can pass gpurun's 64 MiB copy-back)
 python3 $R/tools/rocprof_summary.py $OUT/trace/run_results.db > $OUT/steady_state_kernels.txt 2>&1 || true
 python3 $R/tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv \
-  --symbol 'gemm_glds_kernel<256, 192, 4, 2, 0, true, 0>' --json $OUT/pmc_traffic.json > $OUT/pmc_traffic.txt 2>&1 || true
+  --symbol 'gemm_glds_kernel<256, 192, 4, 2, 0, true, 0, 0>' --json $OUT/pmc_traffic.json > $OUT/pmc_traffic.txt 2>&1 || true
 rm -f $OUT/pmc_fetch/*.csv $OUT/pmc_write/*.csv
 echo done > $OUT/ok
