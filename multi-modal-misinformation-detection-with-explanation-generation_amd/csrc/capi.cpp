@@ -2045,14 +2045,10 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
       if (after & 4) HIPCHK(hipStreamWaitEvent(st_ctxt, h->text_ev, 0));
       if (after & 8) HIPCHK(hipStreamWaitEvent(s, h->text_ev, 0));
     }
-    // after_text bit 16 / 32: the EfficientNet tower chained behind the CLIP-text / ViT tower on that
-    // tower's stream instead of on a stream of its own
-    const hipStream_t st_e = (after & 16) ? st_ctxt : (after & 32) ? s : st_eff;
     if (!(skip & 4) && !pair) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
-    if (!(skip & 2) && !(after & 32)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_e));
+    if (!(skip & 2)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
     if (pair) CHK(run_clip_pair(h, img_clip, clip_ids, clip_mask, B, Lc, w.v_emb, w.t_emb, s));
     else if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
-    if (!(skip & 2) && (after & 32)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_e));
   }
   if (concurrent) {
     for (int i = 0; i < 3; ++i) {
