@@ -728,21 +728,24 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
   {
     constexpr int OPW = 4;  // outputs per wave (Csq <= 64 = 16 waves x 4)
     float acc[OPW] = {0.f, 0.f, 0.f, 0.f};
+    // the wave's outputs walk C together: per step 4 weights of every output in flight (16 loads, one
+    // L2 round trip per step for all outputs); each output's FMAs stay in ascending c (lane, lane + 64, ...)
+    for (int c = lane; c < C; c += 256) {
+      float wv[OPW][4];
 #pragma unroll
-    for (int t = 0; t < OPW; ++t) {
-      const int o = wave + 16 * t;
-      if (o < Csq) {
-        const float* wr = w1 + (size_t)o * C;
-        int c = lane;
-        for (; c + 192 < C; c += 256) {  // 4 loads in flight per output (same ascending-c order)
-          const float w0 = wr[c], w1v = wr[c + 64], w2v = wr[c + 128], w3 = wr[c + 192];
-          acc[t] = fmaf(w0, pooled[c], acc[t]);
-          acc[t] = fmaf(w1v, pooled[c + 64], acc[t]);
-          acc[t] = fmaf(w2v, pooled[c + 128], acc[t]);
-          acc[t] = fmaf(w3, pooled[c + 192], acc[t]);
+      for (int t = 0; t < OPW; ++t) {
+        const int o = wave + 16 * t;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int cc = c + 64 * u;
+          wv[t][u] = (o < Csq && cc < C) ? w1[(size_t)o * C + cc] : 0.f;
         }
-        for (; c < C; c += 64) acc[t] = fmaf(wr[c], pooled[c], acc[t]);
       }
+#pragma unroll
+      for (int t = 0; t < OPW; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (wave + 16 * t < Csq && c + 64 * u < C) acc[t] = fmaf(wv[t][u], pooled[c + 64 * u], acc[t]);
     }
 #pragma unroll
     for (int t = 0; t < OPW; ++t) {
@@ -755,8 +758,20 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
   for (int c = tid; c < C; c += SE_THREADS) {
     float a0 = b2[c], a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int j = 0;
-    // 16 weight loads in flight per step (one L2 round trip per 16 inputs instead of per 4); the
+    // 32 weight loads in flight per step (one L2 round trip per 32 inputs: Csq <= 64 in two); the
     // accumulation order is unchanged (input j -> accumulator j % 4, ascending j)
+    for (; j + 32 <= Csq; j += 32) {
+      float wv[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) wv[u] = w2t[(size_t)(j + u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 32; u += 4) {
+        a0 = fmaf(wv[u], s1[j + u], a0);
+        a1 = fmaf(wv[u + 1], s1[j + u + 1], a1);
+        a2 = fmaf(wv[u + 2], s1[j + u + 2], a2);
+        a3 = fmaf(wv[u + 3], s1[j + u + 3], a3);
+      }
+    }
     for (; j + 16 <= Csq; j += 16) {
       float wv[16];
 #pragma unroll
