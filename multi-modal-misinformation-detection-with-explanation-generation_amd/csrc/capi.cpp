@@ -148,9 +148,9 @@ struct Options {
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
   int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
-  int pw32_mfma = 4;    // fp32 tower's 1x1 convs on the fp32-input MFMA (2: loads 3 K-chunks ahead, 1: one ahead;
-                        // 3 / 4: whole-row tiles for the N <= 256 launches with K <= 64 / any K) or the
-                        // fp32-FMA VALU kernel (0) -- every mode bit-identical
+  int pw32_mfma = 5;    // fp32 tower's 1x1 convs on the fp32-input MFMA (2: loads 3 K-chunks ahead, 1: one ahead;
+                        // 3 / 4: whole-row tiles for the N <= 256 launches with K <= 64 / any K; 5: 4 where the
+                        // row grid has the blocks for it) or the fp32-FMA VALU kernel (0) -- every mode bit-identical
   int dw_cw32 = 1;      // 32-channel groups for the standalone depthwise convs (effnet.hip dw_geometry; B=512 3.648 -> 3.595 ms)
   int effnet_chunks = 2;  // mmf_effnet_forward: batch chunks on concurrent streams (B=512: 3.82 -> 3.57 ms in bench.py)
   int qkv_attn = 1;     // RoBERTa L = 128: attention in the QKV GEMM's epilogue (gemm.hip epi 3)

@@ -452,7 +452,11 @@ hipError_t launch_pw32(const float* A, const float* W, const float* bias, const 
   if (M <= 0 || N <= 0 || K <= 0 || (N % 4) || (K % 4) || (ascale && rows_per_image <= 0) ||
       (act != ACT_NONE && act != ACT_SILU))
     return hipErrorInvalidValue;
-  if (mfma >= 3 && N <= 256 && (K <= 64 || mfma >= 4)) {
+  // mode 5: mode 4 only where the whole-row grid has the parallelism for its long K (>= 1024 blocks,
+  // or >= 512 at NF <= 5): the 14^2 / 7^2 projects with 112 / 192 columns keep pw32m's 64-column tiles
+  const long rblocks = (M + QB - 1) / QB;
+  const bool rows_ok = mfma != 5 || rblocks >= 1024 || (N <= 80 && rblocks >= 512);
+  if (mfma >= 3 && N <= 256 && (K <= 64 || (mfma >= 4 && rows_ok))) {
     // mfma = 3: the whole-row tile kernel for the small-K, write-bound launches; 4 (default): also
     // for every long-K launch of N <= 256 (the projects: A read once instead of once per 64-column
     // tile).  The wider launches (N 320 ... 1280) stay on pw32m: split into <= 256-column tiles of

@@ -113,7 +113,8 @@ def test_fp32_tower_mfma_pointwise_bit_identical(det_sd, clip_sd):
     """The fp32 tower's 1x1 convolutions on the fp32-input MFMA (option pw32_mfma = 1: loads one
     K-chunk ahead; 2: three chunks ahead where K allows -- v_mfma_f32_16x16x4_f32 is a k-ordered
     fp32 fmaf chain; 3, round 5: + whole-row tiles with row-contiguous stores for the K <= 64,
-    N <= 256 launches; 4, default: for every N <= 256 launch) against the fp32-FMA VALU kernel
+    N <= 256 launches; 4: for every N <= 256 launch; 5, default: 4 where the grid has >= 512-1024
+    row blocks) against the fp32-FMA VALU kernel
     (pw32_mfma = 0): every logit bit-identical, on the ill-conditioned He draw the mode exists for."""
     import mmf_amd.synthetic as syn
     import mmf_amd.weights as W
@@ -124,7 +125,7 @@ def test_fp32_tower_mfma_pointwise_bit_identical(det_sd, clip_sd):
         imgs = syn.images(64, 29)
         eng.set_option("pw32_mfma", 0)
         lg0, _ = eng.effnet_forward(imgs)
-        for mode in (1, 2, 3, 4):
+        for mode in (1, 2, 3, 4, 5):
             eng.set_option("pw32_mfma", mode)
             lg1, _ = eng.effnet_forward(imgs)
             torch.cuda.synchronize()
