@@ -138,8 +138,7 @@ struct Workspace {
 struct Options {
   int concurrent = 1;   // towers of mmf_analyze_batch on concurrent streams
   int fuse_stem = 1;    // stem fused into the stage-1 depthwise conv
-  int fuse_expand = 1;  // 1x1 expand fused into the depthwise conv (stages 2-4)
-  int fuse_expand_cin = 96;  // ... and for 3 x 3 blocks of up to this many input channels (<= 96; 96: + stages 4.2 / 4.3)
+  int fuse_expand = 1;  // 1x1 expand fused into the depthwise conv (stages 2 - 4.3: effnet.hip expand_dw_applicable)
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
@@ -158,12 +157,9 @@ struct Options {
   int last_q1 = 1;      // compact last encoder layers: K / V of every row, Q + attention of the pooled rows only
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
                         // GEMMs round to as many rounds as QKV: measured slower, off)
-  int clip_group = 0;   // CLIP towers layer-locked on one stream, each layer's ViT + text GEMMs of a kind as one
-                        // grouped persistent launch (run_clip_pair); 0: the towers on two streams
   int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
   int after_text = 12;  // towers of the concurrent B > mt_enqueue step that start only once RoBERTa is done
                         // (bitmask as diag_skip: 2 EfficientNet, 4 CLIP text, 8 ViT)
-  int after_layer = 12; // ... or once RoBERTa has enqueued its layers 0 .. after_layer - 1 (12: the whole tower)
 };
 // (Round 5 removed the options whose variants were measured slower and stayed off: gemm_ring, gemm_wide,
 // gemm_w4, dw_v2, dw_persist, ln_prod256, cu_split, fuse_expand32, qkv_attn_gm, splitk_fix, gemm_tq,
@@ -171,7 +167,7 @@ struct Options {
 struct OptName { const char* name; int Options::*field; const char* env; };
 const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
-    {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"}, {"fuse_expand_cin", &Options::fuse_expand_cin, "MMF_FUSE_EXPAND_CIN"},
+    {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
     {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
@@ -180,8 +176,7 @@ const OptName kOptNames[] = {
     {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"}, {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
     {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},
-    {"clip_group", &Options::clip_group, "MMF_CLIP_GROUP"}, {"after_text", &Options::after_text, "MMF_AFTER_TEXT"},
-    {"after_layer", &Options::after_layer, "MMF_AFTER_LAYER"},
+    {"after_text", &Options::after_text, "MMF_AFTER_TEXT"},
 };
 Options& process_options() {
   static Options o = [] {
@@ -960,14 +955,10 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
 }
 
 int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
-             float* scores, int score_stride, hipStream_t s, hipEvent_t mid_ev = nullptr, int mid_layer = 12) {
+             float* scores, int score_stride, hipStream_t s) {
   Workspace& w = h->ws;
   const int hilo = text_mode(h);
-  if (hilo >= 2) {
-    CHK(run_text_precise(h, ids, mask, B, L, ai, mi, scores, score_stride, s));
-    if (mid_ev) HIPCHK(hipEventRecord(mid_ev, s));
-    return 0;
-  }
+  if (hilo >= 2) return run_text_precise(h, ids, mask, B, L, ai, mi, scores, score_stride, s);
   uint16_t* rlo = hilo ? w.r_lo : nullptr;
   const int M = B * L;
   {
@@ -977,7 +968,6 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   }
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = h->r_layers[i];
-    if (mid_ev && i == mid_layer) HIPCHK(hipEventRecord(mid_ev, s));  // option after_layer
     // last layer: only the CLS row feeds the heads (misinfo_forensics.py:95), so the rows below
     // run on B compact CLS rows (strided A / residual reads) instead of B*L rows
     const bool last = (i == 11);
@@ -1262,25 +1252,6 @@ int run_clip_encoder(mmf_handle* h, ClipEnc& E, int i0, int i1, hipStream_t s) {
   return 0;
 }
 
-// two lazy-LN GEMMs of one layer (the ViT's and the CLIP text tower's) as one persistent launch
-// (option clip_group, gemm.hip gemm_glds_group_kernel), or apart when their tiles differ
-int gemm2(mmf_handle* h, GemmArgs a, GemmArgs b, hipStream_t s) {
-  apply_options(h->opt, &a);
-  apply_options(h->opt, &b);
-  // clip_group 2: consumers on 256x192 tiles (their grouped 256x256 instantiations spill)
-  if (h->opt.clip_group == 2 && a.epi == 1) a.force_cfg = b.force_cfg = 10 + 1;
-  if (!gemm_group_ok(a, b)) {
-    CHK(gemm(h, a, s));
-    return gemm(h, b, s);
-  }
-  const double fl = 2.0 * ((double)a.M * a.N * a.K + (double)b.M * b.N * b.K);
-  const double by = 2.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)b.M * b.K + (double)b.N * b.K) +
-                    2.0 * ((double)a.M * a.N + (double)b.M * b.N) * (a.epi == 2 ? 2 : 1);
-  ProfScope ps(h, s, (gemm_config(a) * kGemmEpis + a.epi) * kGemmActs + a.act, fl, by);
-  HIPCHK(launch_gemm_group(a, b, s));
-  return 0;
-}
-
 int clip_image_embed(mmf_handle* h, const uint8_t* img, int B, hipStream_t s) {
   Workspace& w = h->ws;
   {
@@ -1355,34 +1326,6 @@ int run_clip_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B,
   ClipEnc E = text_enc(h, mask, B, L);
   CHK(run_clip_encoder(h, E, 0, 12, s));
   return clip_text_tail(h, B, emb, s);
-}
-
-// Both CLIP towers layer-locked on ONE stream (option clip_group, both towers lazy-LN): the ViT's and
-// the text tower's GEMM of each kind in layers 0-10 run as one grouped persistent launch (their
-// sub-round grids -- producers 200 + 231 tiles on 256 CUs -- pack into one), the two attentions
-// back to back; the compact last layers and the heads per tower.  Each tower's arithmetic is its
-// own launch's, so the embeddings are bit-identical to the two-stream path.
-bool clip_group_ok(mmf_handle* h, int B, int L) {
-  return h->opt.clip_group && clip_lazy(h, B * 50) && clip_lazy(h, B * L);
-}
-
-int run_clip_pair(mmf_handle* h, const uint8_t* img, const int32_t* ids, const int32_t* mask, int B, int L,
-                  float* iemb, float* temb, hipStream_t s) {
-  CHK(clip_image_embed(h, img, B, s));
-  CHK(clip_text_embed(h, ids, B, L, s));
-  ClipEnc V = vit_enc(h, B), T = text_enc(h, mask, B, L);
-  for (int i = 0; i < 11; ++i) {
-    CHK(gemm2(h, lazy_qkv(V, i), lazy_qkv(T, i), s));
-    CHK(clip_attn(h, V, s));
-    CHK(clip_attn(h, T, s));
-    CHK(gemm2(h, lazy_o(h, V, i), lazy_o(h, T, i), s));
-    CHK(gemm2(h, lazy_fc1(V, i), lazy_fc1(T, i), s));
-    CHK(gemm2(h, lazy_fc2(h, V, i), lazy_fc2(h, T, i), s));
-  }
-  CHK(run_clip_encoder(h, V, 11, 12, s));
-  CHK(run_clip_encoder(h, T, 11, 12, s));
-  CHK(clip_image_tail(h, B, iemb, s));
-  return clip_text_tail(h, B, temb, s);
 }
 
 // EfficientNet-B0 activation elements per image: block input/output, expanded, depthwise output,
@@ -1502,7 +1445,7 @@ int run_effnet(mmf_handle* h, const uint8_t* img, const float* xf32, int B, floa
     int nch = 0;
     const int Ho = (H - 1) / b.stride + 1, Wo = (W - 1) / b.stride + 1;
     // option fuse_expand = 0: separate expand launch (A/B)
-    const bool fuse = b.expand != 1 && h->opt.fuse_expand && expand_dw_applicable(b.cin, b.cexp, b.k, h->opt.fuse_expand_cin);
+    const bool fuse = b.expand != 1 && h->opt.fuse_expand && expand_dw_applicable(b.cin, b.cexp, b.k);
     if (&b == &b0 && fuse_stem) {
       // stem output recomputed per 18x18 halo tile: 1.27x the stem MACs, image patch read once
       ProfScope ps(h, s, PK_DW, 2.0 * B * 112 * 112 * 32 * (9 + 27 * 1.27),
@@ -1873,11 +1816,6 @@ int mmf_clip_consistency(mmf_handle* h, const uint8_t* img, const int32_t* ids, 
   float* ie = img_emb ? img_emb : h->ws.v_emb;
   float* te = txt_emb ? txt_emb : h->ws.t_emb;
   CHK(ensure_towers(h));
-  if (clip_group_ok(h, B, L)) {  // both towers layer-locked on this stream, grouped GEMM launches
-    CHK(run_clip_pair(h, img, ids, mask, B, L, ie, te, s));
-    HIPCHK(launch_rowdot(ie, te, sim, 1, B, 512, s));
-    return 0;
-  }
   const int concurrent = h->opt.concurrent && !h->prof;
   hipStream_t st = s;
   if (concurrent) {  // the text tower beside the vision tower (disjoint workspaces)
@@ -2001,8 +1939,6 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   // diag_skip (diagnostic only, never set by the API or bench.py): towers left out to measure each
   // tower's marginal cost in the concurrent step (bit 1 text, 2 EfficientNet, 4 CLIP text, 8 ViT)
   const int skip = h->opt.diag_skip;
-  // clip_group: the CLIP pair layer-locked on the ViT's stream (run_clip_pair), the text tower's stream idle
-  const bool pair = clip_group_ok(h, B, Lc) && !(skip & 12);
   if (concurrent && h->opt.mt_enqueue > 0 && B <= h->opt.mt_enqueue) {
     // small batches: three host threads enqueue the text, CLIP-text and EfficientNet towers while
     // this thread enqueues the ViT, so every chain starts at once (each stream keeps its own order)
@@ -2011,13 +1947,11 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
       h->pool->start(h->device);
     }
     float* t_emb = w.t_emb;
-    const bool on[3] = {!(skip & 1), !(skip & 4) && !pair, !(skip & 2)};
+    const bool on[3] = {!(skip & 1), !(skip & 4), !(skip & 2)};
     if (on[0]) h->pool->submit(0, [=] { return run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text); });
     if (on[1]) h->pool->submit(1, [=] { return run_clip_text(h, clip_ids, clip_mask, B, Lc, t_emb, st_ctxt); });
     if (on[2]) h->pool->submit(2, [=] { return run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff, 0); });
-    const int rc = pair       ? run_clip_pair(h, img_clip, clip_ids, clip_mask, B, Lc, w.v_emb, t_emb, s)
-                   : (skip & 8) ? 0
-                                : run_clip_image(h, img_clip, B, w.v_emb, s);
+    const int rc = (skip & 8) ? 0 : run_clip_image(h, img_clip, B, w.v_emb, s);
     int wrc = 0;
     std::string werr;
     for (int i = 0; i < 3; ++i) {
@@ -2034,21 +1968,19 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
   } else {
     // option after_text: the chosen towers' streams wait for the RoBERTa tower (its persistent GEMMs
     // then own every CU instead of sharing them with the other towers' launches)
+    // (releasing them before RoBERTa's last layer or two, and EfficientNet chained behind a CLIP tower or
+    // split over two streams, measured slower: DESIGN.md §1 round 5)
     const int after = concurrent && !(skip & 1) ? h->opt.after_text : 0;
-    const int mid = after && h->opt.after_layer >= 0 && h->opt.after_layer < 12 ? h->opt.after_layer : 12;
-    if (!(skip & 1))
-      CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text, mid < 12 ? h->text_ev : nullptr,
-                   mid));
+    if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
     if (after) {
-      if (mid == 12) HIPCHK(hipEventRecord(h->text_ev, st_text));
+      HIPCHK(hipEventRecord(h->text_ev, st_text));
       if (after & 2) HIPCHK(hipStreamWaitEvent(st_eff, h->text_ev, 0));
       if (after & 4) HIPCHK(hipStreamWaitEvent(st_ctxt, h->text_ev, 0));
       if (after & 8) HIPCHK(hipStreamWaitEvent(s, h->text_ev, 0));
     }
-    if (!(skip & 4) && !pair) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
+    if (!(skip & 4)) CHK(run_clip_text(h, clip_ids, clip_mask, B, Lc, w.t_emb, st_ctxt));
     if (!(skip & 2)) CHK(run_effnet(h, img_eff, nullptr, B, nullptr, scores5 + 2, 5, st_eff));
-    if (pair) CHK(run_clip_pair(h, img_clip, clip_ids, clip_mask, B, Lc, w.v_emb, w.t_emb, s));
-    else if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
+    if (!(skip & 8)) CHK(run_clip_image(h, img_clip, B, w.v_emb, s));
   }
   if (concurrent) {
     for (int i = 0; i < 3; ++i) {

@@ -990,11 +990,11 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
 #define MMF_EDW_SPLIT_BELOW 8192  // fused fronts with fewer (tile, image) blocks split their channel groups (0: never; B = 512: 3.502 -> 3.475 ms)
 #endif
 
-// Cin <= 64 (stages 2 - 4.1, KS <= 2), and 3 x 3 blocks of Cin <= min(max_cin, 96) (stages 4.2 / 4.3:
-// Cin 80, KS = 3; their two launches 28 + 33 -> 45 us per 256 images).  The 5 x 5 blocks of Cin 80 / 112
-// (stages 5.1 - 6.1, KS = 3 / 4) measured a tie or slower fused (230-256 VGPRs: two waves per SIMD).
-bool expand_dw_applicable(int cin, int cexp, int k, int max_cin) {
-  const bool ok_cin = cin <= 64 || (k == 3 && cin <= max_cin && cin <= 96);
+// Cin <= 64 (stages 2 - 4.1, KS <= 2), and 3 x 3 blocks of Cin <= 96 (stages 4.2 / 4.3: Cin 80, KS = 3;
+// their two launches 28 + 33 -> 45 us per 256 images).  The 5 x 5 blocks of Cin 80 / 112 (stages 5.1 -
+// 6.1, KS = 3 / 4) measured a tie or slower fused (230-256 VGPRs: two waves per SIMD).
+bool expand_dw_applicable(int cin, int cexp, int k) {
+  const bool ok_cin = cin <= 64 || (k == 3 && cin <= 96);
   return ok_cin && (cin % 8) == 0 && (cexp % 48) == 0;
 }
 
@@ -1003,7 +1003,7 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
                             int stride, int* nchunks_out, hipStream_t s, int ct) {
   int T, CW, tiles_x, ntiles;
   dw_geometry(H, W, C, stride, &T, &CW, &tiles_x, &ntiles);
-  if (!expand_dw_applicable(cin, C, k, 96) || CW != 48) return hipErrorInvalidValue;
+  if (!expand_dw_applicable(cin, C, k) || CW != 48) return hipErrorInvalidValue;
   *nchunks_out = ntiles;
   const int IT = (T - 1) * stride + k, PX = 256 / (CW / 8), KS = (cin + 31) / 32;
   if (IT > 19) return hipErrorInvalidValue;  // the kernel's MAXRF prefetch depth

@@ -511,37 +511,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g
 #undef MMF_GLDS_FIRST_TILE
 }
 
-// One problem of a grouped launch: its tiles follow `skip` tiles of the previous problem in the global
-// order wgid, wgid + nwg, ... (gemm_glds_group_kernel).  The LDS arrays are function-scope __shared__
-// variables of this function, so both passes of the grouped kernel share one allocation.
-template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2, int EPI>
-MMF_DEV void glds_run(GemmArgs g, int tilesN, int tiles, int tilesM, int gm, int skip) {
-  constexpr int DBG = 0;
-#define MMF_GLDS_FIRST_TILE (wgid >= skip ? wgid - skip : wgid + (skip - wgid + nwg - 1) / nwg * nwg - skip)
-#include "gemm_glds_body.inc"
-#undef MMF_GLDS_FIRST_TILE
-}
-
-// Grouped launch (option clip_group; the ViT and CLIP-text GEMMs of one layer, which share a tile
-// instantiation): one persistent grid over problem 0's tiles, then problem 1's, in one global order
-// t = 0 .. tiles0 + tiles1 - 1 (workgroup w takes w, w + nwg, ...), so the two sub-round launches of
-// the separate towers (ViT 200 + text 231 producer tiles on 256 CUs) pack into one.  Problem 0 is the
-// one with the longer K (longest tiles first).  Each tile is computed exactly as in its own launch.
-struct GemmPair {
-  GemmArgs g[2];
-  int tilesN[2], tiles[2], tilesM[2];
-};
-template <int BM, int BN, int WGM, int WGN, int ACT, int EPI>
-__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_group_kernel(GemmPair pr) {
-  // one copy of the tile loop (two inlined copies spill 50-90 VGPRs at 256x256): the problem's
-  // arguments are read per pass
-#pragma unroll 1
-  for (int p = 0; p < 2; ++p) {
-    if (p) __syncthreads();  // (the next problem's prologue refills the stages)
-    glds_run<BM, BN, WGM, WGN, ACT, true, EPI>(pr.g[p], pr.tilesN[p], pr.tiles[p], pr.tilesM[p], 0, p ? pr.tiles[0] : 0);
-  }
-}
-
 // persistent grid: one workgroup per CU (256 CUs), fewer when the launch has fewer tiles
 template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false, int DBG = 0>
 hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
@@ -601,27 +570,6 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   }
 #undef MMF_EPI_CASE
-  return hipGetLastError();
-}
-
-template <int BM, int BN, int WGM, int WGN>
-hipError_t run_glds_group(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
-  GemmPair pr;
-  pr.g[0] = a0;
-  pr.g[1] = a1;
-  for (int i = 0; i < 2; ++i) {
-    pr.tilesM[i] = (pr.g[i].M + BM - 1) / BM;
-    pr.tilesN[i] = (pr.g[i].N + BN - 1) / BN;
-    pr.tiles[i] = pr.tilesM[i] * pr.tilesN[i];
-  }
-  const int tiles = pr.tiles[0] + pr.tiles[1];
-  const dim3 grid(tiles < 256 ? tiles : 256), blk(64 * WGM * WGN);
-#define MMF_GRP_CASE(EPI, ACT) hipLaunchKernelGGL((gemm_glds_group_kernel<BM, BN, WGM, WGN, ACT, EPI>), grid, blk, 0, s, pr)
-  if (a0.epi == 1 && a0.act == ACT_NONE) MMF_GRP_CASE(1, ACT_NONE);
-  else if (a0.epi == 1 && a0.act == ACT_QUICK_GELU) MMF_GRP_CASE(1, ACT_QUICK_GELU);
-  else if (a0.epi == 2 && a0.act == ACT_NONE && BN == 192) MMF_GRP_CASE(2, ACT_NONE);
-  else return hipErrorNotSupported;
-#undef MMF_GRP_CASE
   return hipGetLastError();
 }
 
@@ -798,25 +746,6 @@ const char* gemm_config_name(int c) {
       "gemm_glds_pipe2<256,256,2,4>", "(removed)", "(removed)", "(removed)", "gemm_glds_dma_only",
       "gemm_glds_compute_only"};
   return (c >= 0 && c < kGemmConfigs) ? names[c] : "gemm_f16<?>";
-}
-
-// two lazy-LN GEMMs of one tile instantiation in one persistent launch (gemm_glds_group_kernel); the
-// longer-K problem first.  hipErrorNotSupported when they differ in tile, epilogue or activation
-// (the caller then launches them apart).
-bool gemm_group_ok(const GemmArgs& a, const GemmArgs& b) {
-  if (a.epi == 0 || a.epi != b.epi || a.act != b.act || a.epi == 3) return false;
-  if (a.act != ACT_NONE && a.act != ACT_QUICK_GELU) return false;
-  if (a.epi == 2 && a.act != ACT_NONE) return false;
-  return gemm_config(a) == gemm_config(b);
-}
-
-hipError_t launch_gemm_group(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
-  if (!gemm_group_ok(a, b)) return hipErrorNotSupported;
-  if (!epi_ok(a) || !epi_ok(b)) return hipErrorInvalidValue;
-  const int ca = gemm_config(a);
-  const GemmArgs& a0 = a.K >= b.K ? a : b;
-  const GemmArgs& a1 = a.K >= b.K ? b : a;
-  return ca == 11 ? run_glds_group<256, 256, 2, 4>(a0, a1, s) : run_glds_group<256, 192, 4, 2>(a0, a1, s);
 }
 
 #ifdef MMF_GEMM_STAMP

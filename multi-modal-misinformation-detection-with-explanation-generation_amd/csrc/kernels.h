@@ -47,11 +47,6 @@ int gemm_ln_tn(const GemmArgs& a);
 // results stay batch-invariant; 1 = no split.  Workspace need: splitk_factor * M * N floats.
 int gemm_splitk_factor(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
-// two lazy-LN GEMMs (epi 1 or 2) of the same tile instantiation as ONE persistent launch
-// (option clip_group: the ViT and CLIP-text GEMMs of a layer); hipErrorNotSupported if they differ
-// two lazy-LN GEMMs (same tile, epilogue and activation: gemm_group_ok) as one persistent launch
-bool gemm_group_ok(const GemmArgs& a, const GemmArgs& b);
-hipError_t launch_gemm_group(const GemmArgs& a, const GemmArgs& b, hipStream_t s);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks
 constexpr int kGemmConfigs = 17;  // numbering of the tile instantiations (0 .. 16; gemm.hip config_exists)
 const char* gemm_config_name(int c);
@@ -164,7 +159,7 @@ hipError_t launch_gap_classifier(const f16_t* x, int HW, int C, const float* w, 
 hipError_t launch_fill_strided(float* p, int stride, int B, float v, hipStream_t s);
 // fused MBConv front: expand 1x1 (we fp16 [C][cin], be fp32, BN folded) + SiLU computed per input
 // tile into LDS, then the depthwise conv of launch_dwconv (same outputs, same pool partials)
-bool expand_dw_applicable(int cin, int cexp, int k, int max_cin);
+bool expand_dw_applicable(int cin, int cexp, int k);
 hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const float* be, const float* w,
                             const float* bias, f16_t* out, float* pool_part, int B, int H, int W, int C, int k,
                             int stride, int* nchunks_out, hipStream_t s, int ct = 1);

@@ -455,44 +455,12 @@ def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
         engine.set_option("mt_enqueue", mt)
 
 
-@pytest.mark.parametrize("B", [37, 256])
-def test_clip_group_bit_identical(engine, B):
-    """Option clip_group (round 5): both CLIP towers layer-locked on one stream,
-    each layer's ViT and CLIP-text GEMMs of a kind as one grouped persistent launch
-    (gemm_glds_group_kernel).  Every tile is computed as in its own launch, so the embeddings, the
-    consistency scores and all of analyze_batch's outputs are bit-identical to the two-stream path;
-    ragged captions exercise the causal masks.  B = 256 is BASELINE configs[3]."""
-    import mmf_amd.synthetic as syn
-    rid, rm = syn.roberta_ids(B, 128, 77, [128, 64, 9])
-    cid, cm = syn.clip_ids(B, 77, 77, [77, 33, 6, 50])
-    imgs = syn.images(B, 77)
-
-    def run():
-        out = {k: v.clone() for k, v in engine.analyze_batch(rid, rm, cid, cm, imgs).items()}
-        out.update({"cons_" + k: v.clone() for k, v in engine.clip_consistency(imgs, cid, cm).items()})
-        torch.cuda.synchronize()
-        return out
-    old = engine.get_option("clip_group")
-    try:
-        engine.set_option("clip_group", 0)
-        ref = run()
-        for grp in (1, 2):  # (2: the grouped consumers on 256x192 tiles)
-            engine.set_option("clip_group", grp)
-            for _ in range(2):
-                out = run()
-                for k, v in ref.items():
-                    assert torch.equal(v, out[k]), (grp, k)
-    finally:
-        engine.set_option("clip_group", old)
-
-
 @pytest.mark.parametrize("B", [100, 256])
 def test_tower_order_bit_identical(engine, B):
-    """Options after_text / after_layer (round 5): in the concurrent B > mt_enqueue step the chosen
-    towers' streams wait on an event of the RoBERTa stream (after its last layer, or before layer
-    after_layer).  Only the start order of independent towers changes, so every output of
-    analyze_batch is bit-identical to the fully concurrent step; ragged texts / captions and a
-    mid-tower event exercise the masks."""
+    """Option after_text (round 5): in the concurrent B > mt_enqueue step the chosen towers' streams
+    wait on an event the RoBERTa stream records after its last layer.  Only the start order of
+    independent towers changes, so every output of analyze_batch is bit-identical to the fully
+    concurrent step (and to concurrent = 0); ragged texts / captions exercise the masks."""
     import mmf_amd.synthetic as syn
     rid, rm = syn.roberta_ids(B, 128, 91, [128, 64, 9])
     cid, cm = syn.clip_ids(B, 77, 91, [77, 33, 6, 50])
@@ -502,20 +470,19 @@ def test_tower_order_bit_identical(engine, B):
         out = {k: v.clone() for k, v in engine.analyze_batch(rid, rm, cid, cm, imgs).items()}
         torch.cuda.synchronize()
         return out
-    names = ("after_text", "after_layer", "concurrent")
+    names = ("after_text", "concurrent")
     old = {n: engine.get_option(n) for n in names}
     try:
         engine.set_option("concurrent", 1)
         engine.set_option("after_text", 0)
-        engine.set_option("after_layer", 12)
         ref = run()
-        for at, al in ((12, 12), (14, 12), (12, 10), (2, 12), (4, 11)):
+        for conc, at in ((1, 12), (1, 14), (1, 2), (1, 4), (0, 12)):
+            engine.set_option("concurrent", conc)
             engine.set_option("after_text", at)
-            engine.set_option("after_layer", al)
             for _ in range(2):
                 out = run()
                 for k, v in ref.items():
-                    assert torch.equal(v, out[k]), (at, al, k)
+                    assert torch.equal(v, out[k]), (conc, at, k)
     finally:
         for n, v in old.items():
             engine.set_option(n, v)

@@ -64,10 +64,6 @@ def main():
         if "clip" in what:
             eng.set_option("concurrent", 1)
             add("clip_concurrent_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
-            for grp in (1, 2):
-                eng.set_option("clip_group", grp)
-                add(f"clip_grouped{grp}_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
-            eng.set_option("clip_group", 0)
             eng.set_option("concurrent", 0)
             add("clip_serial_ms", timed(lambda: eng.clip_consistency(img, cid, cm, out=cons), a.steps))
             eng.set_option("concurrent", 1)
@@ -75,10 +71,7 @@ def main():
             add("clip_text_alone_ms", timed(lambda: eng.clip_text(cid, cm), a.steps))
         if "step" in what:
             ab_out = eng.alloc_outputs(B)
-            for grp in (0, 1, 2):
-                eng.set_option("clip_group", grp)
-                add(f"analyze_b256_clip_group{grp}_ms", timed(lambda: eng.analyze_batch(rid, rm, cid, cm, img, out=ab_out), a.steps))
-            eng.set_option("clip_group", 0)
+            add("analyze_b256_ms", timed(lambda: eng.analyze_batch(rid, rm, cid, cm, img, out=ab_out), a.steps))
         if "text" in what:
             for mode in (0, 1, 2):
                 eng.set_option("text_hilo", mode)
