@@ -954,11 +954,17 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
   return 0;
 }
 
+// heads_ev: recorded once the encoder is done, before the heads (mmf_analyze_batch's after_text event:
+// the waiting towers start while the two small head MLPs run)
 int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int L, float* ai, float* mi,
-             float* scores, int score_stride, hipStream_t s) {
+             float* scores, int score_stride, hipStream_t s, hipEvent_t heads_ev = nullptr) {
   Workspace& w = h->ws;
   const int hilo = text_mode(h);
-  if (hilo >= 2) return run_text_precise(h, ids, mask, B, L, ai, mi, scores, score_stride, s);
+  if (hilo >= 2) {
+    CHK(run_text_precise(h, ids, mask, B, L, ai, mi, scores, score_stride, s));
+    if (heads_ev) HIPCHK(hipEventRecord(heads_ev, s));
+    return 0;
+  }
   uint16_t* rlo = hilo ? w.r_lo : nullptr;
   const int M = B * L;
   {
@@ -1060,6 +1066,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
     CHK(lnorm(h, last ? w.r_x : w.r_y, 768, Ly.ln2, w.r_x, 768, w.r_xb, 768, Mr, 768, s));
   }
   // w.r_x now holds the B final CLS rows, compact
+  if (heads_ev) HIPCHK(hipEventRecord(heads_ev, s));
   ProfScope ps(h, s, PK_HEADS, 2.0 * B * 2 * (768 * 256 + 256 * 2), (double)B * 768 * 4 + 2 * 768 * 256 * 4);
   HIPCHK(launch_text_heads(w.r_x, 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,
                            h->h_b2m, ai, mi, scores, score_stride, B, s));
@@ -1971,9 +1978,8 @@ int mmf_analyze_batch(mmf_handle* h, const int32_t* rob_ids, const int32_t* rob_
     // (releasing them before RoBERTa's last layer or two, and EfficientNet chained behind a CLIP tower or
     // split over two streams, measured slower: DESIGN.md §1 round 5)
     const int after = concurrent && !(skip & 1) ? h->opt.after_text : 0;
-    if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text));
+    if (!(skip & 1)) CHK(run_text(h, rob_ids, rob_mask, B, Lr, nullptr, nullptr, scores5, 5, st_text, after ? h->text_ev : nullptr));
     if (after) {
-      HIPCHK(hipEventRecord(h->text_ev, st_text));
       if (after & 2) HIPCHK(hipStreamWaitEvent(st_eff, h->text_ev, 0));
       if (after & 4) HIPCHK(hipStreamWaitEvent(st_ctxt, h->text_ev, 0));
       if (after & 8) HIPCHK(hipStreamWaitEvent(s, h->text_ev, 0));

@@ -201,6 +201,71 @@ __global__ __launch_bounds__(256) void vault_sims_kernel(const float* q, const f
   }
 }
 
+// The same similarities on the fp32-input MFMA (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fmaf
+// chain, as effnet_f32.hip's pw32m): BIT-IDENTICAL to vault_sims_kernel (every output the chain over
+// k = 0 .. D-1 in order from 0) at the MFMA rate -- the launch sits on the step's serial tail.  Block
+// = 64 vault rows x 16 queries, wave w = vault rows 16 w .. 16 w + 15; K in 16-deep chunks staged
+// through LDS k-transposed ([row][g][s] = X[row][4 s + g]: a lane of group g reads its four steps'
+// operands k = g, 4 + g, 8 + g, 12 + g with one ds_read_b128; step s covers k = 4 s .. 4 s + 3 in
+// lane-group order), the next chunk's loads in flight under the current one's MFMAs.  Vault rows are
+// the MFMA's A operand, so each lane ends with 4 consecutive vault rows of one query: 16-B stores.
+__device__ __forceinline__ int vq_off(int row, int g) { return row * 16 + ((g ^ (((row >> 3) & 1) << 1)) << 2); }
+
+__global__ __launch_bounds__(256) void vault_sims_mfma_kernel(const float* __restrict__ q, const float* __restrict__ v,
+                                                              float* __restrict__ S, int B, int N, int D) {
+  __shared__ __attribute__((aligned(16))) float qs[2][16 * 16];
+  __shared__ __attribute__((aligned(16))) float vs[2][64 * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  const int n0 = blockIdx.x * 64, b0 = blockIdx.y * 16;
+  // loaders: V chunk 64 x 16 = one float4 per thread (row lr, k quad lc); Q chunk 16 x 16 = threads 0-63
+  const int lr = tid >> 2, lc = tid & 3;
+  const float* vp = v + (size_t)min(n0 + lr, N - 1) * D + lc * 4;  // clamped rows: loaded, never stored
+  const float* qp = q + (size_t)min(b0 + (lr & 15), B - 1) * D + lc * 4;
+  float4 rv, rq;
+  auto gload = [&](int k0) {
+    rv = *reinterpret_cast<const float4*>(vp + k0);
+    rq = *reinterpret_cast<const float4*>(qp + k0);
+  };
+  auto lstore = [&](int buf) {  // k = 4 lc + e -> [row][g = e][s = lc]
+    const float av[4] = {rv.x, rv.y, rv.z, rv.w}, bv[4] = {rq.x, rq.y, rq.z, rq.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) vs[buf][vq_off(lr, e) + lc] = av[e];
+    if (tid < 64) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qs[buf][vq_off(lr, e) + lc] = bv[e];
+    }
+  };
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nch = D / 16;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) gload((c + 1) * 16);
+    const float4 wf = *reinterpret_cast<const float4*>(&vs[buf][vq_off(wave * 16 + fr, fg)]);
+    const float4 xf = *reinterpret_cast<const float4*>(&qs[buf][vq_off(fr, fg)]);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.x, xf.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.y, xf.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.z, xf.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.w, xf.w, acc, 0, 0, 0);
+    if (c + 1 < nch) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // lane: S[query b0 + fr][vault rows n .. n + 3], n = n0 + 16 wave + 4 fg
+  const int b = b0 + fr, n = n0 + wave * 16 + fg * 4;
+  if (b < B) {
+    float* dst = S + (size_t)b * N + n;
+    if (n + 3 < N && ((N & 3) == 0)) {
+      *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < N) dst[r] = acc[r];
+    }
+  }
+}
+
 // Ranking of the reference's np.argsort(sims)[-k:][::-1] (misinfo_forensics.py:449): value
 // descending; numpy sorts NaN (a zero-norm vault row: 0/0 in the renormalisation, :443-445) after
 // every number, so the reversed tail puts NaN rows FIRST.  The scans rank by a key: the similarity,
@@ -359,7 +424,12 @@ hipError_t launch_rowdot(const float* a, const float* c, float* out, int ostride
 hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s) {
   if (D & 63) return hipErrorInvalidValue;
   if (B <= 0 || N <= 0) return hipSuccess;
+  // the fp32-MFMA kernel (bit-identical); a -DMMF_VAULT_VALU build keeps the VALU kernel (A/B builds)
+#ifdef MMF_VAULT_VALU
   hipLaunchKernelGGL(vault_sims_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
+#else
+  hipLaunchKernelGGL(vault_sims_mfma_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
+#endif
   return hipGetLastError();
 }
 
