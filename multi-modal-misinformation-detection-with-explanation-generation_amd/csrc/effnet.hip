@@ -211,7 +211,8 @@ MMF_DEV float fma_mix(uint32_t h2, float w, float acc) {
 // reuses the kernel row's weights for all R outputs (K reads instead of R*K).  Per output the
 // VALU work drops by ~30 % at K = 5, R = 7, and every tile offset is an immediate.
 // Items = NG * T * (T / R) over the first (256 / NG) * NG threads (each keeps its channel group).
-template <int K, int S, int T, int CW, int R>
+// PS: halfs per tile pixel (CW, or CW + a pad that spreads a wave's 16-B tap reads over more LDS banks).
+template <int K, int S, int T, int CW, int R, int PS = CW>
 MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, float* red, f16_t* __restrict__ out,
                            float* __restrict__ pool_part, int bi, int c0, int oy0, int ox0, int Ho, int Wo, int C,
                            int tix, int ntiles) {
@@ -219,6 +220,7 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
   constexpr int STRIDE = (256 / NG) * NG;  // active threads: a thread's channel group g never changes
   constexpr int NRED = STRIDE / NG;         // partial-sum slots per channel (<= the caller's red rows)
   static_assert(T % R == 0, "runs tile the row");
+  static_assert(PS >= CW && PS % 8 == 0, "16-B aligned pixels");
   const int tid = threadIdx.x;
   const int g = tid % NG;
   float psum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -242,10 +244,10 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
           wk[kx][0] = w0.x; wk[kx][1] = w0.y; wk[kx][2] = w0.z; wk[kx][3] = w0.w;
           wk[kx][4] = w1.x; wk[kx][5] = w1.y; wk[kx][6] = w1.z; wk[kx][7] = w1.w;
         }
-        const f16_t* row = tile + ((size_t)((oy * S + ky) * IT + ox * S) * NG + g) * 8;
+        const f16_t* row = tile + (size_t)((oy * S + ky) * IT + ox * S) * PS + g * 8;
 #pragma unroll
         for (int col = 0; col < IC; ++col) {
-          const uint4 v = *reinterpret_cast<const uint4*>(row + col * NG * 8);
+          const uint4 v = *reinterpret_cast<const uint4*>(row + col * PS);
           if constexpr (MMF_DW_MIX) {
             const uint32_t hv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -304,8 +306,8 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
 
 // LDS bytes of the input tile region.  Compile-time-geometry kernels (dw_compute_ct) reuse it for
 // the pool-partial slots `red` once the taps are done (fewer LDS bytes -> one more block per CU).
-MMF_DEV_HOST_INLINE int dw_tile_bytes(int IT, int CW, bool alias_red) {
-  const int t = IT * IT * CW * 2, r = (256 / (CW / 8)) * CW * 4;
+MMF_DEV_HOST_INLINE int dw_tile_bytes(int IT, int CW, bool alias_red, int PS = 0) {
+  const int t = IT * IT * (PS ? PS : CW) * 2, r = (256 / (CW / 8)) * CW * 4;
   return ((alias_red && r > t ? r : t) + 15) & ~15;
 }
 
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
 #ifndef MMF_EDW_PF
 #define MMF_EDW_PF 1
 #endif
-template <int K, int S, int KS, int TT, int R>
+template <int K, int S, int KS, int TT, int R, int TPAD>
 #ifndef MMF_EDW_MINB1
 #define MMF_EDW_MINB1 4  // resident blocks per CU hipcc budgets registers for (KS = 1: stage 3.1 148 -> 128 VGPRs, 4 blocks/CU; -0.9 %)
 #endif
@@ -420,6 +422,7 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
   extern __shared__ __attribute__((aligned(16))) unsigned char dw_smem[];
   constexpr int PAD = (K - 1) / 2, KP = KS * 32;
   constexpr int CW = 48, NF = CW / 16;  // the host launches 48-channel groups only
+  constexpr int PS = CW + (TT ? TPAD : 0);  // halfs per tile pixel (the runtime-geometry dw_compute: CW)
   constexpr int NRF_CT = TT ? ((((TT - 1) * S + K) * ((TT - 1) * S + K)) + 15) / 16 : 0;
   const int T = TT ? TT : T_;
   const int NG = CW / 8, IT = (T - 1) * S + K;
@@ -429,10 +432,10 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
   const int ty0 = blockIdx.x / tiles_x, tx0 = blockIdx.x - ty0 * tiles_x;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   const int oy0 = ty0 * T, ox0 = tx0 * T;
-  f16_t* tile = (f16_t*)dw_smem;                                 // [IT][IT][CW]
-  float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, TT > 0));  // [K*K][CW]
-  float* sb = sw + K * K * CW;                                     // [CW]
-  float* red = TT > 0 ? (float*)dw_smem : sb + CW;                 // [PX][CW]
+  f16_t* tile = (f16_t*)dw_smem;                                     // [IT][IT][PS]
+  float* sw = (float*)(dw_smem + dw_tile_bytes(IT, CW, TT > 0, PS));  // [K*K][CW]
+  float* sb = sw + K * K * CW;                                         // [CW]
+  float* red = TT > 0 ? (float*)dw_smem : sb + CW;                     // [PX][CW]
   float* sbe = TT > 0 ? sb + CW : red + (256 / NG) * CW;           // [CW] expand bias
   f16_t* swe = (f16_t*)(sbe + CW);                        // [CW][KP] expand weights (zero-padded K)
 
@@ -535,7 +538,7 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
 #pragma unroll
             for (int r = 0; r < 4; ++r) e[r] = inimg ? e[r] : 0.f;
             if (pix < npix)
-              *reinterpret_cast<uint2*>(tile + (size_t)pix * CW + nf * 16 + fg * 4) =
+              *reinterpret_cast<uint2*>(tile + (size_t)pix * PS + nf * 16 + fg * 4) =
                   make_uint2(pack2h(e[0], e[1]), pack2h(e[2], e[3]));
           }
         }
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
     __syncthreads();
     EST()
     if constexpr (TT > 0)
-      dw_compute_ct<K, S, TT, CW, R>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, blockIdx.x, gridDim.x);
+      dw_compute_ct<K, S, TT, CW, R, PS>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, blockIdx.x, gridDim.x);
     else dw_compute<K, S>(tile, sw, sb, red, out, pool_part, bi, c0, oy0, ox0, Ho, Wo, C, CW, T, IT);
     EST()
     __syncthreads();  // the next group restages sw / sb / swe / tile and rewrites red
@@ -563,6 +566,10 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
 //  accumulation) so the conv keeps ~20 mantissa bits, well under the fp16 rounding of its output.
 // grid (49, 1, B); block 256
 constexpr int SD_T = 16, SD_IT = 18, SD_PR = 2 * SD_IT + 1, SD_PW = SD_PR * 3;
+#ifndef MMF_SD_PAD
+#define MMF_SD_PAD 0  // halfs of pad per stem-tile pixel; 16 halves the tap reads' LDS cycles but costs a block per CU: +0.4 % tower
+#endif
+constexpr int SD_PS = 32 + MMF_SD_PAD;
 
 template <bool F32>
 __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const float* __restrict__ ws,
@@ -571,7 +578,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
                                                       float* __restrict__ pool_part) {
   constexpr int CW = 32, NPIX = SD_IT * SD_IT, NMT = (NPIX + 15) / 16;
   __shared__ __attribute__((aligned(16))) float patch[(SD_PR * SD_PW + 255) / 256 * 256];  // image patch, HWC
-  __shared__ __attribute__((aligned(16))) f16_t tile[NPIX * CW];  // stem tile (+halo)
+  __shared__ __attribute__((aligned(16))) f16_t tile[NPIX * SD_PS];  // stem tile (+halo), SD_PS halfs per pixel
   __shared__ __attribute__((aligned(16))) float sw[9 * CW];
   __shared__ __attribute__((aligned(16))) float sb[CW];
   float* red = patch;  // pool-partial slots [64][32]: the patch is dead once the stem tile is built
@@ -682,14 +689,14 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
       float e4[4] = {acc[0] + sbias[nt].x, acc[1] + sbias[nt].y, acc[2] + sbias[nt].z, acc[3] + sbias[nt].w};
       act4<ACT_SILU>(e4);
       const int ch = nt * 16 + fg * 4;
-      f16_t* dst = tile + p * CW + ch;
+      f16_t* dst = tile + p * SD_PS + ch;
       if (p < NPIX)
         *reinterpret_cast<uint2*>(dst) = inimg ? make_uint2(pack2h(e4[0], e4[1]), pack2h(e4[2], e4[3])) : make_uint2(0, 0);
     }
   }
   __syncthreads();
   EST()
-  dw_compute_ct<3, 1, SD_T, CW, 4>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW, blockIdx.x, 49);
+  dw_compute_ct<3, 1, SD_T, CW, 4, SD_PS>(tile, sw, sb, red, out, pool_part, bi, 0, oy0, ox0, 112, 112, CW, blockIdx.x, 49);
   EST()
   EST_END()
 }
@@ -986,6 +993,12 @@ hipError_t launch_dwconv(const f16_t* in, const float* w, const float* bias, f16
   return hipErrorInvalidValue;
 }
 
+#ifndef MMF_EDW_PAD
+#define MMF_EDW_PAD 8
+#endif
+#ifndef MMF_EDW_PAD52
+#define MMF_EDW_PAD52 MMF_EDW_PAD  // stage 3.1 (5 x 5, stride 2; 40.6 KB per block at pad 8: still 4 per CU)
+#endif
 #ifndef MMF_EDW_SPLIT_BELOW
 #define MMF_EDW_SPLIT_BELOW 8192  // fused fronts with fewer (tile, image) blocks split their channel groups (0: never; B = 512: 3.502 -> 3.475 ms)
 #endif
@@ -1009,7 +1022,9 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
   if (IT > 19) return hipErrorInvalidValue;  // the kernel's MAXRF prefetch depth
   const size_t smem =
       (size_t)dw_tile_bytes(IT, CW, false) + (size_t)(k * k * CW + CW + PX * CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
-  const size_t smem_ct = (size_t)dw_tile_bytes(IT, CW, true) + (size_t)(k * k * CW + CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
+  auto smem_ct = [&](int pad) {
+    return (size_t)dw_tile_bytes(IT, CW, true, CW + pad) + (size_t)(k * k * CW + CW + CW) * 4 + (size_t)CW * KS * 32 * 2;
+  };
   // launches with few tiles (the 28^2 / 14^2 stages) split their channel groups over blocks: one
   // block per (tile, group) instead of a block walking every group, so the chip fills (each block
   // re-reads its Cin-channel input tile from L2; every output and pool partial is computed as before)
@@ -1018,24 +1033,25 @@ hipError_t launch_expand_dw(const f16_t* x, int cin, const f16_t* we, const floa
   const int split = blocks < MMF_EDW_SPLIT_BELOW ? groups : 1;
   const int gpb = (groups + split - 1) / split;
   const dim3 grid(ntiles, (groups + gpb - 1) / gpb, B), blk(256);
-#define MMF_EDWCT(KK, SS, QS, TT, RR)                                                                       \
-  if (k == KK && stride == SS && KS == QS && T == TT) {                                                       \
-    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, TT, RR>), grid, blk, smem_ct, s, x, cin, we, be, w, bias, out, \
-                       pool_part, H, W, C, CW, T, tiles_x, gpb);                                              \
-    return hipGetLastError();                                                                                 \
+#define MMF_EDWCT(KK, SS, QS, TT, RR, PP)                                                                    \
+  if (k == KK && stride == SS && KS == QS && T == TT) {                                                        \
+    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, TT, RR, PP>), grid, blk, smem_ct(PP), s, x, cin, we, be, w, bias, \
+                       out, pool_part, H, W, C, CW, T, tiles_x, gpb);                                          \
+    return hipGetLastError();                                                                                  \
   }
+  // PP: tile-pixel pad in halfs (tools/dw_bank_model.py: 112-B pixels cut the tap reads' LDS cycles 10-21 %)
   if (ct) {
-    MMF_EDWCT(3, 2, 1, 8, MMF_R_E21)
-    MMF_EDWCT(3, 1, 1, 14, MMF_R_E22)
-    MMF_EDWCT(5, 1, 2, 14, MMF_R_E32)
-    MMF_EDWCT(5, 2, 1, 7, MMF_R_E31)
-    MMF_EDWCT(3, 2, 2, 7, MMF_R_E41)
-    MMF_EDWCT(3, 1, 3, 14, MMF_R_D14)  // stages 4.2 / 4.3 (Cin 80)
+    MMF_EDWCT(3, 2, 1, 8, MMF_R_E21, MMF_EDW_PAD)
+    MMF_EDWCT(3, 1, 1, 14, MMF_R_E22, MMF_EDW_PAD)
+    MMF_EDWCT(5, 1, 2, 14, MMF_R_E32, MMF_EDW_PAD)
+    MMF_EDWCT(5, 2, 1, 7, MMF_R_E31, MMF_EDW_PAD52)
+    MMF_EDWCT(3, 2, 2, 7, MMF_R_E41, MMF_EDW_PAD)
+    MMF_EDWCT(3, 1, 3, 14, MMF_R_D14, MMF_EDW_PAD)  // stages 4.2 / 4.3 (Cin 80)
   }
 #undef MMF_EDWCT
 #define MMF_EDW(KK, SS, QS)                                                                                      \
   if (k == KK && stride == SS && KS == QS) {                                                                     \
-    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, 0, 1>), grid, blk, smem, s, x, cin, we, be, w, bias, out,    \
+    hipLaunchKernelGGL((expand_dw_kernel<KK, SS, QS, 0, 1, 0>), grid, blk, smem, s, x, cin, we, be, w, bias, out,    \
                        pool_part, H, W, C, CW, T, tiles_x, gpb);                                                 \
     return hipGetLastError();                                                                                    \
   }
