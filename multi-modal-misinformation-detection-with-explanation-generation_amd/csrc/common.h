@@ -90,20 +90,32 @@ MMF_DEV f32x2_t gelu_erf2(f32x2_t x) {
   return (f32x2_t){fmaf(-ax.x, pe.x, fmaxf(x.x, 0.0f)), fmaf(-ax.y, pe.y, fmaxf(x.y, 0.0f))};
 }
 // x * sigmoid(k x) for a pair (SiLU k = 1, quick-GELU k = 1.702)
+// PKX: exp(a) evaluated exactly as hipcc lowers __expf -- v_exp_f32(a * 0x3fb8aa3b) -- with the
+// log2(e) scale as one packed multiply for the pair instead of two scalar ones (bit-identical; the
+// EfficientNet fronts / depthwise convs are VALU-bound on their SiLU: tower -1 %.  The GEMM epilogues
+// keep the scalar form: the packed one measured +0.6 % on the step)
+template <bool PKX = false>
 MMF_DEV f32x2_t xsigmoid2(f32x2_t x, float k) {
   const f32x2_t a = x * -k;
-  const f32x2_t d = (f32x2_t){__expf(a.x), __expf(a.y)} + 1.0f;
+  f32x2_t e;
+  if constexpr (PKX) {
+    const f32x2_t t = a * 1.44269502f;
+    e = (f32x2_t){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  } else {
+    e = (f32x2_t){__expf(a.x), __expf(a.y)};
+  }
+  const f32x2_t d = e + 1.0f;
   return x * (f32x2_t){fast_rcp(d.x), fast_rcp(d.y)};
 }
 // activation of 4 consecutive accumulator values (compile-time ACT), packed where it pays
-template <int ACT>
+template <int ACT, bool PKX = false>
 MMF_DEV void act4(float* v) {
 #pragma unroll
   for (int h = 0; h < 4; h += 2) {
     f32x2_t x = {v[h], v[h + 1]};
     if constexpr (ACT == ACT_GELU) x = gelu_erf2(x);
     else if constexpr (ACT == ACT_QUICK_GELU) x = xsigmoid2(x, 1.702f);
-    else if constexpr (ACT == ACT_SILU) x = xsigmoid2(x, 1.0f);
+    else if constexpr (ACT == ACT_SILU) x = xsigmoid2<PKX>(x, 1.0f);
     else if constexpr (ACT == ACT_RELU) x = (f32x2_t){fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f)};
     v[h] = x.x;
     v[h + 1] = x.y;

@@ -278,8 +278,8 @@ MMF_DEV void dw_compute_ct(const f16_t* tile, const float* sw, const float* sb, 
 #pragma unroll
       for (int o = 0; o < R; ++o) {
         if (ox0 + ox + o < Wo) {
-          act4<ACT_SILU>(acc[o]);
-          act4<ACT_SILU>(acc[o] + 4);
+          act4<ACT_SILU, true>(acc[o]);
+          act4<ACT_SILU, true>(acc[o] + 4);
 #pragma unroll
           for (int j = 0; j < 8; ++j) psum[j] += acc[o][j];
           *reinterpret_cast<uint4*>(at_bytes(out + (size_t)bi * Ho * Wo * C,
@@ -534,12 +534,11 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
 #pragma unroll
           for (int nf = 0; nf < NF; ++nf) {
             float e[4] = {acc[nf][0] + bev[nf].x, acc[nf][1] + bev[nf].y, acc[nf][2] + bev[nf].z, acc[nf][3] + bev[nf].w};
-            act4<ACT_SILU>(e);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) e[r] = inimg ? e[r] : 0.f;
-            if (pix < npix)
-              *reinterpret_cast<uint2*>(tile + (size_t)pix * PS + nf * 16 + fg * 4) =
-                  make_uint2(pack2h(e[0], e[1]), pack2h(e[2], e[3]));
+            act4<ACT_SILU, true>(e);
+            // zero padding masked on the packed halves (2 ANDs instead of 4 selects; fp16 +0 either way)
+            const uint32_t keep = 0u - (uint32_t)inimg;
+            const uint2 hv = make_uint2(pack2h(e[0], e[1]) & keep, pack2h(e[2], e[3]) & keep);
+            if (pix < npix) *reinterpret_cast<uint2*>(tile + (size_t)pix * PS + nf * 16 + fg * 4) = hv;
           }
         }
       }
@@ -687,7 +686,7 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
       acc = mfma16x16x32(whi[nt], xlo, acc);
       acc = mfma16x16x32(whi[nt], xhi, acc);
       float e4[4] = {acc[0] + sbias[nt].x, acc[1] + sbias[nt].y, acc[2] + sbias[nt].z, acc[3] + sbias[nt].w};
-      act4<ACT_SILU>(e4);
+      act4<ACT_SILU, true>(e4);
       const int ch = nt * 16 + fg * 4;
       f16_t* dst = tile + p * SD_PS + ch;
       if (p < NPIX)
