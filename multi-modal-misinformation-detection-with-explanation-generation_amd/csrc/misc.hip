@@ -95,17 +95,17 @@ __global__ __launch_bounds__(256) void fusion_kernel(const float* x5, const floa
   __shared__ float sw0[64 * 5], sb0[64], sw3[32 * 65], sb3[32], sw5[64], sb5[2];
   __shared__ float hs[4][64], h2[4][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  const bool live = row < B;
+  float x[5];  // (issued before the weight staging: one load latency for both)
+#pragma unroll
+  for (int i = 0; i < 5; ++i) x[i] = live ? x5[(size_t)row * 5 + i] : 0.f;
   for (int i = tid; i < 320; i += 256) sw0[i] = w0[i];
   for (int i = tid; i < 2048; i += 256) sw3[(i >> 6) * 65 + (i & 63)] = w3[i];  // padded rows: no bank conflicts
   if (tid < 64) { sb0[tid] = b0[tid]; sw5[tid] = w5[tid]; }
   if (tid < 32) sb3[tid] = b3[tid];
   if (tid < 2) sb5[tid] = b5[tid];
   __syncthreads();
-  const int row = blockIdx.x * 4 + wave;
-  const bool live = row < B;
-  float x[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) x[i] = live ? x5[(size_t)row * 5 + i] : 0.f;
   {
     float a = sb0[lane];
 #pragma unroll
@@ -150,7 +150,18 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* a, const float
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
   float s = 0.f;
-  for (int i = lane; i < C; i += 64) s = fmaf(a[(size_t)row * C + i], c[(size_t)row * C + i], s);
+  for (int i0 = lane; i0 < C; i0 += 512) {  // 8 columns per lane in flight, then the ascending-i chain
+    float ta[8], tc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 64 * u;
+      ta[u] = i < C ? a[(size_t)row * C + i] : 0.f;
+      tc[u] = i < C ? c[(size_t)row * C + i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + 64 * u < C) s = fmaf(ta[u], tc[u], s);
+  }
   s = wave_sum(s);
   if (lane == 0) out[(size_t)row * ostride] = s;
 }
@@ -211,45 +222,57 @@ __global__ __launch_bounds__(256) void vault_sims_kernel(const float* q, const f
 // the MFMA's A operand, so each lane ends with 4 consecutive vault rows of one query: 16-B stores.
 __device__ __forceinline__ int vq_off(int row, int g) { return row * 16 + ((g ^ (((row >> 3) & 1) << 1)) << 2); }
 
+// CH 16-deep chunks per LDS stage (one barrier per 16 CH of K; D % (16 CH) == 0, host-checked): the
+// same chunk images and MFMA order as CH = 1, so the same ascending-k chains
+template <int CH>
 __global__ __launch_bounds__(256) void vault_sims_mfma_kernel(const float* __restrict__ q, const float* __restrict__ v,
                                                               float* __restrict__ S, int B, int N, int D) {
-  __shared__ __attribute__((aligned(16))) float qs[2][16 * 16];
-  __shared__ __attribute__((aligned(16))) float vs[2][64 * 16];
+  __shared__ __attribute__((aligned(16))) float qs[2][CH][16 * 16];
+  __shared__ __attribute__((aligned(16))) float vs[2][CH][64 * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 64, b0 = blockIdx.y * 16;
   // loaders: V chunk 64 x 16 = one float4 per thread (row lr, k quad lc); Q chunk 16 x 16 = threads 0-63
   const int lr = tid >> 2, lc = tid & 3;
   const float* vp = v + (size_t)min(n0 + lr, N - 1) * D + lc * 4;  // clamped rows: loaded, never stored
   const float* qp = q + (size_t)min(b0 + (lr & 15), B - 1) * D + lc * 4;
-  float4 rv, rq;
+  float4 rv[CH], rq[CH];
   auto gload = [&](int k0) {
-    rv = *reinterpret_cast<const float4*>(vp + k0);
-    rq = *reinterpret_cast<const float4*>(qp + k0);
+#pragma unroll
+    for (int h = 0; h < CH; ++h) {
+      rv[h] = *reinterpret_cast<const float4*>(vp + k0 + 16 * h);
+      rq[h] = *reinterpret_cast<const float4*>(qp + k0 + 16 * h);
+    }
   };
   auto lstore = [&](int buf) {  // k = 4 lc + e -> [row][g = e][s = lc]
-    const float av[4] = {rv.x, rv.y, rv.z, rv.w}, bv[4] = {rq.x, rq.y, rq.z, rq.w};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) vs[buf][vq_off(lr, e) + lc] = av[e];
-    if (tid < 64) {
+    for (int h = 0; h < CH; ++h) {
+      const float av[4] = {rv[h].x, rv[h].y, rv[h].z, rv[h].w}, bv[4] = {rq[h].x, rq[h].y, rq[h].z, rq[h].w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) qs[buf][vq_off(lr, e) + lc] = bv[e];
+      for (int e = 0; e < 4; ++e) vs[buf][h][vq_off(lr, e) + lc] = av[e];
+      if (tid < 64) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qs[buf][h][vq_off(lr, e) + lc] = bv[e];
+      }
     }
   };
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nch = D / 16;
+  const int nst = D / (16 * CH);
   gload(0);
   lstore(0);
   __syncthreads();
-  for (int c = 0; c < nch; ++c) {
+  for (int c = 0; c < nst; ++c) {
     const int buf = c & 1;
-    if (c + 1 < nch) gload((c + 1) * 16);
-    const float4 wf = *reinterpret_cast<const float4*>(&vs[buf][vq_off(wave * 16 + fr, fg)]);
-    const float4 xf = *reinterpret_cast<const float4*>(&qs[buf][vq_off(fr, fg)]);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.x, xf.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.y, xf.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.z, xf.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.w, xf.w, acc, 0, 0, 0);
-    if (c + 1 < nch) lstore(buf ^ 1);
+    if (c + 1 < nst) gload((c + 1) * 16 * CH);
+#pragma unroll
+    for (int h = 0; h < CH; ++h) {
+      const float4 wf = *reinterpret_cast<const float4*>(&vs[buf][h][vq_off(wave * 16 + fr, fg)]);
+      const float4 xf = *reinterpret_cast<const float4*>(&qs[buf][h][vq_off(fr, fg)]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.x, xf.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.y, xf.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.z, xf.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.w, xf.w, acc, 0, 0, 0);
+    }
+    if (c + 1 < nst) lstore(buf ^ 1);
     __syncthreads();
   }
   // lane: S[query b0 + fr][vault rows n .. n + 3], n = n0 + 16 wave + 4 fg
@@ -277,28 +300,33 @@ MMF_DEV float rank_key(float v) { return v != v ? INFINITY : v; }
 MMF_DEV float unkey(float k) { return k == INFINITY ? NAN : k; }
 MMF_DEV bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia > ib); }
 
+// One 256-thread block per query row: each wave keeps per-lane top-K lists over its share of the
+// columns (columns w * 64 + lane + 256 i, 8 loads in flight per lane), reduces them to the wave's
+// top-K, and wave 0 merges the four waves' 4K candidates.  `better` is a strict total order (value,
+// then index), so the K selected (value, index) pairs do not depend on how the columns were split.
 template <int K>
 __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, int N, float thresh, float* sims,
                                                          int32_t* idx, float* disc, int disc_stride,
                                                          const float* temb, const float* title, int D,
                                                          float* tsim) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= B) return;
+  static_assert(4 * K <= 64, "wave 0 holds the 4K candidates one per lane");
+  __shared__ float cv[4 * K];
+  __shared__ int ci[4 * K];
+  const int row = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (row >= B) return;  // (uniform per block)
   float tv[K];
   int ti[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) { tv[i] = -INFINITY; ti[i] = -1; }
   const float* s = S + (size_t)row * N;
-  // 8 loads in flight per lane, then the same ascending-j insertions (one round trip per 512
-  // columns instead of per 64: the scan was ~34 dependent L2 trips, ~26 us)
-  for (int j0 = lane; j0 < N; j0 += 512) {
+  for (int j0 = wave * 64 + lane; j0 < N; j0 += 256 * 8) {
     float vv[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) vv[u] = (j0 + 64 * u < N) ? rank_key(s[j0 + 64 * u]) : -INFINITY;
+    for (int u = 0; u < 8; ++u) vv[u] = (j0 + 256 * u < N) ? rank_key(s[j0 + 256 * u]) : -INFINITY;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const float v = vv[u];
-      const int vi = j0 + 64 * u;
+      const int vi = j0 + 256 * u;
       if (vi < N && better(v, vi, tv[K - 1], ti[K - 1])) {
         tv[K - 1] = v; ti[K - 1] = vi;
 #pragma unroll
@@ -311,8 +339,7 @@ __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, 
       }
     }
   }
-  float outv[K];
-  int outi[K];
+  // the wave's top K: K rounds of a wave arg-max over the lists' heads, the winning lane pops
 #pragma unroll
   for (int t = 0; t < K; ++t) {
     float bv = tv[0];
@@ -323,12 +350,32 @@ __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, 
       const int oi = __shfl_xor(bi, o, 64);
       if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
     }
-    outv[t] = bv; outi[t] = bi;
-    if (ti[0] == bi) {  // pop the head of the winning lane
+    if (lane == 0) { cv[wave * K + t] = bv; ci[wave * K + t] = bi; }
+    if (ti[0] == bi) {
 #pragma unroll
       for (int i = 0; i < K - 1; ++i) { tv[i] = tv[i + 1]; ti[i] = ti[i + 1]; }
       tv[K - 1] = -INFINITY; ti[K - 1] = -1;
     }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // merge: lane l < 4K holds candidate l
+  float mv = lane < 4 * K ? cv[lane] : -INFINITY;
+  int mi = lane < 4 * K ? ci[lane] : -1;
+  float outv[K];
+  int outi[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    float bv = mv;
+    int bi = mi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    outv[t] = bv; outi[t] = bi;
+    if (mi == bi) { mv = -INFINITY; mi = -1; }
   }
   const bool hit = outv[0] > thresh && outv[0] != INFINITY;  // NaN > thresh is false
   if (lane == 0) {
@@ -342,7 +389,19 @@ __global__ __launch_bounds__(256) void vault_topk_kernel(const float* S, int B, 
   if (tsim) {
     float d = 0.f;
     if (hit && temb && title) {
-      for (int c = lane; c < D; c += 64) d = fmaf(temb[(size_t)row * D + c], title[(size_t)outi[0] * D + c], d);
+      // 8 columns per lane in flight at once (D <= 512), then the same ascending-c fmaf chain
+      for (int c0 = lane; c0 < D; c0 += 512) {
+        float ta[8], tb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int c = c0 + 64 * u;
+          ta[u] = c < D ? temb[(size_t)row * D + c] : 0.f;
+          tb[u] = c < D ? title[(size_t)outi[0] * D + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (c0 + 64 * u < D) d = fmaf(ta[u], tb[u], d);
+      }
       d = wave_sum(d);
     }
     if (lane == 0) tsim[row] = d;
@@ -421,6 +480,9 @@ hipError_t launch_rowdot(const float* a, const float* c, float* out, int ostride
   return hipGetLastError();
 }
 
+#ifndef MMF_VAULT_CH
+#define MMF_VAULT_CH 4  // 16-deep K chunks per LDS stage / barrier
+#endif
 hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s) {
   if (D & 63) return hipErrorInvalidValue;
   if (B <= 0 || N <= 0) return hipSuccess;
@@ -428,7 +490,10 @@ hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, in
 #ifdef MMF_VAULT_VALU
   hipLaunchKernelGGL(vault_sims_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
 #else
-  hipLaunchKernelGGL(vault_sims_mfma_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
+  if ((D % (16 * MMF_VAULT_CH)) == 0)
+    hipLaunchKernelGGL(vault_sims_mfma_kernel<MMF_VAULT_CH>, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
+  else
+    hipLaunchKernelGGL(vault_sims_mfma_kernel<1>, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
 #endif
   return hipGetLastError();
 }
@@ -436,7 +501,7 @@ hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, in
 hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, float* sims, int32_t* idx,
                              float* disc, int disc_stride, const float* text_emb, const float* title_emb, int D,
                              float* text_sim, hipStream_t s) {
-  const dim3 grid((B + 3) / 4), blk(256);
+  const dim3 grid(B), blk(256);  // one block (four waves) per query row
 #define TOPK_CASE(KK)                                                                                          \
   case KK:                                                                                                     \
     hipLaunchKernelGGL(vault_topk_kernel<KK>, grid, blk, 0, s, S, B, N, thresh, sims, idx, disc, disc_stride, \
