@@ -353,26 +353,39 @@ __global__ __launch_bounds__(256) void attention_q1_kernel(const float* __restri
   }
   const int last = qpos ? qpos[bi] : L - 1;  // causal: keys <= the query position
   float m = -INFINITY;
-  for (int j = lane; j < L; j += 64) {
-    const bool valid = (!mask || mask[(size_t)bi * L + j] != 0) && j <= last;
-    float sdot = -INFINITY;
-    if (valid) {
-      const uint4* kp = reinterpret_cast<const uint4*>(qkv + ((size_t)bi * L + j) * ld + koff + h * 64);
-      float a = 0.f;
+  // two keys per lane per trip (j, j + 64): both K rows' loads in flight before either dot product
+  for (int j0 = lane; j0 < L; j0 += 128) {
+    uint4 kv[2][8];
+    bool valid[2];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint4 v = kp[c];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int t = 0; t < 2; ++t) {
+      const int j = j0 + 64 * t;
+      valid[t] = j < L && (!mask || mask[(size_t)bi * L + j] != 0) && j <= last;
+      const uint4* kp = reinterpret_cast<const uint4*>(qkv + ((size_t)bi * L + min(j, L - 1)) * ld + koff + h * 64);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a = fmaf(qf[c * 8 + e * 2], lo_h(w[e]), a);
-          a = fmaf(qf[c * 8 + e * 2 + 1], hi_h(w[e]), a);
-        }
-      }
-      sdot = a * 0.125f;  // 1 / sqrt(64)
+      for (int c = 0; c < 8; ++c) kv[t][c] = kp[c];
     }
-    ps[wave][j] = sdot;
-    m = fmaxf(m, sdot);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = j0 + 64 * t;
+      if (j >= L) break;
+      float sdot = -INFINITY;
+      if (valid[t]) {
+        float a = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const uint32_t w[4] = {kv[t][c].x, kv[t][c].y, kv[t][c].z, kv[t][c].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a = fmaf(qf[c * 8 + e * 2], lo_h(w[e]), a);
+            a = fmaf(qf[c * 8 + e * 2 + 1], hi_h(w[e]), a);
+          }
+        }
+        sdot = a * 0.125f;  // 1 / sqrt(64)
+      }
+      ps[wave][j] = sdot;
+      m = fmaxf(m, sdot);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
@@ -390,7 +403,16 @@ __global__ __launch_bounds__(256) void attention_q1_kernel(const float* __restri
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const f16_t* vp = qkv + (size_t)bi * L * ld + voff + h * 64 + lane;
   float o = 0.f;
-  for (int j = 0; j <= last && j < L; ++j) o = fmaf(ps[wave][j], h2f(vp[(size_t)j * ld]), o);
+  // keys in chunks of 32: the chunk's V loads all in flight, then the same ascending-j fmaf chain
+  const int jend = min(last + 1, L);
+  for (int jb = 0; jb < jend; jb += 32) {
+    f16_t vv[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) vv[u] = vp[(size_t)min(jb + u, jend - 1) * ld];
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (jb + u < jend) o = fmaf(ps[wave][jb + u], h2f(vv[u]), o);
+  }
   out[(size_t)bi * ldo + h * 64 + lane] = f2h(sum > 0.f ? o / sum : 0.f);
 }
 
