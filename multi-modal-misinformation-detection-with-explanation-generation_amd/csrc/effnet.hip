@@ -709,6 +709,9 @@ __global__ __launch_bounds__(256, 3) void stem_dw_kernel(const void* src, const 
 //   fc2  : scale[c] = sigmoid(b2[c] + sum_j w2t[j][c] s1[j])  (w2t = fc2 weight transposed at load,
 //          so consecutive threads read consecutive addresses)
 constexpr int SE_THREADS = 1024;
+#ifndef SE_FC1_U
+#define SE_FC1_U 8
+#endif
 
 template <bool PRECISE>
 __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, int nchunks, float inv_hw,
@@ -721,6 +724,18 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
   for (int c = tid; c < C; c += SE_THREADS) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int k = 0;
+    for (; k + 16 <= nchunks; k += 16) {  // 16 partials in flight (the 49- / 16-tile early stages)
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = pp[(size_t)(k + u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        a0 += v[u];
+        a1 += v[u + 1];
+        a2 += v[u + 2];
+        a3 += v[u + 3];
+      }
+    }
     for (; k + 4 <= nchunks; k += 4) {
       a0 += pp[(size_t)k * C + c];
       a1 += pp[(size_t)(k + 1) * C + c];
@@ -734,15 +749,17 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
   {
     constexpr int OPW = 4;  // outputs per wave (Csq <= 64 = 16 waves x 4)
     float acc[OPW] = {0.f, 0.f, 0.f, 0.f};
-    // the wave's outputs walk C together: per step 4 weights of every output in flight (16 loads, one
-    // L2 round trip per step for all outputs); each output's FMAs stay in ascending c (lane, lane + 64, ...)
-    for (int c = lane; c < C; c += 256) {
-      float wv[OPW][4];
+    // the wave's outputs walk C together: per step SE_FC1_U weights of every output in flight (4 x U
+    // loads, one L2 round trip per step for all outputs); each output's FMAs stay in ascending c
+    // (lane, lane + 64, ...).  U = 8: the C = 672 / 1152 blocks in 2 - 3 steps instead of 3 - 5
+    constexpr int U = SE_FC1_U;
+    for (int c = lane; c < C; c += 64 * U) {
+      float wv[OPW][U];
 #pragma unroll
       for (int t = 0; t < OPW; ++t) {
         const int o = wave + 16 * t;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int cc = c + 64 * u;
           wv[t][u] = (o < Csq && cc < C) ? w1[(size_t)o * C + cc] : 0.f;
         }
@@ -750,7 +767,7 @@ __global__ __launch_bounds__(SE_THREADS) void se_kernel(const float* pool_part, 
 #pragma unroll
       for (int t = 0; t < OPW; ++t)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < U; ++u)
           if (wave + 16 * t < Csq && c + 64 * u < C) acc[t] = fmaf(wv[t][u], pooled[c + 64 * u], acc[t]);
     }
 #pragma unroll
