@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restri
                                                         int ldo, int L, int H) {
   __shared__ __attribute__((aligned(16))) f16_t Ks[LK * 64];
   __shared__ __attribute__((aligned(16))) f16_t Vs[LK * 64];
-  __shared__ __attribute__((aligned(16))) float kbias[LK];
+  __shared__ __attribute__((aligned(16))) float kbias[256];  // (LK used; every thread stores its slot)
 
   const int bh = blockIdx.x, bi = bh / H, h = bh - bi * H;
   const int D = H * 64;
@@ -50,37 +50,38 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restri
   // (K, V and this wave's Q fragments for both of its query tiles) are issued before the first
   // LDS store so the whole workgroup has its 48 KB in flight at once.
   constexpr int NIT = LK * 8 / 256, NQT = LMAX / 64;
+  // Every load goes through buffer descriptors bounded at the sequence's L rows (and the mask's L
+  // words): rows past L read as 0 with no branch or select around a load, so hipcc places no vmcnt
+  // wait between them -- the workgroup pays one HBM round trip for K, V, Q and the mask together.
+  const rsrc_t rseq = make_rsrc(base, (uint32_t)L * (uint32_t)ld * 2u);
+  const rsrc_t rmask = make_rsrc(mask ? mask + (size_t)bi * L : nullptr, (uint32_t)L * 4u);
+  const uint32_t mraw = __builtin_amdgcn_raw_buffer_load_b32(rmask, (uint32_t)tid * 4u, 0, 0);
+  auto ld16 = [&](int row, int col) -> uint4 {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rseq, ((uint32_t)row * (uint32_t)ld + (uint32_t)col) * 2u, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  };
   uint4 kr[NIT], vr[NIT];
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
     const int c = tid + i * 256, key = c >> 3, kc = c & 7;
-    kr[i] = make_uint4(0, 0, 0, 0);
-    vr[i] = make_uint4(0, 0, 0, 0);
-    if (key < L) {
-      kr[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + D + h * 64 + kc * 8);
-      vr[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + 2 * D + h * 64 + kc * 8);
-    }
+    kr[i] = ld16(key, D + h * 64 + kc * 8);
+    vr[i] = ld16(key, 2 * D + h * 64 + kc * 8);
   }
   // Q fragments: row q = qt*16 + fr, dims 32*ks + 8*fg .. +7, for qt = wave + 4*it
   f16x8 qfa[NQT][2];
 #pragma unroll
-  for (int it = 0; it < NQT; ++it) {
-    const int q = (wave + 4 * it) * 16 + fr;
+  for (int it = 0; it < NQT; ++it)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (q < L) v = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + h * 64 + ks * 32 + fg * 8);
-      qfa[it][ks] = as_f16x8(v);
-    }
-  }
+    for (int ks = 0; ks < 2; ++ks) qfa[it][ks] = as_f16x8(ld16((wave + 4 * it) * 16 + fr, h * 64 + ks * 32 + fg * 8));
+  static_assert(LK <= 256, "one key-bias entry per thread");
+  const bool kvalid = tid < L && (!mask || mraw != 0);
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
     const int c = tid + i * 256, key = c >> 3, kc = c & 7;  // key < LK always
     *reinterpret_cast<uint4*>(Ks + kv_swz(key, kc)) = kr[i];
     *reinterpret_cast<uint4*>(Vs + kv_swz(key, kc)) = vr[i];
   }
-  for (int k = tid; k < LK; k += 256)
-    kbias[k] = (k < L && (!mask || mask[(size_t)bi * L + k])) ? 0.f : -INFINITY;
+  kbias[tid] = kvalid ? 0.f : -INFINITY;  // (no branch: the mask load stays with the others)
   __syncthreads();
 
   static_assert(NQT == 2, "two query tiles per wave");

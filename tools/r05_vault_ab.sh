@@ -15,5 +15,5 @@ for L in ${LIBS:-vhead new}; do
   if [ $L != new ]; then export MMF_HIP_LIB=$R/variants/$L/libmmf_hip.so; else unset MMF_HIP_LIB; fi
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/prof_$L -o run -- python3 $R/tools/step_ab.py "concurrent=1" --rounds 2 --iters 10 > $OUT/prof_$L.log 2>&1 || exit 1
   python3 $R/tools/rocprof_summary.py $OUT/prof_$L/run_results.db > $OUT/prof_$L.txt 2>&1 || true
-  echo "== $L"; grep -E "vault|rowdot|fusion_kernel|attention_q1|text_heads|TOTAL" $OUT/prof_$L.txt
+  echo "== $L"; grep -E "${GREP:-vault|rowdot|fusion_kernel|attention_q1|text_heads|TOTAL}" $OUT/prof_$L.txt
 done
