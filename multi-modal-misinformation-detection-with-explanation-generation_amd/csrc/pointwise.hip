@@ -18,6 +18,9 @@
 namespace {
 
 constexpr int PW_THREADS = 256;  // 4 waves
+#ifndef PW_SCALE_PRE
+#define PW_SCALE_PRE 1
+#endif
 
 // LDS image of W: [BN][KP] fp16, 16-B chunks XOR-swizzled per row so the 16-lane groups of the
 // fragment ds_read_b128 are conflict-free (brute-forced against the gfx950 lane groups).
@@ -79,6 +82,26 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
   }
   PW_LOAD_A(acur, rb)
   for (; rb < nrb; rb += gridDim.x) {
+    // SE excitation factors of this row block, loaded BEFORE the next block's A prefetch: the
+    // in-order vmcnt then lets them be consumed while the prefetch is still in flight (issued after
+    // it, every wait for them also waited for the prefetch)
+    // (only where the 8 RPW KS factor registers fit without spills or a lost wave: the narrow
+    // projects; the expands -- ACT_SILU -- never carry a scale)
+    constexpr bool PRE = PW_SCALE_PRE && ACT == ACT_NONE && CF <= 2 && RPW * KS <= 6;
+    float4 sc[PRE ? RPW * KS : 1][2];
+    if (PRE && has_scale) {
+#pragma unroll
+      for (int f = 0; f < RPW; ++f) {
+        const uint32_t bimg = min((uint32_t)rb * ROWS + (wave * RPW + f) * 16 + fr, (uint32_t)(M - 1)) / (uint32_t)g.rows_per_batch;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int k = s * 32 + fg * 8;
+          const uint32_t off = k < K ? (bimg * (uint32_t)K + k) * 4u : kOOB;
+          sc[PRE ? f * KS + s : 0][0] = buf_load_f4(rs, off);
+          sc[PRE ? f * KS + s : 0][1] = buf_load_f4(rs, off + 16u);
+        }
+      }
+    }
     if (rb + (int)gridDim.x < nrb) { PW_LOAD_A(anext, rb + (int)gridDim.x) }
 #pragma unroll
     for (int f = 0; f < RPW; ++f) {
@@ -89,7 +112,8 @@ __global__ __launch_bounds__(PW_THREADS, 4) void pw_kernel(GemmArgs g, int nrb) 
         for (int s = 0; s < KS; ++s) {
           const int k = s * 32 + fg * 8;
           const uint32_t off = k < K ? (bimg * (uint32_t)K + k) * 4u : kOOB;
-          const float4 s0 = buf_load_f4(rs, off), s1 = buf_load_f4(rs, off + 16u);
+          const float4 s0 = PRE ? sc[PRE ? f * KS + s : 0][0] : buf_load_f4(rs, off);
+          const float4 s1 = PRE ? sc[PRE ? f * KS + s : 0][1] : buf_load_f4(rs, off + 16u);
           u32x4& v = acur[f * KS + s];
           v.x = pack2h(lo_h(v.x) * s0.x, hi_h(v.x) * s0.y);
           v.y = pack2h(lo_h(v.y) * s0.z, hi_h(v.y) * s0.w);
