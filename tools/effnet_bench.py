@@ -20,11 +20,14 @@ def main():
     ap.add_argument("--ab", nargs="*", default=[], help="interleaved option variants 'opt=v[,opt2=v]'")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--opt", nargs="*", default=[], help="handle options set before the run 'opt=v'")
+    ap.add_argument("--pinned", action="store_true",
+                    help="fp16 towers pinned (no load-time calibration launches in a profile of the tower)")
     a = ap.parse_args()
     import mmf_amd.synthetic as syn
     import mmf_amd.weights as W
     from mmf_amd.engine import Engine
-    eng = Engine(0, W.synthetic_detector_state(0), None, max_batch=a.batch)
+    pin = dict(effnet_precision="fp16", text_precision="fp16") if a.pinned else {}
+    eng = Engine(0, W.synthetic_detector_state(0), None, max_batch=a.batch, **pin)
     for kv in a.opt:
         k, x = kv.split("=", 1)
         eng.set_option(k, int(x))
