@@ -729,11 +729,12 @@ class MisinfoForensics:
                     fut = ex.submit(host_stage, *chunks[k + 1])
                 self._fit_text(rid.shape[1])
                 eff, clp = self._windows(*rgb)
-                out = self.analyze_batch(rid, rm, cid, cm, eff, clp)
+                out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
                 # clip_similarity is the cosine of the two CLIP embeddings: non-finite only when a
-                # stream overflowed fp16 (a zero vault row's NaN stays in top_sims)
+                # stream overflowed fp16 (a zero vault row's NaN stays in top_sims); checked on the
+                # results already read back (no device launch: analyze() at B = 1 -0.2 ms)
                 if self.engine.clip_stream_overflow(out["scores"][:, 3]):
-                    out = self.analyze_batch(rid, rm, cid, cm, eff, clp)
+                    out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
                 res.extend(self.batch_to_dicts(out))
         return res
 
@@ -786,8 +787,14 @@ class MisinfoForensics:
         self.detector.sync()
         return self.engine.analyze_batch(rob_ids, rob_mask, clip_ids, clip_mask, images_u8, clip_images_u8, out=out)
 
-    def batch_to_dicts(self, out: Dict[str, torch.Tensor]) -> List[Dict]:
-        o = {k: v.cpu().numpy() for k, v in out.items()}
+    @staticmethod
+    def batch_to_host(out: Dict[str, torch.Tensor]) -> Dict[str, np.ndarray]:
+        return {k: v.cpu().numpy() for k, v in out.items()}
+
+    def batch_to_dicts(self, out: Dict) -> List[Dict]:
+        """The reference's result dicts from analyze_batch's outputs (device tensors or their
+        batch_to_host copies)."""
+        o = {k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in out.items()}
         res = []
         for b in range(o["scores"].shape[0]):
             s = o["scores"][b]

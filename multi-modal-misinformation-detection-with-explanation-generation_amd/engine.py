@@ -121,17 +121,22 @@ class Engine:
         self.clip_stream_check = {"max_dcos": dcos, "max_demb": demb, "fp16_streams": ok, "rows": n}
         return self.clip_stream_check
 
-    def clip_stream_overflow(self, *outputs: torch.Tensor) -> bool:
+    def clip_stream_overflow(self, *outputs) -> bool:
         """Run-time overflow trap of the fp16 CLIP streams: the load-time calibration
         measures 8 seeded inputs, so it bounds nothing for later ones.  An input that drives a
         stream past fp16's range turns the embedding non-finite, and clip_similarity / the vault
         scores with it.  The synchronous API paths (which read their results back anyway) pass
         their CLIP outputs here: if fp16 streams are selected and any value is non-finite, the
         engine switches to fp32 streams for good and returns True, and the caller re-runs the
-        batch.  Drift short of overflow is what the calibration alone covers."""
+        batch.  Drift short of overflow is what the calibration alone covers.  An output
+        may be a device tensor or a host array the caller already read back (checked on the host:
+        no device launch or extra synchronisation)."""
         if self.get_option("clip_res16") != 1:
             return False
-        if all(bool(torch.isfinite(v).all()) for v in outputs if v is not None):
+
+        def finite(v) -> bool:
+            return bool(np.isfinite(v).all()) if isinstance(v, np.ndarray) else bool(torch.isfinite(v).all())
+        if all(finite(v) for v in outputs if v is not None):
             return False
         self.set_option("clip_res16", 0)
         self.clip_stream_check = dict(self.clip_stream_check or {}, fp16_streams=False, runtime_overflow=True)
