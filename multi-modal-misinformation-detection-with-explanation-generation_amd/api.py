@@ -719,23 +719,31 @@ class MisinfoForensics:
             rgb = io_utils.decode_rgb([images[a + i] for i in rest]) if rest else []
             return rid, rm, cid, cm, (b - a, st, rest, rgb)
 
-        from concurrent.futures import ThreadPoolExecutor
         res: List[Dict] = []
+
+        def device_part(staged):
+            rid, rm, cid, cm, rgb = staged
+            self._fit_text(rid.shape[1])
+            eff, clp = self._windows(*rgb)
+            out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
+            # clip_similarity is the cosine of the two CLIP embeddings: non-finite only when a
+            # stream overflowed fp16 (a zero vault row's NaN stays in top_sims); checked on the
+            # results already read back (no device launch: analyze() at B = 1 -0.2 ms)
+            if self.engine.clip_stream_overflow(out["scores"][:, 3]):
+                out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
+            res.extend(self.batch_to_dicts(out))
+
+        if len(chunks) == 1:  # nothing to overlap: no staging thread (analyze(): one pair per call)
+            device_part(host_stage(*chunks[0]))
+            return res
+        from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(max_workers=1) as ex:
             fut = ex.submit(host_stage, *chunks[0])
             for k in range(len(chunks)):
-                rid, rm, cid, cm, rgb = fut.result()
+                staged = fut.result()
                 if k + 1 < len(chunks):
                     fut = ex.submit(host_stage, *chunks[k + 1])
-                self._fit_text(rid.shape[1])
-                eff, clp = self._windows(*rgb)
-                out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
-                # clip_similarity is the cosine of the two CLIP embeddings: non-finite only when a
-                # stream overflowed fp16 (a zero vault row's NaN stays in top_sims); checked on the
-                # results already read back (no device launch: analyze() at B = 1 -0.2 ms)
-                if self.engine.clip_stream_overflow(out["scores"][:, 3]):
-                    out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
-                res.extend(self.batch_to_dicts(out))
+                device_part(staged)
         return res
 
     def _windows(self, n: int, st, rest: List[int], rgb: List[np.ndarray]):
