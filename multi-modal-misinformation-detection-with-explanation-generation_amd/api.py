@@ -14,6 +14,7 @@ There is no CPU fallback: without a HIP device the constructors raise.
 from __future__ import annotations
 
 import itertools
+import math
 import os
 import warnings
 from collections import OrderedDict
@@ -509,19 +510,20 @@ class MisinfoForensics:
         _, sc = self.engine.effnet_forward(px)
         return {"deepfake_score": float(sc.cpu().numpy()[0])}
 
-    def _image_emb(self, pil) -> torch.Tensor:
+    def _image_emb(self, pil, check: bool = True) -> torch.Tensor:
         """CLIP image embedding [1,512] of one image.  analyze_consistency and search_vault both
         embed the image (quirk Q6: the reference runs the ViT twice per pair, misinfo_forensics.py:395,
         438; FusionTrainingDataset calls them back to back, train_fusion_judge.py:81-85): the last
         embedding is kept with a 128-bit hash of its 224x224 input window, and an identical window
         reuses it -- the same kernels on the same bytes, so the value is the one a second ViT pass
-        would return."""
+        would return.  check = False: the caller checks a value computed from the embedding for the
+        fp16-stream overflow instead (analyze_consistency: its cosine)."""
         px = io_utils.clip_pixels(pil)
         key = xxhash.xxh3_128_digest(px.tobytes()) if self.reuse_image_embedding else None
         if key is not None and self._emb_cache is not None and self._emb_cache[0] == key:
             return self._emb_cache[1]
         emb = self.engine.clip_image(px[None])
-        if self.engine.clip_stream_overflow(emb):  # fp16 stream overflow: re-run on fp32 streams
+        if check and self.engine.clip_stream_overflow(emb):  # fp16 stream overflow: re-run on fp32 streams
             emb = self.engine.clip_image(px[None])
         self._emb_cache = (key, emb)
         self.vit_passes += 1
@@ -530,12 +532,18 @@ class MisinfoForensics:
     def analyze_consistency(self, text: str, image_path) -> Dict[str, float]:
         """misinfo_forensics.py:375-408."""
         ids, mask = self._clip_ids([text])
+        pil = io_utils.to_pil(image_path)
         t = self.engine.clip_text(ids, mask)
-        if self.engine.clip_stream_overflow(t):
+        i = self._image_emb(pil, check=False)
+        sim = float((t * i).sum().item())
+        # the cosine is non-finite iff either embedding overflowed an fp16 stream: checked on the value
+        # read back anyway (no isfinite launches); then both are re-run on fp32 streams
+        if not math.isfinite(sim) and self.engine.clip_stream_overflow(np.array([sim])):
             self._emb_cache = None
             t = self.engine.clip_text(ids, mask)
-        i = self._image_emb(io_utils.to_pil(image_path))
-        return {"clip_similarity": float((t * i).sum().item())}
+            i = self._image_emb(pil)
+            sim = float((t * i).sum().item())
+        return {"clip_similarity": sim}
 
     def search_vault(self, image_path, user_caption: str = None, top_k: int = 5) -> Dict:
         """misinfo_forensics.py:410-491."""

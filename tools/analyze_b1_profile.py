@@ -1,5 +1,6 @@
-"""cProfile of the B = 1 analyze() path (bench.py per_sample_lines' setup): where the host time of
-one call goes besides the device work.   python tools/analyze_b1_profile.py [calls]"""
+"""cProfile of the B = 1 analyze() path, or of FusionTrainingDataset's per-row calls ("rows"), with
+bench.py per_sample_lines' setup: where the host time of one call goes besides the device work.
+    python tools/analyze_b1_profile.py [calls] [rows]"""
 import cProfile
 import os
 import pstats
@@ -28,16 +29,24 @@ def main():
     mf = MisinfoForensics(fusion_weights="", faiss_index_path="", synthetic_seed=0, roberta_tokenizer=rob,
                           clip_processor=clp, verbose=False)
     mf.set_vault(syn.vault(2170, 512, 77), meta)
+    rows = len(sys.argv) > 2 and sys.argv[2] == "rows"
+
+    def call(i):
+        if not rows:  # the dashboard path
+            return mf.analyze(text=texts[i], image_path=pils[i], verbose=False)
+        # FusionTrainingDataset.__getitem__'s four calls (train_fusion_judge.py:72-86)
+        return (mf.analyze_text(texts[i]), mf.analyze_image(pils[i]), mf.analyze_consistency(texts[i], pils[i]),
+                mf.search_vault(pils[i]))
     for i in range(10):
-        mf.analyze(text=texts[i], image_path=pils[i], verbose=False)
+        call(i)
     t0 = time.perf_counter()
     for i in range(10, 10 + n):
-        mf.analyze(text=texts[i], image_path=pils[i], verbose=False)
-    print(f"plain: {(time.perf_counter() - t0) / n * 1e3:.3f} ms / call")
+        call(i)
+    print(f"plain: {(time.perf_counter() - t0) / n * 1e3:.3f} ms / call ({'rows' if rows else 'analyze'})")
     pr = cProfile.Profile()
     pr.enable()
     for i in range(10, 10 + n):
-        mf.analyze(text=texts[i], image_path=pils[i], verbose=False)
+        call(i)
     pr.disable()
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(25)
