@@ -222,19 +222,46 @@ int mmf_profile_begin(mmf_handle* h);
 int mmf_profile_end(mmf_handle* h, int max_kinds, int* counts, double* ms, double* flops, double* bytes);
 const char* mmf_profile_kind_name(int kind);
 
-/* Run-time options (defaults read once per process from MMF_* environment variables):
- * "concurrent" (tower streams), "fuse_stem", "fuse_expand", "dw_ct", "dw_v2", "gemm_splitk",
- * "gemm_config", "gemm_group_m", "gemm_prio", "text_hilo", "clip_res16", "lazy_ln" (A/B switches
- * of layouts and fusions; the defaults are the measured best) and "effnet_fp32"
- * (EfficientNet tower with fp32 activations, fp32-FMA 1x1 convs and precise SiLU: the mode for
- * checkpoints whose logits amplify fp16 storage rounding past 1e-3; ~4x the tower time).  With the
- * defaults a row's results do not depend on the batch it runs in (tests/test_gpu_parity.py).
- * "text_hilo" = -1 (default) picks RoBERTa's residual-stream layout when the weights are packed:
- * fp16 hi + lo if the LayerNorm parameters bound the stream above 64 (max_c |beta_c| + 4|gamma_c|,
- * trained-model outlier channels), fp16 alone otherwise; the read-only name "text_hilo_effective"
- * (mmf_get_option with a handle) returns the layout in use.
- * h = NULL reads/changes the process defaults used by the handle-less ops below and by handles
- * created afterwards. */
+/* Run-time options.  Defaults are read once per process from MMF_<NAME> environment variables
+ * (e.g. MMF_GEMM_KLOOP), copied into every handle at mmf_create and changed with mmf_set_option
+ * (h = NULL: the process defaults, used by the handle-less ops below and by handles created
+ * afterwards).  The library's list is exactly the following (mmf_option_name enumerates it; the CPU
+ * test tests/test_capi_cpu.py::test_header_options_match_library ties the two):
+ *   "concurrent"     1: towers of mmf_analyze_batch on concurrent streams (0: one stream)
+ *   "fuse_stem"      1: EfficientNet stem fused into the stage-1 depthwise conv
+ *   "fuse_expand"    1: 1x1 expand fused into the depthwise conv (stages 2 - 4.3)
+ *   "gemm_splitk"    1: split-K on the skinny-M (M <= 512) GEMM path
+ *   "gemm_config"   -1: automatic GEMM tile choice; c >= 0 forces instantiation c (A/B tools)
+ *   "gemm_group_m"   0: persistent GEMM tile order (g > 0: grouped by g row panels)
+ *   "gemm_kloop"     0: K-loop schedule of the persistent plain / producer GEMMs (0 two LDS stages,
+ *                       1 ping-pong SIMD partners, 3 A-operand ring of three slots; bit-identical)
+ *   "text_hilo"     -1: RoBERTa stream layout: -1 chosen at weight-load time from the LayerNorm
+ *                       bound (fp16 hi + lo if max_c |beta_c| + sqrt(767) |gamma_c| > 64, fp16 alone
+ *                       otherwise), 0 fp16, 1 fp16 hi + lo, 2 precise mode (fp32 stream, LayerNorm,
+ *                       attention and branch outputs; GEMM operands per "text_prec_mask").  2 needs
+ *                       the precise weights (packed unless the layout was pinned to 0 / 1 at load)
+ *   "text_prec_mask" 15: precise mode: GEMM kinds on ~22-bit K-concatenated hi / lo operands (bit 1
+ *                       QKV, 2 out-proj, 4 FFN-1, 8 FFN-2); the other kinds read fp16 operands
+ *   "effnet_fp32"    0: 1 = EfficientNet tower with fp32 activations, fp32-MFMA 1x1 convs and
+ *                       precise SiLU (checkpoints whose logits amplify fp16 storage rounding)
+ *   "clip_res16"     1: CLIP pre-LN residual streams in fp16 (0: fp32)
+ *   "lazy_ln"        1: CLIP encoder LayerNorms folded into the GEMM epilogues
+ *   "pw32_mfma"      5: fp32 tower's 1x1 convs (0 fp32-FMA VALU, 1 / 2 fp32 MFMA with 1 / 3 K-chunks
+ *                       prefetched, 3 / 4 / 5 whole-row tiles; bit-identical)
+ *   "effnet_chunks"  2: mmf_effnet_forward batch chunks on concurrent streams
+ *   "dw_cw32"        1: 32-channel groups for the standalone depthwise convs
+ *   "diag_skip"      0: diagnostic bitmask of towers mmf_analyze_batch leaves out (2 EfficientNet,
+ *                       4 CLIP text, 8 ViT, ...; measurement only)
+ *   "qkv_attn"       1: RoBERTa L = 128: attention in the QKV GEMM's epilogue
+ *   "mt_enqueue"    64: batches of <= this many pairs: towers enqueued by host threads side by side
+ *   "last_q1"        1: compact last encoder layers (bit 1 RoBERTa, bit 2 CLIP towers)
+ *   "after_text"    12: towers of the concurrent step that start once RoBERTa is done (bitmask as
+ *                       diag_skip)
+ * The defaults are the measured best; with them a row's results do not depend on the
+ * batch it runs in (tests/test_gpu_parity.py).  Read-only names for mmf_get_option with a handle:
+ * "text_hilo_effective" (the RoBERTa layout in use) and "text_precise_packed" (bitmask of the GEMM
+ * kinds whose precise-mode weights are packed, as "text_prec_mask"). */
+const char* mmf_option_name(int i); /* i-th option name, NULL past the end */
 int mmf_set_option(mmf_handle* h, const char* name, int value);
 int mmf_get_option(mmf_handle* h, const char* name, int* value);
 /* Device bytes currently owned by the handle (weights, workspaces, vault). */

@@ -500,15 +500,20 @@ class MisinfoForensics:
         ids = self._rob_ids(text)
         self.detector.sync(("text",))
         _, _, sc = self.engine.text_forward(ids, np.ones_like(ids))
-        s = sc.cpu().numpy()[0]
-        return {"ai_score": float(s[0]), "misinfo_score": float(s[1])}
+        s = sc.cpu().numpy()
+        if self.engine.text_overflow(s):  # fp16 branch output overflowed: re-run in the precise mode
+            s = self.engine.text_forward(ids, np.ones_like(ids))[2].cpu().numpy()
+        return {"ai_score": float(s[0, 0]), "misinfo_score": float(s[0, 1])}
 
     def analyze_image(self, image_path) -> Dict[str, float]:
         """misinfo_forensics.py:354-373."""
         px = io_utils.effnet_pixels(io_utils.to_pil(image_path))[None]
         self.detector.sync(("effnet",))
         _, sc = self.engine.effnet_forward(px)
-        return {"deepfake_score": float(sc.cpu().numpy()[0])}
+        s = sc.cpu().numpy()
+        if self.engine.effnet_overflow(s):  # fp16 activation overflowed: re-run on the fp32 tower
+            s = self.engine.effnet_forward(px)[1].cpu().numpy()
+        return {"deepfake_score": float(s[0])}
 
     def _image_emb(self, pil, check: bool = True) -> torch.Tensor:
         """CLIP image embedding [1,512] of one image.  analyze_consistency and search_vault both
@@ -594,6 +599,8 @@ class MisinfoForensics:
         self.detector.sync(("effnet",))
         cap = self.engine.max_batch  # frames beyond the reserved batch run as further launches
         dsc = torch.cat([self.engine.effnet_forward(eff[i:i + cap])[1] for i in range(0, F, cap)])
+        if self.engine.effnet_overflow(dsc.cpu().numpy()):
+            dsc = torch.cat([self.engine.effnet_forward(eff[i:i + cap])[1] for i in range(0, F, cap)])
         iemb = torch.cat([self.engine.clip_image(clp[i:i + cap]) for i in range(0, F, cap)])
         if self.engine.clip_stream_overflow(iemb):
             iemb = torch.cat([self.engine.clip_image(clp[i:i + cap]) for i in range(0, F, cap)])
@@ -734,10 +741,11 @@ class MisinfoForensics:
             self._fit_text(rid.shape[1])
             eff, clp = self._windows(*rgb)
             out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
-            # clip_similarity is the cosine of the two CLIP embeddings: non-finite only when a
-            # stream overflowed fp16 (a zero vault row's NaN stays in top_sims); checked on the
-            # results already read back (no device launch: analyze() at B = 1 -0.2 ms)
-            if self.engine.clip_stream_overflow(out["scores"][:, 3]):
+            # run-time precision traps on the results already read back (no device launch: analyze()
+            # at B = 1 -0.2 ms): a non-finite text score / deepfake score / clip_similarity (the cosine
+            # of the two CLIP embeddings; a zero vault row's NaN stays in top_sims) means an fp16
+            # stream overflowed -- that tower switches precision and the batch runs again
+            if self.engine.scores_overflow(out["scores"]):
                 out = self.batch_to_host(self.analyze_batch(rid, rm, cid, cm, eff, clp))
             res.extend(self.batch_to_dicts(out))
 

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256, 4) void attention_kernel(const f16_t* __restri
     }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
-    const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+    const float inv = sum == 0.f ? 0.f : 1.0f / sum;
     // O^T[d][q] = sum_key V^T[d][key] P^T[key][q] over 32-key blocks; B operand of lane (fr, fg):
     // k-index 8fg + i <-> key 32kb + 4fg + i (i < 4, tile 2kb) / 32kb + 16 + 4fg + (i - 4) (tile 2kb+1)
     f32x4 o[4];
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void attention_long_kernel(const f16_t* __rest
       }
     }
     if (qq < L) {
-      const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+      const float inv = sum == 0.f ? 0.f : 1.0f / sum;
       f16_t* dst = out + ((size_t)bi * L + qq) * ldo + h * 64 + fg * 4;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(256) void attention_q1_kernel(const float* __restri
     for (int u = 0; u < 32; ++u)
       if (jb + u < jend) o = fmaf(ps[wave][jb + u], h2f(vv[u]), o);
   }
-  out[(size_t)bi * ldo + h * 64 + lane] = f2h(sum > 0.f ? o / sum : 0.f);
+  out[(size_t)bi * ldo + h * 64 + lane] = f2h(sum == 0.f ? 0.f : o / sum);  // (non-finite sum: propagates)
 }
 
 }  // namespace

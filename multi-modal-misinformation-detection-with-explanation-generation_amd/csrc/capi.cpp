@@ -100,6 +100,7 @@ struct Workspace {
   // RoBERTa
   float *r_x = nullptr, *r_y = nullptr;
   uint16_t* r_lo = nullptr;  // fp16 low part of the split post-LN residual stream (hi = r_xb)
+  int* r_ovf = nullptr;      // [cap_b] overflow sentinel of the fp16 / split stream (norm.hip; run_text)
   f16_t *r_xb = nullptr, *r_qkv = nullptr, *r_ctx = nullptr, *r_h = nullptr;
   // CLIP vision
   f16_t *v_col = nullptr, *v_xb = nullptr, *v_qkv = nullptr, *v_ctx = nullptr, *v_h = nullptr, *v_cls = nullptr;
@@ -142,8 +143,11 @@ struct Options {
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
+  int gemm_kloop = 0;   // K-loop variant of the persistent plain / producer GEMMs (gemm_glds_body.inc KL: 0 two
+                        // stages, 1 ping-pong, 3 A-ring; all bit-identical)
   int text_hilo = -1;   // RoBERTa residual stream as fp16 hi + fp16 lo (1), fp16 alone (0), or chosen at
-                        // weight-load time from the LayerNorm parameters (-1, default: DESIGN §4)
+                        // weight-load time from the LayerNorm parameters (-1, default: DESIGN §4); 2 = precise mode
+  int text_prec_mask = 15;  // precise mode: GEMM kinds on hi / lo operands (1 QKV, 2 out-proj, 4 FFN-1, 8 FFN-2)
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
   int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
@@ -169,8 +173,9 @@ const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
     {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
-    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"},
-    {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
+    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_kloop", &Options::gemm_kloop, "MMF_GEMM_KLOOP"},
+    {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"text_prec_mask", &Options::text_prec_mask, "MMF_TEXT_PREC_MASK"},
+    {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},
     {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"}, {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},
@@ -194,12 +199,16 @@ void apply_options(const Options& o, GemmArgs* g) {
   g->force_cfg = o.gemm_config >= 0 ? o.gemm_config + 1 : 0;
   g->no_splitk = o.gemm_splitk ? 0 : 1;
   g->group_m = o.gemm_group_m;
+  g->kloop = o.gemm_kloop;
 }
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the
 // workspaces) frees exactly what it replaces.
 enum AllocGroup {
   AG_WS = 0, AG_TEXT, AG_EFF, AG_VIS, AG_CTEXT, AG_FUSION, AG_VAULT, AG_TITLES, AG_SIMS, AG_EFF32, AG_RESIZE, AG_TEXT32,
+  // the RoBERTa precise mode's K-concatenated weights, one group per GEMM kind (bit k of option
+  // text_prec_mask <-> group AG_TP0 + k: QKV, out-proj, FFN-1, FFN-2), releasable one kind at a time
+  AG_TP0, AG_TP1, AG_TP2, AG_TP3,
   AG_COUNT
 };
 
@@ -288,7 +297,7 @@ struct mmf_handle {
   // the split stream it selects under text_hilo = -1 (finalize_text)
   float r_stream_mag = 0.f;
   int r_hilo_auto = 0;
-  int r_precise = 0;  // the precise-mode weights (EncLayer qkv3 ...) are packed
+  int r_precise = 0;  // bitmask of the GEMM kinds whose precise-mode weights (EncLayer qkv3 ...) are packed
   float *h_w1a = nullptr, *h_b1a = nullptr, *h_w2a = nullptr, *h_b2a = nullptr;
   float *h_w1m = nullptr, *h_b1m = nullptr, *h_w2m = nullptr, *h_b2m = nullptr;
   // EfficientNet
@@ -437,7 +446,8 @@ int up_f16(mmf_handle* h, f16_t** dst, const std::vector<float>& v) {
 }
 
 // W [out][in] fp32 -> [W_hi | W_hi | W_lo] fp16 [out][3 in] (precise.hip: the K-concatenated weight)
-int up_split3(mmf_handle* h, Lin16* dst, const std::vector<float>& w, const float* bias, int out, int in) {
+int up_split3(mmf_handle* h, Lin16* dst, const std::vector<float>& w, const float* bias, int out, int in,
+              int group = -1) {
   std::vector<uint16_t> b((size_t)out * 3 * in);
   for (int n = 0; n < out; ++n)
     for (int k = 0; k < in; ++k) {
@@ -448,7 +458,11 @@ int up_split3(mmf_handle* h, Lin16* dst, const std::vector<float>& w, const floa
       r[in + k] = hi;
       r[2 * in + k] = f2h_host(x - h2f_host(hi));
     }
-  CHK(upload(h, &dst->w, b));
+  const int saved = h->cur_group;
+  if (group >= 0) h->cur_group = group;
+  const int r = upload(h, &dst->w, b);
+  h->cur_group = saved;
+  CHK(r);
   dst->b = const_cast<float*>(bias);
   dst->out = out;
   dst->in = 3 * in;
@@ -492,13 +506,14 @@ int load_ln(mmf_handle* h, LNp* ln, const std::string& p, int n) {
   CHK(load_f32_padded(h, &ln->g, p + ".weight", n));
   return load_f32_padded(h, &ln->b, p + ".bias", n);
 }
-int load_lin(mmf_handle* h, Lin16* l, const std::string& p, int out, int in, bool bias, Lin16* split3 = nullptr) {
+int load_lin(mmf_handle* h, Lin16* l, const std::string& p, int out, int in, bool bias, Lin16* split3 = nullptr,
+             int split3_group = -1) {
   GET(w, p + ".weight", (size_t)out * in);
   CHK(up_f16(h, &l->w, w->f));
   if (bias) CHK(load_f32_padded(h, &l->b, p + ".bias", out));
   l->out = out;
   l->in = in;
-  if (split3) CHK(up_split3(h, split3, w->f, l->b, out, in));
+  if (split3) CHK(up_split3(h, split3, w->f, l->b, out, in, split3_group));
   return 0;
 }
 // LN(x) W^T + b with LN = (gamma, beta) folded (gemm.hip lazy LN): w' = fp16(w diag(gamma)),
@@ -550,7 +565,7 @@ int load_qkv(mmf_handle* h, EncLayer* L, const std::string& q, const std::string
   CHK(up_f32_padded(h, &l->b, b));
   l->out = 3 * H;
   l->in = H;
-  if (split3) CHK(up_split3(h, &L->qkv3, w, l->b, 3 * H, H));
+  if (split3) CHK(up_split3(h, &L->qkv3, w, l->b, 3 * H, H, AG_TP0));
   if (heads) {
     std::vector<float> wh(w.size()), bh(b.size());
     for (int hd = 0; hd < H / 64; ++hd)
@@ -635,21 +650,24 @@ int finalize_text(mmf_handle* h) {
   }
   // the precise mode's K-concatenated weights (+510 MB) are packed unless the layout is pinned to an
   // fp16 stream (text_hilo 0 / 1): the load-time calibration (engine.py) may select the mode
+  // (each kind's K-concatenated weights in its own allocation group AG_TP0 + k, so that the engine's
+  // calibration can release the kinds the selected mode does not read: option text_precise_packed)
   const bool sp = h->opt.text_hilo < 0 || h->opt.text_hilo >= 2;
   h->r_precise = 0;
+  for (int k = 0; k < 4; ++k) CHK(free_group(h, AG_TP0 + k));
   for (int i = 0; i < 12; ++i) {
     const std::string l = p + "encoder.layer." + std::to_string(i) + ".";
     EncLayer& L = h->r_layers[i];
     L.qkv3 = L.o3 = L.fc13 = L.fc23 = Lin16{};
     CHK(load_qkv(h, &L, l + "attention.self.query", l + "attention.self.key", l + "attention.self.value", 768, "",
                  true, sp));
-    CHK(load_lin(h, &L.o, l + "attention.output.dense", 768, 768, true, sp ? &L.o3 : nullptr));
+    CHK(load_lin(h, &L.o, l + "attention.output.dense", 768, 768, true, sp ? &L.o3 : nullptr, AG_TP0 + 1));
     CHK(load_ln(h, &L.ln1, l + "attention.output.LayerNorm", 768));
-    CHK(load_lin(h, &L.fc1, l + "intermediate.dense", 3072, 768, true, sp ? &L.fc13 : nullptr));
-    CHK(load_lin(h, &L.fc2, l + "output.dense", 768, 3072, true, sp ? &L.fc23 : nullptr));
+    CHK(load_lin(h, &L.fc1, l + "intermediate.dense", 3072, 768, true, sp ? &L.fc13 : nullptr, AG_TP0 + 2));
+    CHK(load_lin(h, &L.fc2, l + "output.dense", 768, 3072, true, sp ? &L.fc23 : nullptr, AG_TP0 + 3));
     CHK(load_ln(h, &L.ln2, l + "output.LayerNorm", 768));
   }
-  h->r_precise = sp ? 1 : 0;
+  h->r_precise = sp ? 15 : 0;
   for (int hd = 0; hd < 2; ++hd) {
     const std::string n = hd ? "misinfo_head" : "ai_head";
     GET(w1, n + ".0.weight", (size_t)256 * 768);
@@ -885,9 +903,9 @@ int add_ln(mmf_handle* h, f16_t* x, int ldx, const f16_t* y, int ldy, const LNp&
 }
 
 int add_ln_hilo(mmf_handle* h, f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const LNp& p, int rows,
-                hipStream_t s) {
+                hipStream_t s, int* ovf = nullptr, int L = 0) {
   ProfScope ps(h, s, PK_LN, 9.0 * rows * 768, (double)rows * 768 * (2 + 2 + 2 + 2 + 2));
-  HIPCHK(launch_add_ln_hilo(hi, lo, ld, y, ldy, p.g, p.b, 1e-5f, rows, 768, s));
+  HIPCHK(launch_add_ln_hilo(hi, lo, ld, y, ldy, p.g, p.b, 1e-5f, rows, 768, s, ovf, L));
   return 0;
 }
 
@@ -909,8 +927,10 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
                      float* scores, int score_stride, hipStream_t s) {
   Workspace& w = h->ws;
   const int M = B * L;
-  if (!h->r_precise) return fail(MMF_EINVAL, "text_hilo = 2: the precise-mode weights were not packed (load the text "
-                                             "model with text_hilo -1 or 2)");
+  const int pm = h->opt.text_prec_mask & 15;
+  if (pm & ~h->r_precise)
+    return fail(MMF_EINVAL, "text_hilo = 2: text_prec_mask %d needs precise-mode weights that are not packed (packed: %d; "
+                            "re-load the text model with text_hilo -1 or 2)", pm, h->r_precise);
   if (!w.p32 || w.t32_rows < (size_t)M) return fail(MMF_EINVAL, "text_hilo = 2: precise workspaces not reserved");
   float* x = w.r_x;  // the fp32 residual stream [M][768]
   float* y = w.r_y;  // branch outputs / ctx [M][768]
@@ -919,10 +939,17 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
     HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, nullptr,
                                 w.r_xb, B, L, 768, 1, s, x));
   }
-  HIPCHK(launch_split3(x, 768, w.s3, M, 768, s));
+  // GEMM kind k on hi / lo operands (bit k of text_prec_mask): the K-concatenated weight, K = 3 in;
+  // otherwise the fp16 weight against the hi third of the same operand rows (K = in): fp16 x fp16
+  // products, fp32 accumulation and output.  split3 writes the lo / second hi thirds only for a
+  // consumer that reads them.
+  auto lin = [&](const f16_t* A, int lda, const Lin16& fast, const Lin16& prec, int kind) {
+    return (pm >> kind & 1) ? gemm_args(A, lda, prec, M) : gemm_args(A, lda, fast, M);
+  };
+  HIPCHK(launch_split3(x, 768, w.s3, M, 768, s, pm & 1));
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = h->r_layers[i];
-    GemmArgs g = with_ws(gemm_args(w.s3, 2304, Ly.qkv3, M), w.sk_text, w.sk_elems);
+    GemmArgs g = with_ws(lin(w.s3, 2304, Ly.qkv, Ly.qkv3, 0), w.sk_text, w.sk_elems);
     g.c32 = w.p32;
     g.ldc = 2304;
     CHK(gemm(h, g, s));
@@ -930,23 +957,23 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
       ProfScope ps(h, s, PK_ATTN, 4.0 * B * 12 * (double)L * L * 64, (double)M * (2304 + 768) * 4);
       HIPCHK(launch_attention32(w.p32, 2304, 768, 1536, mask, y, 768, B, L, 12, s));
     }
-    HIPCHK(launch_split3(y, 768, w.s3, M, 768, s));
-    g = with_ws(gemm_args(w.s3, 2304, Ly.o3, M), w.sk_text, w.sk_elems);
+    HIPCHK(launch_split3(y, 768, w.s3, M, 768, s, pm >> 1 & 1));
+    g = with_ws(lin(w.s3, 2304, Ly.o, Ly.o3, 1), w.sk_text, w.sk_elems);
     g.c32 = y;
     CHK(gemm(h, g, s));
     CHK(lnorm_add(h, x, y, Ly.ln1, M, s));
-    HIPCHK(launch_split3(x, 768, w.s3, M, 768, s));
-    g = with_ws(gemm_args(w.s3, 2304, Ly.fc13, M), w.sk_text, w.sk_elems);
+    HIPCHK(launch_split3(x, 768, w.s3, M, 768, s, pm >> 2 & 1));
+    g = with_ws(lin(w.s3, 2304, Ly.fc1, Ly.fc13, 2), w.sk_text, w.sk_elems);
     g.act = 1;  // GELU-erf
     g.c32 = w.p32;
     g.ldc = 3072;
     CHK(gemm(h, g, s));
-    HIPCHK(launch_split3(w.p32, 3072, w.h3, M, 3072, s));
-    g = with_ws(gemm_args(w.h3, 9216, Ly.fc23, M), w.sk_text, w.sk_elems);
+    HIPCHK(launch_split3(w.p32, 3072, w.h3, M, 3072, s, pm >> 3 & 1));
+    g = with_ws(lin(w.h3, 9216, Ly.fc2, Ly.fc23, 3), w.sk_text, w.sk_elems);
     g.c32 = y;
     CHK(gemm(h, g, s));
     CHK(lnorm_add(h, x, y, Ly.ln2, M, s));
-    if (i < 11) HIPCHK(launch_split3(x, 768, w.s3, M, 768, s));
+    if (i < 11) HIPCHK(launch_split3(x, 768, w.s3, M, 768, s, pm & 1));
   }
   ProfScope ps(h, s, PK_HEADS, 2.0 * B * 2 * (768 * 256 + 256 * 2), (double)B * 768 * 4 + 2 * 768 * 256 * 4);
   HIPCHK(launch_text_heads(x, L * 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,
@@ -967,10 +994,15 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   }
   uint16_t* rlo = hilo ? w.r_lo : nullptr;
   const int M = B * L;
+  // overflow sentinel: a sequence whose fp16 stream or branch output leaves fp16's range gets NaN
+  // scores (the masked softmax would hide it; engine.py's run-time trap then re-runs the batch in the
+  // precise mode)
+  int* ovf = w.r_ovf;
+  HIPCHK(hipMemsetAsync(ovf, 0, (size_t)B * sizeof(int), s));
   {
     ProfScope ps(h, s, PK_EMBED, 10.0 * M * 768, (double)M * 768 * (4 + 4 + 2 + 2));
     HIPCHK(launch_roberta_embed(ids, h->r_word, h->r_pos, h->r_type0, h->r_embln.g, h->r_embln.b, 1e-5f, rlo,
-                                w.r_xb, B, L, 768, 1, s));
+                                w.r_xb, B, L, 768, 1, s, nullptr, ovf));
   }
   for (int i = 0; i < 12; ++i) {
     const EncLayer& Ly = h->r_layers[i];
@@ -1033,7 +1065,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       g = with_ws(gemm_args(w.r_ctx, 768, Ly.o, M), w.sk_text, w.sk_elems);
       g.c16 = y;
       CHK(gemm(h, g, s));
-      CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln1, M, s));
+      CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln1, M, s, ovf, L));
       g = with_ws(gemm_args(w.r_xb, 768, Ly.fc1, M), w.sk_text, w.sk_elems);
       g.act = 1;  // GELU-erf
       g.c16 = w.r_h;
@@ -1042,7 +1074,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
       g = with_ws(gemm_args(w.r_h, 3072, Ly.fc2, M), w.sk_text, w.sk_elems);
       g.c16 = y;
       CHK(gemm(h, g, s));
-      CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln2, M, s));
+      CHK(add_ln_hilo(h, w.r_xb, rlo, 768, y, 768, Ly.ln2, M, s, ovf, L));
       continue;
     }
     const int Mr = last ? B : M;            // rows after the attention
@@ -1069,7 +1101,7 @@ int run_text(mmf_handle* h, const int32_t* ids, const int32_t* mask, int B, int 
   if (heads_ev) HIPCHK(hipEventRecord(heads_ev, s));
   ProfScope ps(h, s, PK_HEADS, 2.0 * B * 2 * (768 * 256 + 256 * 2), (double)B * 768 * 4 + 2 * 768 * 256 * 4);
   HIPCHK(launch_text_heads(w.r_x, 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,
-                           h->h_b2m, ai, mi, scores, score_stride, B, s));
+                           h->h_b2m, ai, mi, scores, score_stride, B, s, ovf));
   return 0;
 }
 
@@ -1543,7 +1575,7 @@ int ensure_mode_ws(mmf_handle* h) {
   Workspace& w = h->ws;
   const size_t rows = (size_t)h->cap_b * h->cap_lr;
   void* p;
-  if (text_mode(h) >= 2 && h->r_precise) {
+  if (text_mode(h) >= 2) {
     if (w.t32_rows < rows) {
       CHK(free_group(h, AG_TEXT32));
       CHK(dev_alloc(h, &p, rows * 3072 * 4, AG_TEXT32)); w.p32 = (float*)p;
@@ -1682,6 +1714,7 @@ int mmf_reserve(mmf_handle* h, int B, int Lr, int Lc) {
   CHK(A((void**)&w.r_y, Mr * 768 * 4));
   CHK(A((void**)&w.r_xb, Mr * 768 * 2));
   CHK(A((void**)&w.r_lo, Mr * 768 * 2));
+  CHK(A((void**)&w.r_ovf, (size_t)B * 4));
   CHK(A((void**)&w.r_qkv, Mr * 2304 * 2));
   CHK(A((void**)&w.r_ctx, Mr * 768 * 2));
   CHK(A((void**)&w.r_h, Mr * 3072 * 2));
@@ -2032,12 +2065,34 @@ const char* mmf_profile_kind_name(int kind) { return prof_kind_name(kind); }
 
 int mmf_set_option(mmf_handle* h, const char* name, int value) {
   if (!name) return fail(MMF_EINVAL, "null option name");
+  if (h && !strcmp(name, "text_precise_packed")) {
+    // release the precise-mode weights of the GEMM kinds not in `value` (the engine's calibration, once
+    // it has selected a mode that does not read them); packing happens only at weight load
+    if (value & ~h->r_precise & 15)
+      return fail(MMF_EINVAL, "text_precise_packed %d: only a subset of the packed kinds (%d) can be kept; re-load the "
+                              "text model to re-pack", value, h->r_precise);
+    if (text_mode(h) >= 2 && (h->opt.text_prec_mask & 15 & ~value))
+      return fail(MMF_EINVAL, "text_precise_packed %d: the selected precise mode (text_prec_mask %d) reads them", value,
+                  h->opt.text_prec_mask);
+    (void)hipSetDevice(h->device);
+    for (int k = 0; k < 4; ++k) {
+      if (!((h->r_precise >> k) & 1) || ((value >> k) & 1)) continue;
+      CHK(free_group(h, AG_TP0 + k));
+      for (EncLayer& L : h->r_layers) (k == 0 ? L.qkv3 : k == 1 ? L.o3 : k == 2 ? L.fc13 : L.fc23) = Lin16{};
+    }
+    h->r_precise = value & 15;
+    return 0;
+  }
   Options& o = h ? h->opt : process_options();
   for (const OptName& n : kOptNames)
     if (!strcmp(n.name, name)) {
-      if (h && !strcmp(name, "text_hilo") && value >= 2 && !h->r_precise && (h->ready & 1))
-        return fail(MMF_EINVAL, "text_hilo = 2 needs the precise-mode weights: the text model was packed with text_hilo "
-                                "%d (re-load it with -1 or 2)", o.text_hilo);
+      if (h && (h->ready & 1)) {
+        const bool prec = !strcmp(name, "text_hilo") ? value >= 2 : o.text_hilo >= 2;
+        const int pm = (!strcmp(name, "text_prec_mask") ? value : o.text_prec_mask) & 15;
+        if ((!strcmp(name, "text_hilo") || !strcmp(name, "text_prec_mask")) && prec && (pm & ~h->r_precise))
+          return fail(MMF_EINVAL, "text_hilo = 2 with text_prec_mask %d needs precise-mode weights that are not packed "
+                                  "(packed: %d; re-load the text model with text_hilo -1 or 2)", pm, h->r_precise);
+      }
       o.*(n.field) = value;
       if (h) {
         (void)hipSetDevice(h->device);
@@ -2048,10 +2103,19 @@ int mmf_set_option(mmf_handle* h, const char* name, int value) {
   return fail(MMF_EINVAL, "unknown option '%s'", name);
 }
 
+const char* mmf_option_name(int i) {
+  constexpr int n = (int)(sizeof(kOptNames) / sizeof(kOptNames[0]));
+  return (i >= 0 && i < n) ? kOptNames[i].name : nullptr;
+}
+
 int mmf_get_option(mmf_handle* h, const char* name, int* value) {
   if (!name || !value) return fail(MMF_EINVAL, "null argument");
   if (h && !strcmp(name, "text_hilo_effective")) {  // read-only: the stream layout run_text uses
     *value = h->opt.text_hilo < 0 ? h->r_hilo_auto : h->opt.text_hilo;
+    return 0;
+  }
+  if (h && !strcmp(name, "text_precise_packed")) {  // kinds whose precise-mode weights are packed
+    *value = h->r_precise;
     return 0;
   }
   const Options& o = h ? h->opt : process_options();

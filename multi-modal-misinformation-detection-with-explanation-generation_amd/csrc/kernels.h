@@ -22,6 +22,8 @@ struct GemmArgs {
   int force_cfg;                 // 0 = automatic tile choice, c + 1 = instantiation c (A/B option)
   int no_splitk;                 // 1 = never split K on the skinny-M path (A/B option)
   int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
+  int kloop;                     // K-loop variant of the persistent plain / producer GEMMs (option gemm_kloop:
+                                 // 0 two stages, 1 ping-pong, 3 A-ring; gemm_glds_body.inc)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
@@ -48,7 +50,7 @@ int gemm_ln_tn(const GemmArgs& a);
 int gemm_splitk_factor(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks
-constexpr int kGemmConfigs = 17;  // numbering of the tile instantiations (0 .. 16; gemm.hip config_exists)
+constexpr int kGemmConfigs = 19;  // numbering of the tile instantiations (0 .. 18; gemm.hip config_exists)
 const char* gemm_config_name(int c);
 // streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable
 bool pw_applicable(const GemmArgs& a);
@@ -82,16 +84,20 @@ hipError_t launch_attention(const f16_t* qkv, int ldqkv, const int32_t* mask, f1
 // with x32 non-null, the fp32 stream only (precise mode)
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
                                 const float* g, const float* b, float eps, uint16_t* xlo, f16_t* xb, int B, int L,
-                                int H, int pad_id, hipStream_t s, float* x32 = nullptr);
+                                int H, int pad_id, hipStream_t s, float* x32 = nullptr, int* ovf = nullptr);
+// ovf (nullable, [B] int32): the overflow sentinel of the fp16 / split stream -- a row whose
+// LayerNorm statistics are non-finite sets ovf[sequence] = 1 (embeddings and add+LN); the text heads
+// then return NaN for that sequence (capi.cpp run_text)
 // RoBERTa precise mode (precise.hip, option text_hilo = 2): fp32 rows -> [hi | lo | hi] fp16 rows of 3C
 // (the K-concatenated GEMM operand), and fp32 attention over an fp32 qkv (q at h*64, k at koff + h*64,
 // v at voff + h*64; key-padding mask int32 [B][L] or null) -> fp32 out [B*L][ldo]
-hipError_t launch_split3(const float* x, int ldx, f16_t* out, int rows, int C, hipStream_t s);
+// with_lo = 0: only the hi third is written (a consumer on fp16 operands)
+hipError_t launch_split3(const float* x, int ldx, f16_t* out, int rows, int C, hipStream_t s, int with_lo = 1);
 hipError_t launch_attention32(const float* qkv, int ld, int koff, int voff, const int32_t* mask, float* out, int ldo,
                               int B, int L, int H, hipStream_t s);
 // RoBERTa post-LN residual stream split as hi = fp16(x) (also the GEMM operand), lo = fp16(x - hi)
 hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const float* g,
-                              const float* b, float eps, int rows, int C, hipStream_t s);
+                              const float* b, float eps, int rows, int C, hipStream_t s, int* ovf = nullptr, int L = 0);
 hipError_t launch_hilo_rows(const f16_t* hi, const uint16_t* lo, int row_stride, float* out, int B, int C,
                             hipStream_t s);
 // CLIP text embeddings (tok + pos) -> x fp32 (or x16 fp16: exactly one non-null), then LN1 of layer 0
@@ -124,7 +130,7 @@ hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s);
 hipError_t launch_text_heads(const float* x, int row_stride, const float* w1a, const float* b1a,
                              const float* w2a, const float* b2a, const float* w1m, const float* b1m,
                              const float* w2m, const float* b2m, float* ai_logits, float* mi_logits,
-                             float* scores, int score_stride, int B, hipStream_t s);
+                             float* scores, int score_stride, int B, hipStream_t s, const int* ovf = nullptr);
 // fusion MLP 5->64->32->2 (+ verdict, confidence, explanation rule)
 hipError_t launch_fusion(const float* x5, const float* w0, const float* b0, const float* w3, const float* b3,
                          const float* w5, const float* b5, float* probs, int32_t* verdict, float* conf,

@@ -15,7 +15,7 @@ __global__ __launch_bounds__(1024) void text_heads_kernel(const float* x, int ro
                                                          const float* b1a, const float* w2a, const float* b2a,
                                                          const float* w1m, const float* b1m, const float* w2m,
                                                          const float* b2m, float* ai_logits, float* mi_logits,
-                                                         float* scores, int score_stride, int B) {
+                                                         float* scores, int score_stride, int B, const int* ovf) {
   // 1024 threads: hidden unit h = tid % 256 of K-slice ks = tid / 256 (192 inputs each), so each
   // thread's dependent load/FMA chain is a quarter of the 768; slices combined in fixed order.
   constexpr int KS = 4, KL = 768 / KS;
@@ -74,6 +74,7 @@ __global__ __launch_bounds__(1024) void text_heads_kernel(const float* x, int ro
 #pragma unroll
     for (int o = 0; o < 2; ++o) l[o] = red[0][r][o] + red[1][r][o] + red[2][r][o] + red[3][r][o];
     l[0] += b2[0]; l[1] += b2[1];
+    if (ovf && ovf[row]) l[0] = l[1] = __builtin_nanf("");  // the sequence's fp16 stream overflowed (norm.hip)
     if (logits) { logits[row * 2] = l[0]; logits[row * 2 + 1] = l[1]; }
     if (scores) {  // softmax(l)[1] = exp(l1 - m) / (exp(l0 - m) + exp(l1 - m))
       const float m = fmaxf(l[0], l[1]);
@@ -461,9 +462,9 @@ __global__ __launch_bounds__(1024) void vault_sort_topk_kernel(const float* S, i
 hipError_t launch_text_heads(const float* x, int row_stride, const float* w1a, const float* b1a, const float* w2a,
                              const float* b2a, const float* w1m, const float* b1m, const float* w2m,
                              const float* b2m, float* ai_logits, float* mi_logits, float* scores, int score_stride,
-                             int B, hipStream_t s) {
+                             int B, hipStream_t s, const int* ovf) {
   hipLaunchKernelGGL(text_heads_kernel, dim3((B + 3) / 4, 2), dim3(1024), 0, s, x, row_stride, w1a, b1a, w2a, b2a, w1m,
-                     b1m, w2m, b2m, ai_logits, mi_logits, scores, score_stride, B);
+                     b1m, w2m, b2m, ai_logits, mi_logits, scores, score_stride, B, ovf);
   return hipGetLastError();
 }
 

@@ -10,7 +10,7 @@
 namespace {
 
 template <int NV>
-MMF_DEV void ln_row(float4 (&v)[NV], const float* g, const float* b, float eps, int C, int lane) {
+MMF_DEV bool ln_row(float4 (&v)[NV], const float* g, const float* b, float eps, int C, int lane) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) s += v[i].x + v[i].y + v[i].z + v[i].w;
@@ -32,6 +32,9 @@ MMF_DEV void ln_row(float4 (&v)[NV], const float* g, const float* b, float eps, 
     v[i].z = v[i].z * rstd * gg.z + bb.z;
     v[i].w = v[i].w * rstd * gg.w + bb.w;
   }
+  // the row's statistics are finite iff every input was (an inf or NaN makes the mean or the
+  // variance non-finite): wave-uniform
+  return __builtin_isfinite(mean) && __builtin_isfinite(rstd);
 }
 
 template <int NV>
@@ -166,7 +169,8 @@ MMF_DEV void store_row_hilo(const float4 (&v)[NV], f16_t* hi, uint16_t* lo, int 
 // HILO = false: the stream is hi alone (fp16; option text_hilo = 0)
 template <int NV, bool HILO>
 __global__ __launch_bounds__(256) void add_ln_hilo_kernel(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy,
-                                                          const float* g, const float* b, float eps, int rows) {
+                                                          const float* g, const float* b, float eps, int rows,
+                                                          int* ovf, int L) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   float4 v[NV];
@@ -188,7 +192,11 @@ __global__ __launch_bounds__(256) void add_ln_hilo_kernel(f16_t* hi, uint16_t* l
     v[i].z = (lo_h(xh[i].y) + lo_h(xl[i].y)) + lo_h(a[i].y);
     v[i].w = (hi_h(xh[i].y) + hi_h(xl[i].y)) + hi_h(a[i].y);
   }
-  ln_row<NV>(v, g, b, eps, NV * 256, lane);
+  // overflow sentinel (ovf, per sequence of L rows): an fp16 branch output or stream row that
+  // left fp16's range makes this row's statistics non-finite -- flagged, so that the text heads
+  // return NaN scores for the sequence (the attention's masked softmax would otherwise hide a
+  // non-finite key row behind finite outputs) and the API's run-time trap sees it
+  if (!ln_row<NV>(v, g, b, eps, NV * 256, lane) && ovf && lane == 0) ovf[row / L] = 1;
   store_row_hilo<NV>(v, hr, HILO ? lr : nullptr, lane);
 }
 
@@ -213,7 +221,7 @@ template <int NV>
 __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, const float* word, const float* pos,
                                                             const float* type0, const float* g, const float* b,
                                                             float eps, uint16_t* xlo, f16_t* xb, float* x32, int L,
-                                                            int pad) {
+                                                            int pad, int* ovf) {
   __shared__ int s_ids[512];
   __shared__ int s_pos[512];
   const int bi = blockIdx.x, tid = threadIdx.x;
@@ -244,7 +252,7 @@ __global__ __launch_bounds__(256) void roberta_embed_kernel(const int32_t* ids, 
     add_row<NV>(v, type0, lane);
     add_row<NV>(v, pos + (size_t)s_pos[t] * C, lane);
     const size_t r = (size_t)bi * L + t;
-    ln_row<NV>(v, g, b, eps, C, lane);
+    if (!ln_row<NV>(v, g, b, eps, C, lane) && ovf && lane == 0) ovf[bi] = 1;
     if (x32) store_row<NV>(v, x32 + r * C, nullptr, lane);  // precise mode: the fp32 stream
     else store_row_hilo<NV>(v, xb + r * C, xlo ? xlo + r * C : nullptr, lane);
   }
@@ -439,11 +447,11 @@ hipError_t launch_add_ln(const f16_t* x, int ldx, const f16_t* y, int ldy, const
 
 hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const float* pos, const float* type0,
                                 const float* g, const float* b, float eps, uint16_t* xlo, f16_t* xb, int B, int L,
-                                int H, int pad_id, hipStream_t s, float* x32) {
+                                int H, int pad_id, hipStream_t s, float* x32, int* ovf) {
   if (H != 768 || L > 512) return hipErrorInvalidValue;
   // 4 workgroups per sequence: one per sequence left the chip at 256 workgroups (~77 us at B = 256)
   hipLaunchKernelGGL(roberta_embed_kernel<3>, dim3(B, 4), dim3(256), 0, s, ids, word, pos, type0, g, b, eps, xlo, xb, x32,
-                     L, pad_id);
+                     L, pad_id, ovf);
   return hipGetLastError();
 }
 
@@ -517,14 +525,14 @@ hipError_t launch_l2norm(float* x, int B, int C, hipStream_t s) {
 }
 
 hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const float* g,
-                              const float* b, float eps, int rows, int C, hipStream_t s) {
-  if (C != 768 || (ld & 3) || (ldy & 3)) return hipErrorInvalidValue;
+                              const float* b, float eps, int rows, int C, hipStream_t s, int* ovf, int L) {
+  if (C != 768 || (ld & 3) || (ldy & 3) || (ovf && L <= 0)) return hipErrorInvalidValue;
   if (lo)
     hipLaunchKernelGGL((add_ln_hilo_kernel<3, true>), dim3((rows + 3) / 4), dim3(256), 0, s, hi, lo, ld, y, ldy, g, b, eps,
-                       rows);
+                       rows, ovf, L);
   else
     hipLaunchKernelGGL((add_ln_hilo_kernel<3, false>), dim3((rows + 3) / 4), dim3(256), 0, s, hi, lo, ld, y, ldy, g, b,
-                       eps, rows);
+                       eps, rows, ovf, L);
   return hipGetLastError();
 }
 

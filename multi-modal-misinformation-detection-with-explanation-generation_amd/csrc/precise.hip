@@ -14,7 +14,9 @@
 
 namespace {
 
-// out[r][0:C] = hi, out[r][C:2C] = lo, out[r][2C:3C] = hi; one thread per 4 consecutive columns
+// out[r][0:C] = hi, out[r][C:2C] = lo, out[r][2C:3C] = hi; one thread per 4 consecutive columns.
+// LO = false: hi alone (the consumer GEMM reads the first third: text_prec_mask bit clear)
+template <bool LO>
 __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x, int ldx, f16_t* __restrict__ out,
                                                      int rows, int C) {
   const int q = C >> 2;
@@ -26,8 +28,10 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
   const uint2 lo = make_uint2(pack2h(v.x - lo_h(hi.x), v.y - hi_h(hi.x)), pack2h(v.z - lo_h(hi.y), v.w - hi_h(hi.y)));
   f16_t* o = out + (size_t)r * 3 * C + c;
   *reinterpret_cast<uint2*>(o) = hi;
-  *reinterpret_cast<uint2*>(o + C) = lo;
-  *reinterpret_cast<uint2*>(o + 2 * C) = hi;
+  if constexpr (LO) {
+    *reinterpret_cast<uint2*>(o + C) = lo;
+    *reinterpret_cast<uint2*>(o + 2 * C) = hi;
+  }
 }
 
 // fp32 multi-head attention, head dim 64, any L (RoBERTa <= 512): one thread per query, 128 queries
@@ -125,11 +129,14 @@ __global__ __launch_bounds__(A32_Q) void attention32_kernel(const float* __restr
 
 }  // namespace
 
-hipError_t launch_split3(const float* x, int ldx, f16_t* out, int rows, int C, hipStream_t s) {
+hipError_t launch_split3(const float* x, int ldx, f16_t* out, int rows, int C, hipStream_t s, int with_lo) {
   if (rows <= 0) return hipSuccess;
   if ((C & 3) || (ldx & 3)) return hipErrorInvalidValue;
   const size_t n = (size_t)rows * (C / 4);
-  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, out, rows, C);
+  if (with_lo)
+    hipLaunchKernelGGL(split3_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, out, rows, C);
+  else
+    hipLaunchKernelGGL(split3_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, out, rows, C);
   return hipGetLastError();
 }
 

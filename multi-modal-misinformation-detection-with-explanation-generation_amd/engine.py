@@ -50,7 +50,18 @@ class Engine:
         self.text_precision = text_precision
         self.effnet_check = None
         self.text_check = None
-        self.set_option("text_hilo", self.TEXT_PRECISIONS[text_precision])
+        # an MMF_TEXT_HILO / MMF_EFFNET_FP32 environment value pins the tower under "auto"
+        # (no calibration overrides it); so does a set_option of text_hilo / effnet_fp32 made after
+        # the engine's own last write (_auto_set records those writes)
+        self._auto_set = {}
+        if text_precision == "auto" and os.environ.get("MMF_TEXT_HILO"):
+            self.text_precision = "pinned"
+        else:
+            self._auto_write("text_hilo", self.TEXT_PRECISIONS[text_precision])
+        if effnet_precision == "auto" and os.environ.get("MMF_EFFNET_FP32"):
+            self.effnet_precision = "pinned"
+        elif effnet_precision == "auto":
+            self._auto_set["effnet_fp32"] = self.get_option("effnet_fp32")
         self.clip_stream_check = None
         self.vault_n = 0
         if detector_state is not None:
@@ -146,6 +157,14 @@ class Engine:
     # the calibration images (half the north-star bar; the ordinary draw measures ~1e-4 over 256)
     EFFNET_TOL = 5e-4
 
+    def _auto_write(self, name: str, value: int) -> None:
+        self.set_option(name, value)
+        self._auto_set[name] = int(value)
+
+    def _pinned(self, name: str) -> bool:
+        """True when the option was changed since the engine last wrote it (a user pin)."""
+        return name in self._auto_set and self.get_option(name) != self._auto_set[name]
+
     def calibrate(self, components=("effnet",)) -> None:
         """Load-time precision selection for re-packed components (called at construction and by
         the detector's sync after every re-pack: trained weights reach the engine through
@@ -159,19 +178,37 @@ class Engine:
     # precise mode on the calibration texts (half the north-star bar)
     TEXT_TOL = 5e-4
 
+    # precise-mode GEMM kinds (option text_prec_mask bits: QKV, out-proj, FFN-1, FFN-2) and their
+    # relative GEMM cost in the mode (a bit set: 3x the K loop): the calibration keeps the cheapest
+    # mask within TEXT_TOL of the full mode
+    PREC_KIND_COST = (3, 1, 4, 4)
+
+    @classmethod
+    def _mask_cost(cls, m: int) -> int:
+        return sum(c * (3 if m >> k & 1 else 1) for k, c in enumerate(cls.PREC_KIND_COST))
+
     def check_text_precision(self, n: int = 64) -> dict:
-        """Load-time selection of the RoBERTa precise mode.  The fp16-operand
-        design holds 1e-3 only while the LayerNorms do not amplify operand rounding: a checkpoint
-        with one channel dominating every LayerNorm (gamma ~7: DESIGN.md §4) moves the scores by
-        1.6e-3 even on the split stream.  With text_precision "auto" the fast layout (fp16 or split
-        stream, from the LayerNorm bound) and the precise mode (~22-bit GEMM operands, fp32 stream,
-        LayerNorm and attention) run on n seeded texts of 128 tokens; if any score is non-finite or
-        moves by more than TEXT_TOL, the precise mode stays selected (option text_hilo = 2)."""
+        """Load-time selection of the RoBERTa text mode.  The
+        fp16-operand design holds 1e-3 only while the LayerNorms do not amplify operand rounding: a
+        checkpoint with one channel dominating every LayerNorm (gamma ~7: DESIGN.md §4) moves the
+        scores by 1.6e-3 even on the split stream.  With text_precision "auto", on n seeded texts of
+        128 tokens:
+          1. the fast layout (fp16 or split stream, from the LayerNorm bound) against the full
+             precise mode (fp32 stream / LayerNorm / attention, every GEMM on ~22-bit hi / lo
+             operands); within TEXT_TOL on every score -> the fast layout, and the precise weights
+             are released (the run-time trap falls back to the precise mode on fp16 operands,
+             which needs none of them);
+          2. otherwise every cheaper operand mask (option text_prec_mask: which GEMM kinds read hi / lo
+             operands, the rest fp16) against the full mode; the cheapest within TEXT_TOL is
+             selected and only its kinds' weights stay packed.
+        A user pin (text_precision other than "auto", MMF_TEXT_HILO, or a set_option of text_hilo
+        after the engine's last write) is left alone."""
         from . import synthetic as syn
-        if self.text_precision != "auto":
-            self.text_check = {"mode": self.text_precision, "calibrated": False}
+        if self.text_precision != "auto" or self._pinned("text_hilo"):
+            self.text_check = {"mode": self.text_precision if self.text_precision != "auto" else "pinned",
+                               "calibrated": False}
             return self.text_check
-        self.set_option("text_hilo", -1)
+        self._auto_write("text_hilo", -1)
         n = max(1, n)
         L = min(128, self.max_text_len)
         ids, mask = syn.roberta_ids(n, L, 6007, [L, L // 2, 17, 5])
@@ -179,19 +216,81 @@ class Engine:
         def scores():
             return torch.cat([self.text_forward(ids[i:i + self.max_batch], mask[i:i + self.max_batch])[2].double()
                               for i in range(0, n, self.max_batch)])
+
+        def dist(a, b):
+            return float((a - b).abs().max()) if bool(torch.isfinite(a).all()) else float("inf")
+        names = {0: "fp16", 1: "split", 2: "precise"}
         fast = scores()
         fast_mode = self.get_option("text_hilo_effective")
-        self.set_option("text_hilo", 2)
-        prec = scores()
-        finite = bool(torch.isfinite(fast).all())
-        d = float((fast - prec).abs().max()) if finite else float("inf")
-        ok = finite and d <= self.TEXT_TOL
-        if ok:
-            self.set_option("text_hilo", -1)
-        names = {0: "fp16", 1: "split", 2: "precise"}
-        self.text_check = {"max_dscore": d, "fast_layout": names[fast_mode], "mode": names[fast_mode] if ok else "precise",
-                           "texts": n, "calibrated": True}
+        packed = self.get_option("text_precise_packed")
+        if packed != 15:  # (weights packed under a pinned layout: nothing to compare against)
+            self.text_check = {"mode": names[fast_mode], "calibrated": False, "precise_packed": packed}
+            return self.text_check
+        self.set_option("text_prec_mask", 15)
+        self._auto_write("text_hilo", 2)
+        full = scores()
+        d = dist(fast, full)
+        self.text_check = {"max_dscore": d, "fast_layout": names[fast_mode], "texts": n, "calibrated": True}
+        if d <= self.TEXT_TOL:
+            self._auto_write("text_hilo", -1)
+            self.set_option("text_precise_packed", 0)  # the +510 MB go when the mode is not used
+            self.text_check["mode"] = names[fast_mode]
+            return self.text_check
+        tried = {}
+        best = 15
+        for m in sorted(range(15), key=self._mask_cost):
+            self.set_option("text_prec_mask", m)
+            tried[m] = dist(scores(), full)
+            if tried[m] <= self.TEXT_TOL:
+                best = m
+                break
+        self.set_option("text_prec_mask", best)
+        self.set_option("text_precise_packed", best)
+        self.text_check.update(mode="precise", prec_mask=best, mask_dscore=tried,
+                               cost_vs_full=self._mask_cost(best) / self._mask_cost(15))
         return self.text_check
+
+    def text_overflow(self, scores) -> bool:
+        """Run-time overflow trap of the fast RoBERTa layouts (the counterpart of
+        clip_stream_overflow).  The load-time calibration bounds the drift on its seeded texts; an
+        input whose branch output passes fp16's range (a token driving an FFN-2 row past 65504) turns
+        that text's scores non-finite.  Given text scores the caller already read back: if a fast
+        layout is selected and any is non-finite, the engine switches to the precise mode for good
+        (fp32 stream and branch outputs; hi / lo operands for the kinds still packed, fp16 for the
+        rest) and returns True, and the caller re-runs the batch.  A pinned layout is left alone."""
+        if self.get_option("text_hilo_effective") >= 2 or self._pinned("text_hilo"):
+            return False
+        if bool(np.isfinite(np.asarray(scores)).all()):
+            return False
+        self.set_option("text_prec_mask", self.get_option("text_precise_packed"))
+        self._auto_write("text_hilo", 2)
+        self.text_check = dict(self.text_check or {}, mode="precise", runtime_overflow=True,
+                               prec_mask=self.get_option("text_prec_mask"))
+        return True
+
+    def effnet_overflow(self, scores) -> bool:
+        """Run-time overflow trap of the fp16 EfficientNet tower: given
+        deepfake scores the caller already read back, a non-finite one under the fp16 tower switches
+        the engine to the fp32 tower for good and returns True (the caller re-runs the batch).  An
+        image whose activation passes fp16's range (a saturated colour on a high-gain stem channel)
+        is what the load-time calibration on seeded images cannot see.  A pinned tower is left
+        alone."""
+        if self.get_option("effnet_fp32") != 0 or self.effnet_precision != "auto" or self._pinned("effnet_fp32"):
+            return False
+        if bool(np.isfinite(np.asarray(scores)).all()):
+            return False
+        self._auto_write("effnet_fp32", 1)
+        self.effnet_check = dict(self.effnet_check or {}, tower="fp32", runtime_overflow=True)
+        return True
+
+    def scores_overflow(self, scores5) -> bool:
+        """All three run-time traps on an analyze_batch result read back to the host ([B, 5]: ai,
+        misinfo, deepfake, clip_similarity, vault): True when any tower switched precision (the
+        caller re-runs the batch once)."""
+        s = np.asarray(scores5)
+        hit = self.text_overflow(s[:, :2])
+        hit = self.effnet_overflow(s[:, 2]) or hit
+        return self.clip_stream_overflow(s[:, 3]) or hit
 
     def check_effnet_precision(self, n: int = 64) -> dict:
         """Load-time guard of the fp16 EfficientNet tower (the counterpart of
@@ -201,15 +300,17 @@ class Engine:
         is non-finite or moves by more than EFFNET_TOL, the fp32 tower stays selected.  "fp16" /
         "fp32" pin the tower without measuring.  Returns (and keeps as `effnet_check`) the result."""
         from . import synthetic as syn
-        if self.effnet_precision != "auto":
-            self.set_option("effnet_fp32", int(self.effnet_precision == "fp32"))
-            self.effnet_check = {"tower": self.effnet_precision, "calibrated": False}
+        if self.effnet_precision != "auto" or self._pinned("effnet_fp32"):
+            if self.effnet_precision in ("fp16", "fp32"):
+                self.set_option("effnet_fp32", int(self.effnet_precision == "fp32"))
+            self.effnet_check = {"tower": self.effnet_precision if self.effnet_precision != "auto" else "pinned",
+                                 "calibrated": False}
             return self.effnet_check
         n = max(1, n)
         imgs = torch.from_numpy(syn.images(n, 5003)).to(self.device)
 
         def scores(fp32: int):
-            self.set_option("effnet_fp32", fp32)
+            self._auto_write("effnet_fp32", fp32)
             out = []
             for i in range(0, n, self.max_batch):
                 out.append(self.effnet_forward(imgs[i:i + self.max_batch])[1].double())
@@ -218,7 +319,7 @@ class Engine:
         finite = bool(torch.isfinite(s16).all())
         d = float((s16 - s32).abs().max()) if finite else float("inf")
         ok = finite and d <= self.EFFNET_TOL
-        self.set_option("effnet_fp32", 0 if ok else 1)
+        self._auto_write("effnet_fp32", 0 if ok else 1)
         self.effnet_check = {"max_ddeepfake": d, "tower": "fp16" if ok else "fp32", "images": n, "calibrated": True}
         return self.effnet_check
 

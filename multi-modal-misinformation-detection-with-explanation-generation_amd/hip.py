@@ -51,6 +51,7 @@ SIGNATURES = {
     "mmf_profile_kind_name": (ctypes.c_char_p, [_I]),
     "mmf_set_option": (_I, [_P, ctypes.c_char_p, _I]),
     "mmf_get_option": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_I)]),
+    "mmf_option_name": (ctypes.c_char_p, [_I]),
     "mmf_device_bytes": (ctypes.c_int64, [_P]),
     "mmf_gemm_f16": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "mmf_gemm_f16_ex": (_I, [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P]),

@@ -55,3 +55,32 @@ def test_resize_tap_budget_host_only():
     assert lib.mmf_resize_supported(10528, 200) == 1   # squash: scale 47 -> 95 taps
     assert lib.mmf_resize_supported(10529, 200) == 0
     assert lib.mmf_resize_supported(0, 10) == 0
+
+
+def test_header_options_match_library():
+    """include/mmf_hip.h lists exactly the library's run-time options
+    (mmf_option_name enumerates kOptNames), and every listed name round-trips through the process
+    defaults (mmf_get_option / mmf_set_option with a NULL handle: no device call)."""
+    import re
+    import mmf_amd.hip as hip
+    text = open(HEADER).read()
+    block = text[text.index("/* Run-time options."):text.index("const char* mmf_option_name(int i);")]
+    listed = re.findall(r'^ \*   "(\w+)"\s+(-?\d+):', block, flags=re.M)
+    assert listed, "no option list in the header"
+    lib = hip.load()
+    names = []
+    while True:
+        n = lib.mmf_option_name(len(names))
+        if n is None:
+            break
+        names.append(n.decode())
+    assert sorted(n for n, _ in listed) == sorted(names)
+    for name, default in listed:
+        v = hip.get_process_option(name)
+        env = "MMF_" + name.upper()
+        if env not in os.environ:
+            assert v == int(default), (name, v, default)
+        hip.set_process_option(name, v)  # round trip
+        assert hip.get_process_option(name) == v
+    with pytest.raises(hip.MMFError):
+        hip.get_process_option("gemm_prio")  # removed in round 5: rejected

@@ -178,11 +178,13 @@ def _ln_bound(det, xhat):
                for k, v in det.items() if k.startswith("roberta") and k.endswith("LayerNorm.weight"))
 
 
-@pytest.mark.parametrize("gamma_out", [3.5, 5.0])
-def test_dominating_gamma_channel_selects_split_stream(det_sd, clip_sd, gamma_out):
-    """The sound bound |beta| + sqrt(767) |gamma| selects the split hi + lo stream on a draw whose
-    post-LN stream is ~82 / ~113 in one dominating channel with beta ~ 0 (the round-3 bound, 17 / 24,
-    did not), and the full-size scores and probabilities stay within 1e-3 of the oracle.  (At
+@pytest.mark.parametrize("gamma_out,mode", [(3.5, "split"), (5.0, "precise")])
+def test_dominating_gamma_channel_calibration(det_sd, clip_sd, gamma_out, mode):
+    """The sound bound |beta| + sqrt(767) |gamma| selects the split hi + lo stream as the fast layout
+    on a draw whose post-LN stream is ~82 / ~113 in one dominating channel with beta ~ 0 (the
+    round-3 bound, 17 / 24, did not); the calibration then keeps it at gamma 3.5 (2.9e-4 from the
+    precise mode) and selects the precise mode at gamma 5 (6.9e-4, round 5), and the full-size
+    scores and probabilities stay within 1e-3 of the oracle (the exact mode is asserted).  (At
     gamma 7 -- stream ~151 -- the split stream measured 1.6e-3 / 1.1e-3 and fp16-only 2.7e-3 / 3.6e-3:
     that draw amplifies the fp16 rounding of the GEMM operands themselves -- the oracle with only its
     encoder weights rounded to fp16 moves by 5e-4 there, 3e-5 on the plain draw -- which no stream
@@ -199,7 +201,8 @@ def test_dominating_gamma_channel_selects_split_stream(det_sd, clip_sd, gamma_ou
     eng = Engine(0, det, clip_sd, max_batch=Bf)
     print(f"RoBERTa calibration: {eng.text_check}")
     assert eng.text_check["fast_layout"] == "split"  # the bound alone already leaves the fp16-only stream
-    assert eng.get_option("text_hilo_effective") in (1, 2)
+    assert eng.text_check["mode"] == mode
+    assert eng.get_option("text_hilo_effective") == {"split": 1, "precise": 2}[mode]
     rid, rm = syn.roberta_ids(Bf, 128, 1234)
     cid, cm = syn.clip_ids(Bf, 77, 1234)
     imgs = syn.images(Bf, 1234)
@@ -300,6 +303,10 @@ def test_gamma7_draw_selects_precise_mode(det_sd, clip_sd):
     eng = Engine(0, det, clip_sd, max_batch=Bf)
     print(f"RoBERTa calibration (gamma 7): {eng.text_check}")
     assert eng.text_check["mode"] == "precise" and eng.get_option("text_hilo_effective") == 2
+    # round 6: the calibration keeps only the GEMM kinds that need hi / lo operands (the rest read
+    # fp16 operands; their precise weights are released)
+    m = eng.text_check["prec_mask"]
+    assert eng.get_option("text_prec_mask") == m and eng.get_option("text_precise_packed") == m
     rid, rm = syn.roberta_ids(Bf, 128, 1234)
     cid, cm = syn.clip_ids(Bf, 77, 1234)
     imgs = syn.images(Bf, 1234)

@@ -83,6 +83,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="auto,3,5,10,11")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds over the configs (median reported)")
     ap.add_argument("--kscale", default="", help="comma list of K multipliers to time (fixed-cost probe)")
     ap.add_argument("--effnet", action="store_true", help="time the EfficientNet 1x1 convolutions instead")
     ap.add_argument("--round", action="store_true", help="one 256-tile round at K = 256 .. 6144")
@@ -121,9 +122,14 @@ def main():
         vals = a.group_m or a.vals
         for v in [""] + [x for x in vals.split(",") if x]:
             hip.set_process_option(opt, int(v or 0))
+            samples = {}
+            for _ in range(a.rounds):
+                for cfg in a.configs.split(","):
+                    force(cfg)
+                    samples.setdefault(cfg, []).append(timed_us(call, a.iters))
             for cfg in a.configs.split(","):
                 force(cfg)
-                us = timed_us(call, a.iters)
+                us = sorted(samples[cfg])[len(samples[cfg]) // 2]
                 row[(f"{opt}={v}:" if v else "") + cfg] = round(2.0 * M * N * K / (us / 1e6) / 1e12, 1)
                 if a.no_store:
                     us0 = timed_us(lambda: call(False), a.iters)

@@ -1,4 +1,4 @@
-"""Round-5 A/B timings on one GPU (interleaved rounds, HIP-event / wall timing of whole calls):
+"""Tower A/B timings on one GPU (interleaved rounds, HIP-event / wall timing of whole calls):
 
 * CLIP towers (BASELINE configs[3], B = 256): both towers on concurrent streams (the production
   mmf_clip_consistency), serialised on one stream (option concurrent = 0), and each tower alone --
@@ -9,7 +9,7 @@
 * EfficientNet (configs[2], B = 512) fp16 and fp32 towers;
 * the engine's construction (weight packing + load-time calibration).
 
-    python tools/r05_ab.py [--rounds 5] [--steps 10]
+    python tools/tower_ab.py [--rounds 5] [--steps 10]
 """
 import argparse
 import json
