@@ -377,8 +377,12 @@ def main():
     B = a.batch
     benchrun.progress(f"rank {rank}/{world}: building the engine on cuda:{local}")
     det = W.synthetic_detector_state(0)
+    t_build = time.perf_counter()
     eng = Engine(local, det, W.synthetic_clip_state(0), max_batch=B)
+    t_build = time.perf_counter() - t_build  # weight packing + load-time calibrations
     t = build_inputs(eng, B, rank)
+    # each rank's engine build (N engines packing and calibrating side by side)
+    build_s = benchrun.gather_per_rank(t_build, world, rank, dist, tdev)
     sync = torch.cuda.synchronize
 
     benchrun.progress("timed region: PCIe-inclusive (headline)")
@@ -422,6 +426,7 @@ def main():
             a, world, B, dt, value,
             "synthetic (seeded token ids, structured uint8 images, 2170-row vault); random-init weights",
             config_extra=dict({"h2d_bytes_per_step_per_gpu": h2d,
+                               "engine_build_s_per_rank": [round(x, 2) for x in build_s],
                                "timing_collective": (f"{'rccl' if backend == 'nccl' else backend}: barrier + "
                                                      f"all_reduce(MAX) over {world} rank(s)" if dist else None)},
                               **({"rehearsal": f"{world} ranks sharing {torch.cuda.device_count()} GPU(s) over gloo "

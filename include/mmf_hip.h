@@ -240,8 +240,9 @@ const char* mmf_profile_kind_name(int kind);
  *                       otherwise), 0 fp16, 1 fp16 hi + lo, 2 precise mode (fp32 stream, LayerNorm,
  *                       attention and branch outputs; GEMM operands per "text_prec_mask").  2 needs
  *                       the precise weights (packed unless the layout was pinned to 0 / 1 at load)
- *   "text_prec_mask" 15: precise mode: GEMM kinds on ~22-bit K-concatenated hi / lo operands (bit 1
- *                       QKV, 2 out-proj, 4 FFN-1, 8 FFN-2); the other kinds read fp16 operands
+ *   "text_prec_mask" 255: precise mode operands per GEMM kind k (0 QKV, 1 out-proj, 2 FFN-1, 3 FFN-2):
+ *                       bit k = hi / lo activations ([A_hi | A_lo] x [W_hi | W_hi], K = 2 in), bit
+ *                       k + 4 = also W_lo (+ A_hi x W_lo, K = 3 in: ~22-bit operands); neither = fp16
  *   "effnet_fp32"    0: 1 = EfficientNet tower with fp32 activations, fp32-MFMA 1x1 convs and
  *                       precise SiLU (checkpoints whose logits amplify fp16 storage rounding)
  *   "clip_res16"     1: CLIP pre-LN residual streams in fp16 (0: fp32)
@@ -260,7 +261,8 @@ const char* mmf_profile_kind_name(int kind);
  * The defaults are the measured best; with them a row's results do not depend on the
  * batch it runs in (tests/test_gpu_parity.py).  Read-only names for mmf_get_option with a handle:
  * "text_hilo_effective" (the RoBERTa layout in use) and "text_precise_packed" (bitmask of the GEMM
- * kinds whose precise-mode weights are packed, as "text_prec_mask"). */
+ * kinds whose precise-mode weights are packed, bits 0-3 as "text_prec_mask"; setting it to a subset
+ * releases the others' weights). */
 const char* mmf_option_name(int i); /* i-th option name, NULL past the end */
 int mmf_set_option(mmf_handle* h, const char* name, int value);
 int mmf_get_option(mmf_handle* h, const char* name, int* value);

@@ -154,6 +154,16 @@ def max_over_ranks(x: float, dist=None, device: Optional[torch.device] = None) -
     return float(t.item())
 
 
+def gather_per_rank(x: float, world: int, rank: int, dist=None, device: Optional[torch.device] = None) -> list:
+    """[x of rank 0, x of rank 1, ...] on every rank (a SUM all-reduce of one-hot slots)."""
+    if not dist:
+        return [x]
+    t = torch.zeros(world, dtype=torch.float64, device=device)
+    t[rank] = x
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.cpu()]
+
+
 def whole_job_rate(world: int, units_per_rank_step: int, steps: int, seconds: float) -> float:
     """Units all ranks processed / whole-job time (weak scaling: per-rank work fixed)."""
     return world * units_per_rank_step * steps / seconds

@@ -147,7 +147,8 @@ struct Options {
                         // stages, 1 ping-pong, 3 A-ring; all bit-identical)
   int text_hilo = -1;   // RoBERTa residual stream as fp16 hi + fp16 lo (1), fp16 alone (0), or chosen at
                         // weight-load time from the LayerNorm parameters (-1, default: DESIGN §4); 2 = precise mode
-  int text_prec_mask = 15;  // precise mode: GEMM kinds on hi / lo operands (1 QKV, 2 out-proj, 4 FFN-1, 8 FFN-2)
+  int text_prec_mask = 255;  // precise mode: bits 0-3 = GEMM kinds on hi / lo activations (1 QKV, 2 out-proj,
+                             // 4 FFN-1, 8 FFN-2), bits 4-7 = the same kinds also on W_lo (3 products)
   int effnet_fp32 = 0;  // EfficientNet tower with fp32 activations (effnet_f32.hip) instead of fp16
   int clip_res16 = 1;   // CLIP pre-LN residual streams in fp16 (1, default) or fp32 (0)
   int lazy_ln = 1;      // CLIP encoder LayerNorms folded into the GEMM epilogues (gemm.hip)
@@ -927,7 +928,8 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
                      float* scores, int score_stride, hipStream_t s) {
   Workspace& w = h->ws;
   const int M = B * L;
-  const int pm = h->opt.text_prec_mask & 15;
+  const int pm = h->opt.text_prec_mask & 15;  // kinds on hi / lo activations: [A_hi | A_lo] x [W_hi | W_hi] (K = 2 in)
+  const int pw = pm & (h->opt.text_prec_mask >> 4);  // ... of them also on W_lo: + A_hi x W_lo (K = 3 in)
   if (pm & ~h->r_precise)
     return fail(MMF_EINVAL, "text_hilo = 2: text_prec_mask %d needs precise-mode weights that are not packed (packed: %d; "
                             "re-load the text model with text_hilo -1 or 2)", pm, h->r_precise);
@@ -944,7 +946,10 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
   // products, fp32 accumulation and output.  split3 writes the lo / second hi thirds only for a
   // consumer that reads them.
   auto lin = [&](const f16_t* A, int lda, const Lin16& fast, const Lin16& prec, int kind) {
-    return (pm >> kind & 1) ? gemm_args(A, lda, prec, M) : gemm_args(A, lda, fast, M);
+    if (!(pm >> kind & 1)) return gemm_args(A, lda, fast, M);
+    GemmArgs g = gemm_args(A, lda, prec, M);
+    if (!(pw >> kind & 1)) g.K = 2 * fast.in;  // the first two thirds of the concatenated rows
+    return g;
   };
   HIPCHK(launch_split3(x, 768, w.s3, M, 768, s, pm & 1));
   for (int i = 0; i < 12; ++i) {

@@ -686,7 +686,7 @@ static bool glds_ok(const GemmArgs& a) {
 // 256x192 tile: DESIGN.md §3 records each measurement and its last commit).
 static bool config_exists(int c) {
   return c == 0 || c == 1 || c == 2 || c == 3 || c == 5 || c == 9 || c == 10 || c == 11 || c == 12 || c == 13 ||
-         c == 14 || c == 17 || c == 18 ||
+         c == 14 || c == 17 ||
          (MMF_GEMM_DIAG && (c == 15 || c == 16));
 }
 
@@ -696,7 +696,7 @@ static int forced_config(const GemmArgs& a) {
   const int c = a.force_cfg - 1;
   if (!config_exists(c)) return -1;
   if ((c == 5 || c >= 10) && !glds_ok(a)) return -1;
-  if ((c == 14 || c == 17 || c == 18) && a.epi != 0) return -1;
+  if ((c == 14 || c == 17) && a.epi != 0) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
   return c;
 }
@@ -719,10 +719,10 @@ static int glds_pick(const GemmArgs& a, bool with_128) {
 }
 
 // the K-loop variant of a persistent pick (option gemm_kloop): 1 ping-pong 10 -> 12, 11 -> 13;
-// 3 A-ring 10 -> 17, 11 -> 18
+// 3 A-ring 10 -> 17 (256 x 192 only: three 256-row A slots and two W slots of 256 rows fill all 160 KB)
 static int pp_of(const GemmArgs& a, int c) {
   if (a.kloop == 1) return c == 10 ? 12 : c == 11 ? 13 : c;
-  if (a.kloop == 3) return c == 10 ? 17 : c == 11 ? 18 : c;
+  if (a.kloop == 3) return c == 10 ? 17 : c;
   return c;
 }
 
@@ -774,7 +774,7 @@ const char* gemm_config_name(int c) {
       "gemm_glds<256,128,4,2>", "(removed)", "(removed)", "(removed)", "pw_conv", "gemm_glds_pipe2<256,192,4,2>",
       "gemm_glds_pipe2<256,256,2,4>", "gemm_glds_pp<256,192,4,2>", "gemm_glds_pp<256,256,2,4>",
       "gemm_glds_pp1<256,192,4,2>", "gemm_glds_dma_only",
-      "gemm_glds_compute_only", "gemm_glds_aring<256,192,4,2>", "gemm_glds_aring<256,256,2,4>"};
+      "gemm_glds_compute_only", "gemm_glds_aring<256,192,4,2>", "(removed)"};
   return (c >= 0 && c < kGemmConfigs) ? names[c] : "gemm_f16<?>";
 }
 
@@ -813,7 +813,6 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
     case 13: return run_glds<256, 256, 2, 4, true, 0, 1>(a, s);
     case 14: return run_glds<256, 192, 4, 2, true, 0, 2>(a, s);
     case 17: return run_glds<256, 192, 4, 2, true, 0, 3>(a, s);
-    case 18: return run_glds<256, 256, 2, 4, true, 0, 3>(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

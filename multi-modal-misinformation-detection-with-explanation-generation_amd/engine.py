@@ -178,14 +178,23 @@ class Engine:
     # precise mode on the calibration texts (half the north-star bar)
     TEXT_TOL = 5e-4
 
-    # precise-mode GEMM kinds (option text_prec_mask bits: QKV, out-proj, FFN-1, FFN-2) and their
-    # relative GEMM cost in the mode (a bit set: 3x the K loop): the calibration keeps the cheapest
-    # mask within TEXT_TOL of the full mode
+    # precise-mode GEMM kinds (option text_prec_mask: bit k = kind k on hi / lo activations, bit k + 4 =
+    # also on W_lo; kinds QKV, out-proj, FFN-1, FFN-2) and their relative GEMM cost (the K loop is 1x /
+    # 2x / 3x): the calibration keeps the cheapest mask within TEXT_TOL of the full mode (255)
     PREC_KIND_COST = (3, 1, 4, 4)
+    PREC_FULL = 255
 
     @classmethod
     def _mask_cost(cls, m: int) -> int:
-        return sum(c * (3 if m >> k & 1 else 1) for k, c in enumerate(cls.PREC_KIND_COST))
+        return sum(c * (1 + (m >> k & 1) + (m >> k & 1) * (m >> (k + 4) & 1)) for k, c in enumerate(cls.PREC_KIND_COST))
+
+    @classmethod
+    def _prec_masks(cls):
+        """Every operand mask below the full mode, cheapest first (3 levels per kind)."""
+        import itertools
+        ms = [sum((lv >= 1) << k | (lv == 2) << (k + 4) for k, lv in enumerate(lvls))
+              for lvls in itertools.product((0, 1, 2), repeat=4)]
+        return sorted((m for m in ms if m != cls.PREC_FULL), key=lambda m: (cls._mask_cost(m), m))
 
     def check_text_precision(self, n: int = 64) -> dict:
         """Load-time selection of the RoBERTa text mode.  The
@@ -226,7 +235,7 @@ class Engine:
         if packed != 15:  # (weights packed under a pinned layout: nothing to compare against)
             self.text_check = {"mode": names[fast_mode], "calibrated": False, "precise_packed": packed}
             return self.text_check
-        self.set_option("text_prec_mask", 15)
+        self.set_option("text_prec_mask", self.PREC_FULL)
         self._auto_write("text_hilo", 2)
         full = scores()
         d = dist(fast, full)
@@ -237,17 +246,17 @@ class Engine:
             self.text_check["mode"] = names[fast_mode]
             return self.text_check
         tried = {}
-        best = 15
-        for m in sorted(range(15), key=self._mask_cost):
+        best = self.PREC_FULL
+        for m in self._prec_masks():
             self.set_option("text_prec_mask", m)
             tried[m] = dist(scores(), full)
             if tried[m] <= self.TEXT_TOL:
                 best = m
                 break
         self.set_option("text_prec_mask", best)
-        self.set_option("text_precise_packed", best)
+        self.set_option("text_precise_packed", best & 15)
         self.text_check.update(mode="precise", prec_mask=best, mask_dscore=tried,
-                               cost_vs_full=self._mask_cost(best) / self._mask_cost(15))
+                               cost_vs_full=self._mask_cost(best) / self._mask_cost(self.PREC_FULL))
         return self.text_check
 
     def text_overflow(self, scores) -> bool:
@@ -262,7 +271,8 @@ class Engine:
             return False
         if bool(np.isfinite(np.asarray(scores)).all()):
             return False
-        self.set_option("text_prec_mask", self.get_option("text_precise_packed"))
+        packed = self.get_option("text_precise_packed")
+        self.set_option("text_prec_mask", packed | packed << 4)
         self._auto_write("text_hilo", 2)
         self.text_check = dict(self.text_check or {}, mode="precise", runtime_overflow=True,
                                prec_mask=self.get_option("text_prec_mask"))

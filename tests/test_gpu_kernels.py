@@ -91,7 +91,7 @@ def gemm_config(lib):
     hip.set_process_option("gemm_config", -1)
 
 
-@pytest.mark.parametrize("cfg", [3, 5, 10, 11, 12, 13, 14, 17, 18])
+@pytest.mark.parametrize("cfg", [3, 5, 10, 11, 12, 13, 14, 17])
 @pytest.mark.parametrize("M,N,K,act,res", [(1000, 2304, 768, 1, False), (777, 392, 512, 0, True),
                                            (130, 136, 64, 2, False)])
 def test_gemm_forced_configs(lib, gemm_config, cfg, M, N, K, act, res):
@@ -127,7 +127,7 @@ def test_gemm_forced_configs(lib, gemm_config, cfg, M, N, K, act, res):
                                            (777, 392, 512, 1, True), (4096, 3072, 768, 1, False),
                                            (300, 136, 128, 0, True)])
 def test_gemm_pingpong_bit_identical(lib, gemm_config, M, N, K, act, res):
-    """The K-loop variants (ping-pong: configs 12 / 13 / 14; A-ring: 17 / 18; option gemm_kloop) issue
+    """The K-loop variants (ping-pong: configs 12 / 13 / 14; A-ring: 17; option gemm_kloop) issue
     the same MFMAs in the same K order per accumulator and share the epilogue: their outputs equal
     the half-step-pipelined kernels' (10 / 11) bit for bit, on the encoder shapes (several persistent rounds) and ragged
     edges, fp16-only and fp32 + residual epilogues."""
@@ -147,7 +147,7 @@ def test_gemm_pingpong_bit_identical(lib, gemm_config, M, N, K, act, res):
                                     c16.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
         torch.cuda.synchronize()
         return c16, c32
-    for base, pp in ((10, 12), (10, 14), (11, 13), (10, 17), (11, 18)):
+    for base, pp in ((10, 12), (10, 14), (11, 13), (10, 17)):
         r16, r32 = run(base)
         for _ in range(3):
             o16, o32 = run(pp)

@@ -39,20 +39,26 @@ def test_text_signals(engine, golden):
     np.testing.assert_allclose(ai.cpu().numpy(), golden["ai_logits"], atol=5e-3)
 
 
-def test_text_precise_mode_vs_golden(engine, golden):
+@pytest.fixture(scope="module")
+def precise_engine(det_sd, clip_sd, golden_inputs):
+    """The golden draw with text_precision "precise": every GEMM kind's hi / lo weights stay packed
+    (under "auto" the calibration keeps the fp16 stream here and releases them)."""
+    from mmf_amd.engine import Engine
+    eng = Engine(0, det_sd, clip_sd, eos_token_id=golden_inputs["eos"], max_batch=8, text_precision="precise")
+    yield eng
+    eng.close()
+
+
+def test_text_precise_mode_vs_golden(precise_engine, golden):
     """RoBERTa precise mode (option text_hilo = 2, precise.hip: ~22-bit GEMM operands through the
     K-concatenated [hi | lo | hi] x [W_hi | W_hi | W_lo] product, fp32 stream / LayerNorm /
     attention) against the reference-run logits: fp32-level agreement, far inside the fp16 modes'
     bar; batch 1 too (the skinny split-K path at K = 2304 / 9216)."""
-    mode = engine.get_option("text_hilo")
-    try:
-        engine.set_option("text_hilo", 2)
-        assert engine.get_option("text_hilo_effective") == 2
-        ai, mi, sc = engine.text_forward(golden["rob_ids"], golden["rob_mask"])
-        ai1, _, sc1 = engine.text_forward(golden["rob_ids"][:1], golden["rob_mask"][:1])
-        torch.cuda.synchronize()
-    finally:
-        engine.set_option("text_hilo", mode)
+    engine = precise_engine
+    assert engine.get_option("text_hilo_effective") == 2 and engine.get_option("text_prec_mask") == 255
+    ai, mi, sc = engine.text_forward(golden["rob_ids"], golden["rob_mask"])
+    ai1, _, sc1 = engine.text_forward(golden["rob_ids"][:1], golden["rob_mask"][:1])
+    torch.cuda.synchronize()
     sc = sc.cpu().numpy()
     da = np.abs(ai.cpu().numpy() - golden["ai_logits"]).max()
     dm = np.abs(mi.cpu().numpy() - golden["misinfo_logits"]).max()
