@@ -233,8 +233,6 @@ const char* mmf_profile_kind_name(int kind);
  *   "gemm_splitk"    1: split-K on the skinny-M (M <= 512) GEMM path
  *   "gemm_config"   -1: automatic GEMM tile choice; c >= 0 forces instantiation c (A/B tools)
  *   "gemm_group_m"   0: persistent GEMM tile order (g > 0: grouped by g row panels)
- *   "gemm_kloop"     0: K-loop schedule of the persistent plain / producer GEMMs (0 two LDS stages,
- *                       1 ping-pong SIMD partners, 3 A-operand ring of three slots; bit-identical)
  *   "text_hilo"     -1: RoBERTa stream layout: -1 chosen at weight-load time from the LayerNorm
  *                       bound (fp16 hi + lo if max_c |beta_c| + sqrt(767) |gamma_c| > 64, fp16 alone
  *                       otherwise), 0 fp16, 1 fp16 hi + lo, 2 precise mode (fp32 stream, LayerNorm,

@@ -143,8 +143,6 @@ struct Options {
   int gemm_splitk = 1;  // split-K on the skinny-M GEMM path
   int gemm_config = -1; // forced GEMM instantiation (-1 = automatic)
   int gemm_group_m = 0; // persistent GEMM tile order
-  int gemm_kloop = 0;   // K-loop variant of the persistent plain / producer GEMMs (gemm_glds_body.inc KL: 0 two
-                        // stages, 1 ping-pong, 3 A-ring; all bit-identical)
   int text_hilo = -1;   // RoBERTa residual stream as fp16 hi + fp16 lo (1), fp16 alone (0), or chosen at
                         // weight-load time from the LayerNorm parameters (-1, default: DESIGN §4); 2 = precise mode
   int text_prec_mask = 255;  // precise mode: bits 0-3 = GEMM kinds on hi / lo activations (1 QKV, 2 out-proj,
@@ -166,7 +164,8 @@ struct Options {
   int after_text = 12;  // towers of the concurrent B > mt_enqueue step that start only once RoBERTa is done
                         // (bitmask as diag_skip: 2 EfficientNet, 4 CLIP text, 8 ViT)
 };
-// (Round 5 removed the options whose variants were measured slower and stayed off: gemm_ring, gemm_wide,
+// (Round 6 measured and removed gemm_kloop -- ping-pong and A-ring K loops; round 5 removed
+// the options whose variants were measured slower and stayed off: gemm_ring, gemm_wide,
 // gemm_w4, dw_v2, dw_persist, ln_prod256, cu_split, fuse_expand32, qkv_attn_gm, splitk_fix, gemm_tq,
 // se_group, splitk_min_k, and pinned gemm_prio = 2 / dw_ct = 1; DESIGN.md §3 keeps each measurement.)
 struct OptName { const char* name; int Options::*field; const char* env; };
@@ -174,7 +173,7 @@ const OptName kOptNames[] = {
     {"concurrent", &Options::concurrent, "MMF_CONCURRENT"},   {"fuse_stem", &Options::fuse_stem, "MMF_FUSE_STEM"},
     {"fuse_expand", &Options::fuse_expand, "MMF_FUSE_EXPAND"},
     {"gemm_splitk", &Options::gemm_splitk, "MMF_GEMM_SPLITK"}, {"gemm_config", &Options::gemm_config, "MMF_GEMM_CONFIG"},
-    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"}, {"gemm_kloop", &Options::gemm_kloop, "MMF_GEMM_KLOOP"},
+    {"gemm_group_m", &Options::gemm_group_m, "MMF_GEMM_GROUPM"},
     {"text_hilo", &Options::text_hilo, "MMF_TEXT_HILO"}, {"text_prec_mask", &Options::text_prec_mask, "MMF_TEXT_PREC_MASK"},
     {"effnet_fp32", &Options::effnet_fp32, "MMF_EFFNET_FP32"},
     {"clip_res16", &Options::clip_res16, "MMF_CLIP_RES16"}, {"lazy_ln", &Options::lazy_ln, "MMF_LAZY_LN"},
@@ -200,7 +199,6 @@ void apply_options(const Options& o, GemmArgs* g) {
   g->force_cfg = o.gemm_config >= 0 ? o.gemm_config + 1 : 0;
   g->no_splitk = o.gemm_splitk ? 0 : 1;
   g->group_m = o.gemm_group_m;
-  g->kloop = o.gemm_kloop;
 }
 
 // Device allocations are owned per group so that re-loading one component (or the vault, or the

@@ -416,7 +416,7 @@ MMF_DEV void attention_epilogue(const GemmArgs& g, const f32x4 (&acc)[NI][MI], c
       }
       sum += __shfl_xor(sum, 16, 64);
       sum += __shfl_xor(sum, 32, 64);
-      inv[it] = sum == 0.f ? 0.f : 1.0f / sum;
+      inv[it] = sum == 0.f ? 0.f : 1.0f / sum;  // (a non-finite sum propagates: norm.hip overflow sentinel)
     }
     f32x4 o[NQ][4];
 #pragma unroll
@@ -503,8 +503,7 @@ MMF_DEV unsigned long long gst_time() {
 
 // DBG (measurement builds, forced configs 15 / 16 only; outputs garbage): 1 = LDS-DMA + barriers only,
 // 2 = fragment reads + MFMAs + barriers only
-// KL: K-loop schedule (gemm_glds_body.inc: 0 two stages, 1 / 2 ping-pong, 3 A-ring; EPI 0 / 2 only)
-template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0, int KL = 0>
+template <int BM, int BN, int WGM, int WGN, int ACT, bool PIPE2 = false, int EPI = 0, int DBG = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g, int tilesN, int tiles, int tilesM,
                                                                        int gm) {
 #define MMF_GLDS_FIRST_TILE wgid
@@ -513,7 +512,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_glds_kernel(GemmArgs g
 }
 
 // persistent grid: one workgroup per CU (256 CUs), fewer when the launch has fewer tiles
-template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false, int DBG = 0, int KL = 0>
+template <int BM, int BN, int WGM, int WGN, bool PIPE2 = false, int DBG = 0>
 hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM, tilesN = (a.N + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
@@ -522,7 +521,7 @@ hipError_t run_glds(const GemmArgs& a, hipStream_t s) {
   const int gm = a.group_m;  // tile-order option (handle option "gemm_group_m"; 0 = row-major)
 #define MMF_GLDS_CASE(ACT)                                                                                  \
   case ACT:                                                                                                 \
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG, KL>), dim3(grid), blk, 0, s, a, tilesN, tiles, \
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT, PIPE2, 0, DBG>), dim3(grid), blk, 0, s, a, tilesN, tiles, \
                        tilesM, gm);                                                                          \
     break;
   if constexpr (DBG != 0) {
@@ -564,16 +563,7 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
   } else if (a.act != ACT_NONE || BN != 192) {
     return hipErrorInvalidValue;
   } else if (a.epi == 2) {
-    if constexpr (BN == 192) {
-      if (a.kloop == 1)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT_NONE, true, 2, 0, 1>), dim3(grid), blk, 0, s, a,
-                           tilesN, tiles, tilesM, gm);
-      else if (a.kloop == 3)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WGM, WGN, ACT_NONE, true, 2, 0, 3>), dim3(grid), blk, 0, s, a,
-                           tilesN, tiles, tilesM, gm);
-      else
-        MMF_EPI_CASE(2, ACT_NONE);
-    }
+    if constexpr (BN == 192) MMF_EPI_CASE(2, ACT_NONE);
   } else if (a.epi == 3) {
     if constexpr (BN == 192) MMF_EPI_CASE(3, ACT_NONE);
   } else {
@@ -685,8 +675,7 @@ static bool glds_ok(const GemmArgs& a) {
 // and removed in round 5 -- 128-row and 256x384 tiles, the ring / loader-consumer kernels, the 4-wave
 // 256x192 tile: DESIGN.md §3 records each measurement and its last commit).
 static bool config_exists(int c) {
-  return c == 0 || c == 1 || c == 2 || c == 3 || c == 5 || c == 9 || c == 10 || c == 11 || c == 12 || c == 13 ||
-         c == 14 || c == 17 ||
+  return c == 0 || c == 1 || c == 2 || c == 3 || c == 5 || c == 9 || c == 10 || c == 11 ||
          (MMF_GEMM_DIAG && (c == 15 || c == 16));
 }
 
@@ -696,7 +685,6 @@ static int forced_config(const GemmArgs& a) {
   const int c = a.force_cfg - 1;
   if (!config_exists(c)) return -1;
   if ((c == 5 || c >= 10) && !glds_ok(a)) return -1;
-  if ((c == 14 || c == 17) && a.epi != 0) return -1;
   if (c == 9 && !pw_applicable(a)) return -1;
   return c;
 }
@@ -718,19 +706,10 @@ static int glds_pick(const GemmArgs& a, bool with_128) {
   return best;
 }
 
-// the K-loop variant of a persistent pick (option gemm_kloop): 1 ping-pong 10 -> 12, 11 -> 13;
-// 3 A-ring 10 -> 17 (256 x 192 only: three 256-row A slots and two W slots of 256 rows fill all 160 KB)
-static int pp_of(const GemmArgs& a, int c) {
-  if (a.kloop == 1) return c == 10 ? 12 : c == 11 ? 13 : c;
-  if (a.kloop == 3) return c == 10 ? 17 : c;
-  return c;
-}
-
 int gemm_config(const GemmArgs& a) {
   // producers: 256x192 tiles, 96-column partials (P = ceil(N / 96) <= kLnPMax), decided from N
   // only, so a row's statistics (and so its result) do not depend on the batch it runs in
-  if (a.epi == 3) return 10;
-  if (a.epi == 2) return a.kloop == 1 ? 12 : a.kloop == 3 ? 17 : 10;
+  if (a.epi == 2 || a.epi == 3) return 10;
   const int f = forced_config(a);
   if (a.epi == 1) return (f == 10 || f == 11) ? f : glds_pick(a, false);
   if (f >= 0) return f;
@@ -738,7 +717,7 @@ int gemm_config(const GemmArgs& a) {
   if (a.N <= 32) return 0;
   if (a.N <= 64) return 1;
   if (a.M <= 512) return 2;  // skinny-M (projections, M = batch)
-  if (glds_ok(a) && a.N >= 128) return pp_of(a, glds_pick(a, true));
+  if (glds_ok(a) && a.N >= 128) return glds_pick(a, true);
   // register-staged tiles (e.g. the SE-scaled EfficientNet projects): 64x128 tiles when 128x128
   // ones would leave the chip short of workgroups (late stages, M = B * 7^2, K = 1152)
   const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
@@ -772,9 +751,8 @@ const char* gemm_config_name(int c) {
   static const char* names[kGemmConfigs] = {
       "gemm_f16<256,32,4,1>", "gemm_f16<256,64,4,1>", "gemm_f16<64,128,1,4>", "gemm_f16<128,128,2,2>", "(removed)",
       "gemm_glds<256,128,4,2>", "(removed)", "(removed)", "(removed)", "pw_conv", "gemm_glds_pipe2<256,192,4,2>",
-      "gemm_glds_pipe2<256,256,2,4>", "gemm_glds_pp<256,192,4,2>", "gemm_glds_pp<256,256,2,4>",
-      "gemm_glds_pp1<256,192,4,2>", "gemm_glds_dma_only",
-      "gemm_glds_compute_only", "gemm_glds_aring<256,192,4,2>", "(removed)"};
+      "gemm_glds_pipe2<256,256,2,4>", "(removed)", "(removed)", "(removed)", "gemm_glds_dma_only",
+      "gemm_glds_compute_only"};
   return (c >= 0 && c < kGemmConfigs) ? names[c] : "gemm_f16<?>";
 }
 
@@ -809,10 +787,6 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
     case 9: return launch_pw(a, s);
     case 10: return run_glds<256, 192, 4, 2, true>(a, s);
     case 11: return run_glds<256, 256, 2, 4, true>(a, s);
-    case 12: return run_glds<256, 192, 4, 2, true, 0, 1>(a, s);
-    case 13: return run_glds<256, 256, 2, 4, true, 0, 1>(a, s);
-    case 14: return run_glds<256, 192, 4, 2, true, 0, 2>(a, s);
-    case 17: return run_glds<256, 192, 4, 2, true, 0, 3>(a, s);
     default: return run<128, 128, 2, 2>(a, s);
   }
 }

@@ -22,8 +22,6 @@ struct GemmArgs {
   int force_cfg;                 // 0 = automatic tile choice, c + 1 = instantiation c (A/B option)
   int no_splitk;                 // 1 = never split K on the skinny-M path (A/B option)
   int group_m;                   // persistent-tile order: 0 row-major, g > 0 grouped by g row panels
-  int kloop;                     // K-loop variant of the persistent plain / producer GEMMs (option gemm_kloop:
-                                 // 0 two stages, 1 ping-pong, 3 A-ring; gemm_glds_body.inc)
   float* ws;                     // split-K partials workspace (skinny-M GEMMs) or null
   size_t ws_elems;               // its capacity in floats
   // Lazy LayerNorm (option lazy_ln; gemm.hip).  A row's LN statistics travel as P partials
@@ -50,7 +48,7 @@ int gemm_ln_tn(const GemmArgs& a);
 int gemm_splitk_factor(const GemmArgs& a);
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s);
 int gemm_config(const GemmArgs& a);          // which instantiation launch_gemm picks
-constexpr int kGemmConfigs = 19;  // numbering of the tile instantiations (0 .. 18; gemm.hip config_exists)
+constexpr int kGemmConfigs = 17;  // numbering of the tile instantiations (0 .. 16; gemm.hip config_exists)
 const char* gemm_config_name(int c);
 // streaming 1x1-convolution kernel (pointwise.hip), picked by launch_gemm when applicable
 bool pw_applicable(const GemmArgs& a);

@@ -69,10 +69,10 @@ def kind_symbol(kind: str) -> str:
 
 
 def same_kernel(a: str, b: str) -> bool:
-    """Symbols equal up to gemm_glds_kernel's trailing TQ = false (round 4's library had a ninth
-    template argument, the tile-queue variant; its PMC summaries print 9 arguments)."""
+    """Symbols equal up to gemm_glds_kernel's ninth template argument when it is the default: round 4's
+    tile-queue TQ = false, or the K-loop variant KL = 0 measured in round 6 (later summaries print 8)."""
     def norm(s):
-        return re.sub(r"^(gemm_glds_kernel<(?:[^,<>]+, ){7}[^,<>]+), false>$", r"\1>", s)
+        return re.sub(r"^(gemm_glds_kernel<(?:[^,<>]+, ){7}[^,<>]+), (?:false|0)>$", r"\1>", s)
     return norm(a) == norm(b)
 
 

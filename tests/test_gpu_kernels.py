@@ -91,7 +91,7 @@ def gemm_config(lib):
     hip.set_process_option("gemm_config", -1)
 
 
-@pytest.mark.parametrize("cfg", [3, 5, 10, 11, 12, 13, 14, 17])
+@pytest.mark.parametrize("cfg", [3, 5, 10, 11])
 @pytest.mark.parametrize("M,N,K,act,res", [(1000, 2304, 768, 1, False), (777, 392, 512, 0, True),
                                            (130, 136, 64, 2, False)])
 def test_gemm_forced_configs(lib, gemm_config, cfg, M, N, K, act, res):
@@ -120,40 +120,6 @@ def test_gemm_forced_configs(lib, gemm_config, cfg, M, N, K, act, res):
     assert (out[:, N:] == 7.0).all(), "wrote past N"
     if res:
         assert (c32.cpu()[:, :N] - ref).abs().max().item() / scale < 2e-5
-
-
-@pytest.mark.parametrize("M,N,K,act,res", [(32768, 768, 768, 0, False), (32768, 768, 3072, 0, False),
-                                           (12544, 768, 3072, 0, False), (2600, 1536, 512, 2, False),
-                                           (777, 392, 512, 1, True), (4096, 3072, 768, 1, False),
-                                           (300, 136, 128, 0, True)])
-def test_gemm_pingpong_bit_identical(lib, gemm_config, M, N, K, act, res):
-    """The K-loop variants (ping-pong: configs 12 / 13 / 14; A-ring: 17; option gemm_kloop) issue
-    the same MFMAs in the same K order per accumulator and share the epilogue: their outputs equal
-    the half-step-pipelined kernels' (10 / 11) bit for bit, on the encoder shapes (several persistent rounds) and ragged
-    edges, fp16-only and fp32 + residual epilogues."""
-    import mmf_amd.hip as hip
-    g = torch.Generator().manual_seed(M + N + K)
-    dev = torch.device("cuda")
-    Ad = _f16(torch.rand(M, K, generator=g) * 2 - 1).to(dev)
-    Wd = _f16((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(dev)
-    bd = torch.randn(N, generator=g).to(dev)
-    Rd = torch.randn(M, N, generator=g).to(dev) if res else None
-
-    def run(cfg):
-        gemm_config(cfg)
-        c16 = torch.full((M, N), 7.0, device=dev, dtype=torch.float16)
-        c32 = torch.empty(M, N, device=dev) if res else None
-        hip.check(lib.mmf_gemm_f16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), hip.ptr(Rd), hip.ptr(c32),
-                                    c16.data_ptr(), N, M, N, K, act, hip.stream_ptr()))
-        torch.cuda.synchronize()
-        return c16, c32
-    for base, pp in ((10, 12), (10, 14), (11, 13), (10, 17)):
-        r16, r32 = run(base)
-        for _ in range(3):
-            o16, o32 = run(pp)
-            assert torch.equal(r16, o16), (base, pp)
-            if res:
-                assert torch.equal(r32, o32), (base, pp)
 
 
 def _attn_ref(qkv, mask, B, L, H, causal):

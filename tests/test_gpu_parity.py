@@ -461,36 +461,6 @@ def test_threaded_tower_enqueue_bit_identical(engine, golden, B):
         engine.set_option("mt_enqueue", mt)
 
 
-@pytest.mark.parametrize("B", [37, 256])
-def test_gemm_pingpong_step_bit_identical(engine, B):
-    """Option gemm_kloop (round 6): the persistent plain GEMMs (RoBERTa out-proj / FFN, the ViT patch
-    GEMM) and the CLIP lazy-LN producers run the ping-pong K loop.  Same MFMAs in the same order per
-    accumulator, same epilogues: every output of analyze_batch and clip_consistency is bit-identical
-    to the half-step-pipelined kernels'."""
-    import mmf_amd.synthetic as syn
-    rid, rm = syn.roberta_ids(B, 128, 92, [128, 64, 9])
-    cid, cm = syn.clip_ids(B, 77, 92, [77, 33, 6, 50])
-    imgs = syn.images(B, 92)
-
-    def run():
-        out = {k: v.clone() for k, v in engine.analyze_batch(rid, rm, cid, cm, imgs).items()}
-        out.update({"cons_" + k: v.clone() for k, v in engine.clip_consistency(imgs, cid, cm).items()})
-        torch.cuda.synchronize()
-        return out
-    old = engine.get_option("gemm_kloop")
-    try:
-        engine.set_option("gemm_kloop", 0)
-        ref = run()
-        for kl in (1, 3):
-            engine.set_option("gemm_kloop", kl)
-            for _ in range(2):
-                out = run()
-                for k, v in ref.items():
-                    assert torch.equal(v, out[k]), (kl, k)
-    finally:
-        engine.set_option("gemm_kloop", old)
-
-
 @pytest.mark.parametrize("B", [100, 256])
 def test_tower_order_bit_identical(engine, B):
     """Option after_text (round 5): in the concurrent B > mt_enqueue step the chosen towers' streams

@@ -18,7 +18,7 @@ from collections import defaultdict
 def same_kernel(a, b):
     """Symbols equal up to gemm_glds_kernel's trailing TQ = false (as profiling.same_kernel)."""
     def norm(s):
-        return re.sub(r"^(gemm_glds_kernel<(?:[^,<>]+, ){7}[^,<>]+), false>$", r"\1>", s)
+        return re.sub(r"^(gemm_glds_kernel<(?:[^,<>]+, ){7}[^,<>]+), (?:false|0)>$", r"\1>", s)
     return norm(a) == norm(b)
 
 
