@@ -958,14 +958,16 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
     CHK(gemm(h, g, s));
     {
       ProfScope ps(h, s, PK_ATTN, 4.0 * B * 12 * (double)L * L * 64, (double)M * (2304 + 768) * 4);
-      HIPCHK(launch_attention32(w.p32, 2304, 768, 1536, mask, y, 768, B, L, 12, s));
+      // ctx straight into the out-projection's operand rows (no fp32 ctx / split3 pass)
+      HIPCHK(launch_attention32(w.p32, 2304, 768, 1536, mask, y, 768, B, L, 12, s, w.s3, pm >> 1 & 1));
     }
-    HIPCHK(launch_split3(y, 768, w.s3, M, 768, s, pm >> 1 & 1));
     g = with_ws(lin(w.s3, 2304, Ly.o, Ly.o3, 1), w.sk_text, w.sk_elems);
     g.c32 = y;
     CHK(gemm(h, g, s));
-    CHK(lnorm_add(h, x, y, Ly.ln1, M, s));
-    HIPCHK(launch_split3(x, 768, w.s3, M, 768, s, pm >> 2 & 1));
+    {  // x = LN1(x + y) and FFN-1's operand rows of it, one pass
+      ProfScope ps(h, s, PK_LN, 9.0 * M * 768, (double)M * 768 * 14);
+      HIPCHK(launch_layernorm_split3(x, y, Ly.ln1.g, Ly.ln1.b, 1e-5f, w.s3, pm >> 2 & 1, M, 768, s));
+    }
     g = with_ws(lin(w.s3, 2304, Ly.fc1, Ly.fc13, 2), w.sk_text, w.sk_elems);
     g.act = 1;  // GELU-erf
     g.c32 = w.p32;
@@ -975,8 +977,12 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
     g = with_ws(lin(w.h3, 9216, Ly.fc2, Ly.fc23, 3), w.sk_text, w.sk_elems);
     g.c32 = y;
     CHK(gemm(h, g, s));
-    CHK(lnorm_add(h, x, y, Ly.ln2, M, s));
-    if (i < 11) HIPCHK(launch_split3(x, 768, w.s3, M, 768, s, pm & 1));
+    if (i < 11) {  // x = LN2(x + y) and the next layer's QKV operand rows of it
+      ProfScope ps(h, s, PK_LN, 9.0 * M * 768, (double)M * 768 * 14);
+      HIPCHK(launch_layernorm_split3(x, y, Ly.ln2.g, Ly.ln2.b, 1e-5f, w.s3, pm & 1, M, 768, s));
+    } else {
+      CHK(lnorm_add(h, x, y, Ly.ln2, M, s));
+    }
   }
   ProfScope ps(h, s, PK_HEADS, 2.0 * B * 2 * (768 * 256 + 256 * 2), (double)B * 768 * 4 + 2 * 768 * 256 * 4);
   HIPCHK(launch_text_heads(x, L * 768, h->h_w1a, h->h_b1a, h->h_w2a, h->h_b2a, h->h_w1m, h->h_b1m, h->h_w2m,

@@ -91,8 +91,13 @@ hipError_t launch_roberta_embed(const int32_t* ids, const float* word, const flo
 // v at voff + h*64; key-padding mask int32 [B][L] or null) -> fp32 out [B*L][ldo]
 // with_lo = 0: only the hi third is written (a consumer on fp16 operands)
 hipError_t launch_split3(const float* x, int ldx, f16_t* out, int rows, int C, hipStream_t s, int with_lo = 1);
+// out3 (nullable): ctx written as the next GEMM's operand rows [hi | lo | hi] (ld 3 * H * 64; with_lo = 0: hi
+// alone) instead of fp32 rows to out
 hipError_t launch_attention32(const float* qkv, int ld, int koff, int voff, const int32_t* mask, float* out, int ldo,
-                              int B, int L, int H, hipStream_t s);
+                              int B, int L, int H, hipStream_t s, f16_t* out3 = nullptr, int with_lo = 1);
+// precise mode: x = LN(x + add) in place [rows][768] fp32, and s3 = [hi | lo | hi] rows of it (with_lo = 0: hi only)
+hipError_t launch_layernorm_split3(float* x, const float* add, const float* g, const float* b, float eps, f16_t* s3,
+                                   int with_lo, int rows, int C, hipStream_t s);
 // RoBERTa post-LN residual stream split as hi = fp16(x) (also the GEMM operand), lo = fp16(x - hi)
 hipError_t launch_add_ln_hilo(f16_t* hi, uint16_t* lo, int ld, const f16_t* y, int ldy, const float* g,
                               const float* b, float eps, int rows, int C, hipStream_t s, int* ovf = nullptr, int L = 0);

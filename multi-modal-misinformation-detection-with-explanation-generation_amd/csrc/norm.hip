@@ -120,6 +120,34 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx,
   store_row<NV>(v, y32 ? y32 + (size_t)row * ldy32 : nullptr, y16 ? y16 + (size_t)row * ldy16 : nullptr, lane);
 }
 
+// RoBERTa precise mode (precise.hip / capi.cpp run_text_precise): x = LN(x + add) in place (fp32 stream)
+// and the next GEMM's K-concatenated operand rows s3 = [hi | lo | hi] of the result (LO = false: hi
+// alone, for a consumer on fp16 operands) -- the LayerNorm and the split3 pass in one
+template <int NV, bool LO>
+__global__ __launch_bounds__(256) void layernorm_split3_kernel(float* x, const float* add, const float* g,
+                                                               const float* b, float eps, f16_t* s3, int rows) {
+  constexpr int C = NV * 256;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float4 v[NV];
+  load_row<NV>(v, x + (size_t)row * C, lane);
+  add_row<NV>(v, add + (size_t)row * C, lane);
+  ln_row<NV>(v, g, b, eps, C, lane);
+  store_row<NV>(v, x + (size_t)row * C, nullptr, lane);
+  f16_t* o = s3 + (size_t)row * 3 * C;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    const uint2 hi = make_uint2(pack2h(v[i].x, v[i].y), pack2h(v[i].z, v[i].w));
+    *reinterpret_cast<uint2*>(o + c) = hi;
+    if constexpr (LO) {
+      *reinterpret_cast<uint2*>(o + C + c) = make_uint2(pack2h(v[i].x - lo_h(hi.x), v[i].y - hi_h(hi.x)),
+                                                        pack2h(v[i].z - lo_h(hi.y), v[i].w - hi_h(hi.y)));
+      *reinterpret_cast<uint2*>(o + 2 * C + c) = hi;
+    }
+  }
+}
+
 // Residual add + LayerNorm after an out-projection / FFN-2 GEMM whose fp16 output y is the
 // residual branch: s = x + y in fp32 (x = fp32 residual stream), then
 //   pre-LN (CLIP, TF clip:357-385):   s32 = s (the new residual stream), o16 = LN(s)
@@ -401,6 +429,15 @@ __global__ __launch_bounds__(256) void l2norm_kernel(float* x, int B, int C) {
 }
 
 }  // namespace
+
+hipError_t launch_layernorm_split3(float* x, const float* add, const float* g, const float* b, float eps, f16_t* s3,
+                                   int with_lo, int rows, int C, hipStream_t s) {
+  if (C != 768) return hipErrorInvalidValue;
+  const dim3 grid((rows + 3) / 4);
+  if (with_lo) hipLaunchKernelGGL((layernorm_split3_kernel<3, true>), grid, dim3(256), 0, s, x, add, g, b, eps, s3, rows);
+  else hipLaunchKernelGGL((layernorm_split3_kernel<3, false>), grid, dim3(256), 0, s, x, add, g, b, eps, s3, rows);
+  return hipGetLastError();
+}
 
 hipError_t launch_layernorm(const float* x, int ldx, const float* add, int ldadd, const float* g, const float* b,
                             float eps, float* y32, int ldy32, f16_t* y16, int ldy16, int rows, int C,

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
 constexpr int A32_Q = 128, A32_K = 32;
 __global__ __launch_bounds__(A32_Q) void attention32_kernel(const float* __restrict__ qkv, int ld, int koff, int voff,
                                                             const int32_t* __restrict__ mask, float* __restrict__ out,
-                                                            int ldo, int L, int H) {
+                                                            int ldo, int L, int H, f16_t* __restrict__ out3, int with_lo) {
   __shared__ __attribute__((aligned(16))) float Ks[A32_K][64];
   __shared__ __attribute__((aligned(16))) float Vs[A32_K][64];
   __shared__ float kb[A32_K];
@@ -51,20 +51,21 @@ __global__ __launch_bounds__(A32_Q) void attention32_kernel(const float* __restr
   const int qi = blockIdx.y * A32_Q + tid;
   const int qc = qi < L ? qi : L - 1;  // (threads past L compute a clamped row, never stored)
   const float* base = qkv + (size_t)bi * L * ld;
-  float q[64], o[64];
+  // q and o as 32 pairs: every dot-product / accumulation step is one packed fp32 FMA (v_pk_fma_f32,
+  // two lanes' worth of fp32 FMAs per issue; the even / odd columns of the q.k dot product in two
+  // accumulators, added at the end)
+  f32x2_t q[32], o[32];
   {
     const float4* qp = reinterpret_cast<const float4*>(base + (size_t)qc * ld + h * 64);
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       const float4 v = qp[c];
-      q[4 * c] = v.x * 0.125f;  // 1 / sqrt(64): exact
-      q[4 * c + 1] = v.y * 0.125f;
-      q[4 * c + 2] = v.z * 0.125f;
-      q[4 * c + 3] = v.w * 0.125f;
+      q[2 * c] = (f32x2_t){v.x, v.y} * 0.125f;  // 1 / sqrt(64): exact
+      q[2 * c + 1] = (f32x2_t){v.z, v.w} * 0.125f;
     }
   }
 #pragma unroll
-  for (int d = 0; d < 64; ++d) o[d] = 0.f;
+  for (int d = 0; d < 32; ++d) o[d] = (f32x2_t){0.f, 0.f};
   float m = -INFINITY, l = 0.f;
   for (int k0 = 0; k0 < L; k0 += A32_K) {
     __syncthreads();  // the previous chunk's readers are done
@@ -87,16 +88,14 @@ __global__ __launch_bounds__(A32_Q) void attention32_kernel(const float* __restr
     float cm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < A32_K; ++j) {
-      float a = 0.f;
+      f32x2_t a2 = {0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const float4 kv = *reinterpret_cast<const float4*>(&Ks[j][4 * c]);
-        a = fmaf(q[4 * c], kv.x, a);
-        a = fmaf(q[4 * c + 1], kv.y, a);
-        a = fmaf(q[4 * c + 2], kv.z, a);
-        a = fmaf(q[4 * c + 3], kv.w, a);
+        a2 = __builtin_elementwise_fma(q[2 * c], (f32x2_t){kv.x, kv.y}, a2);
+        a2 = __builtin_elementwise_fma(q[2 * c + 1], (f32x2_t){kv.z, kv.w}, a2);
       }
-      s[j] = a + kb[j];
+      s[j] = (a2.x + a2.y) + kb[j];
       cm = fmaxf(cm, s[j]);
     }
     const float mn = fmaxf(m, cm);
@@ -104,27 +103,43 @@ __global__ __launch_bounds__(A32_Q) void attention32_kernel(const float* __restr
     const float sc = expf(m - mn);  // (m = -inf: 0)
     l *= sc;
 #pragma unroll
-    for (int d = 0; d < 64; ++d) o[d] *= sc;
+    for (int d = 0; d < 32; ++d) o[d] = o[d] * sc;
 #pragma unroll
     for (int j = 0; j < A32_K; ++j) {
       const float p = expf(s[j] - mn);  // masked: exp(-inf) = 0
       l += p;
+      const f32x2_t pp = {p, p};
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const float4 vv = *reinterpret_cast<const float4*>(&Vs[j][4 * c]);
-        o[4 * c] = fmaf(p, vv.x, o[4 * c]);
-        o[4 * c + 1] = fmaf(p, vv.y, o[4 * c + 1]);
-        o[4 * c + 2] = fmaf(p, vv.z, o[4 * c + 2]);
-        o[4 * c + 3] = fmaf(p, vv.w, o[4 * c + 3]);
+        o[2 * c] = __builtin_elementwise_fma(pp, (f32x2_t){vv.x, vv.y}, o[2 * c]);
+        o[2 * c + 1] = __builtin_elementwise_fma(pp, (f32x2_t){vv.z, vv.w}, o[2 * c + 1]);
       }
     }
     m = mn;
   }
   if (qi >= L) return;
-  const float inv = l > 0.f ? 1.0f / l : 0.f;
+  const float inv = l == 0.f ? 0.f : 1.0f / l;  // (a non-finite sum propagates)
+  if (out3) {  // the out-projection's operand row, split as split3_kernel does (fused: no fp32 ctx pass)
+    const int D = H * 64;
+    f16_t* o3 = out3 + ((size_t)bi * L + qi) * 3 * D + h * 64;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float v0 = o[2 * c].x * inv, v1 = o[2 * c].y * inv, v2 = o[2 * c + 1].x * inv, v3 = o[2 * c + 1].y * inv;
+      const uint2 hi = make_uint2(pack2h(v0, v1), pack2h(v2, v3));
+      *reinterpret_cast<uint2*>(o3 + 4 * c) = hi;
+      if (with_lo) {
+        *reinterpret_cast<uint2*>(o3 + D + 4 * c) =
+            make_uint2(pack2h(v0 - lo_h(hi.x), v1 - hi_h(hi.x)), pack2h(v2 - lo_h(hi.y), v3 - hi_h(hi.y)));
+        *reinterpret_cast<uint2*>(o3 + 2 * D + 4 * c) = hi;
+      }
+    }
+    return;
+  }
   float4* op = reinterpret_cast<float4*>(out + ((size_t)bi * L + qi) * ldo + h * 64);
 #pragma unroll
-  for (int c = 0; c < 16; ++c) op[c] = make_float4(o[4 * c] * inv, o[4 * c + 1] * inv, o[4 * c + 2] * inv, o[4 * c + 3] * inv);
+  for (int c = 0; c < 16; ++c)
+    op[c] = make_float4(o[2 * c].x * inv, o[2 * c].y * inv, o[2 * c + 1].x * inv, o[2 * c + 1].y * inv);
 }
 
 }  // namespace
@@ -141,10 +156,10 @@ hipError_t launch_split3(const float* x, int ldx, f16_t* out, int rows, int C, h
 }
 
 hipError_t launch_attention32(const float* qkv, int ld, int koff, int voff, const int32_t* mask, float* out, int ldo,
-                              int B, int L, int H, hipStream_t s) {
+                              int B, int L, int H, hipStream_t s, f16_t* out3, int with_lo) {
   if (B <= 0 || L <= 0) return hipSuccess;
   if ((ld & 3) || (koff & 3) || (voff & 3) || (ldo & 3)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(attention32_kernel, dim3(B * H, (L + A32_Q - 1) / A32_Q), dim3(A32_Q), 0, s, qkv, ld, koff, voff,
-                     mask, out, ldo, L, H);
+                     mask, out, ldo, L, H, out3, with_lo);
   return hipGetLastError();
 }
