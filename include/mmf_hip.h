@@ -252,6 +252,8 @@ const char* mmf_profile_kind_name(int kind);
  *   "diag_skip"      0: diagnostic bitmask of towers mmf_analyze_batch leaves out (2 EfficientNet,
  *                       4 CLIP text, 8 ViT, ...; measurement only)
  *   "qkv_attn"       1: RoBERTa L = 128: attention in the QKV GEMM's epilogue
+ *   "vault_ref"      0: diagnostic: vault similarities on the VALU kernel, top-k by full sort (the
+ *                       reference kernels the production MFMA / register top-k kernels equal bit for bit)
  *   "mt_enqueue"    64: batches of <= this many pairs: towers enqueued by host threads side by side
  *   "last_q1"        1: compact last encoder layers (bit 1 RoBERTa, bit 2 CLIP towers)
  *   "after_text"    12: towers of the concurrent step that start once RoBERTa is done (bitmask as

@@ -161,6 +161,8 @@ struct Options {
                         // (bit 1: RoBERTa -- QKV 4.5 -> K/V 3 persistent rounds; bit 2: CLIP towers, whose K/V
                         // GEMMs round to as many rounds as QKV: measured slower, off)
   int diag_skip = 0;    // diagnostic: towers mmf_analyze_batch leaves out (bitmask; measurement only)
+  int vault_ref = 0;    // diagnostic: vault similarities on the VALU kernel and top-k by full sort (the
+                        // reference kernels the production ones are bit-identical to)
   int after_text = 12;  // towers of the concurrent B > mt_enqueue step that start only once RoBERTa is done
                         // (bitmask as diag_skip: 2 EfficientNet, 4 CLIP text, 8 ViT)
 };
@@ -180,6 +182,7 @@ const OptName kOptNames[] = {
     {"pw32_mfma", &Options::pw32_mfma, "MMF_PW32_MFMA"},
     {"effnet_chunks", &Options::effnet_chunks, "MMF_EFFNET_CHUNKS"}, {"dw_cw32", &Options::dw_cw32, "MMF_DW_CW32"},
     {"diag_skip", &Options::diag_skip, "MMF_DIAG_SKIP"}, {"qkv_attn", &Options::qkv_attn, "MMF_QKV_ATTN"},
+    {"vault_ref", &Options::vault_ref, "MMF_VAULT_REF"},
     {"mt_enqueue", &Options::mt_enqueue, "MMF_MT_ENQUEUE"}, {"last_q1", &Options::last_q1, "MMF_LAST_Q1"},
     {"after_text", &Options::after_text, "MMF_AFTER_TEXT"},
 };
@@ -1559,9 +1562,9 @@ int analyze_tail(mmf_handle* h, int B, float* scores5, float* text_sim, float* p
   HIPCHK(launch_rowdot(w.v_emb, w.t_emb, scores5 + 3, 5, B, 512, s));
   if (h->ready & 32) {
     ProfScope ps(h, s, PK_VAULT, 2.0 * B * h->vault_n * 512, (double)h->vault_n * 512 * 4 + (double)B * h->vault_n * 8);
-    HIPCHK(launch_vault_sims(w.v_emb, h->vault, w.s_sims, B, h->vault_n, 512, s));
+    HIPCHK(launch_vault_sims(w.v_emb, h->vault, w.s_sims, B, h->vault_n, 512, s, h->opt.vault_ref));
     HIPCHK(launch_vault_topk(w.s_sims, B, h->vault_n, 5, 0.85f, top_sims, top_idx, scores5 + 4, 5, w.t_emb,
-                             h->vault_title, 512, text_sim, s));
+                             h->vault_title, 512, text_sim, s, h->opt.vault_ref));
   } else {
     HIPCHK(launch_fill_strided(scores5 + 4, 5, B, 0.f, s));
     if (text_sim) HIPCHK(hipMemsetAsync(text_sim, 0, (size_t)B * 4, s));
@@ -1944,9 +1947,9 @@ int mmf_vault_topk(mmf_handle* h, const float* q, int B, int k, float thresh, fl
   CHK(check_cap(h, B, 1, 1));
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
-  HIPCHK(launch_vault_sims(q, h->vault, h->ws.s_sims, B, h->vault_n, 512, s));
+  HIPCHK(launch_vault_sims(q, h->vault, h->ws.s_sims, B, h->vault_n, 512, s, h->opt.vault_ref));
   HIPCHK(launch_vault_topk(h->ws.s_sims, B, h->vault_n, k, thresh, sims, idx, disc, 1, temb, h->vault_title, 512,
-                           tsim, s));
+                           tsim, s, h->opt.vault_ref));
   return 0;
 }
 

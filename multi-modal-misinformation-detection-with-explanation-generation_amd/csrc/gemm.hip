@@ -475,16 +475,31 @@ MMF_DEV unsigned long long gst_time() {
   unsigned long long* gst_ = (g_gemm_stamp && blockIdx.x < 256u) ? g_gemm_stamp + (size_t)blockIdx.x * kGStampSlots \
                                                                  : nullptr;                                  \
   int gst_n_ = 3;                                                                                            \
+  bool gst_first_ = true;                                                                                    \
   {                                                                                                          \
     const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                                          \
     if (gst_ && threadIdx.x == 0) gst_[0] = r_;                                                              \
   }
+#if MMF_GEMM_STAMP == 2
+// phase mode (-DMMF_GEMM_STAMP=2, tools/gemm_stamps.py --phases): wave 0 of each
+// workgroup stamps 4 points of K-steps 1 .. 20 of its FIRST tile -- step start, after the LDS-DMA
+// issue, after the last MFMA issue, after the step barrier -- into slots 3 + 4 (kt - 1) + p
+#define GST() {}
+#define GSTP(p)                                                                                              \
+  if (gst_first_ && kt >= 1 && kt <= 20) {                                                                   \
+    const unsigned long long t_ = gst_time();                                                                \
+    if (gst_ && threadIdx.x == 0) gst_[3 + 4 * (kt - 1) + (p)] = t_;                                          \
+  }
+#else
+#define GSTP(p)
 #define GST()                                                                                                \
   {                                                                                                          \
     const unsigned long long t_ = gst_time();                                                                \
     if (gst_ && threadIdx.x == 0 && gst_n_ < kGStampSlots) gst_[gst_n_] = t_;                                \
     ++gst_n_;                                                                                                \
   }
+#endif
+#define GST_TILE_DONE() gst_first_ = false;
 #define GST_END()                                                                                            \
   {                                                                                                          \
     GST()                                                                                                    \
@@ -494,7 +509,13 @@ MMF_DEV unsigned long long gst_time() {
 #else
 #define GST_INIT()
 #define GST()
+#define GSTP(p)
+#define GST_TILE_DONE()
 #define GST_END()
+#endif
+
+#ifndef MMF_DMA_ILV
+#define MMF_DMA_ILV 1  // LDS-DMA pieces interleaved with the MFMAs of the PIPE2 K loop (gemm_glds_body.inc; 0: A/B builds)
 #endif
 
 #ifndef MMF_GLDS_BUF
@@ -664,7 +685,11 @@ hipError_t run_splitk(const GemmArgs& a, int S, hipStream_t s) {
 static bool glds_ok(const GemmArgs& a) {
   const size_t lim = (size_t)1 << 31;
   const size_t rows = (size_t)a.M + 256;
-  return (a.K % BK) == 0 && !a.ascale && rows * a.ldc * 4 < lim && rows * (a.ldr > 0 ? a.ldr : 0) * 4 < lim;
+  // (the interleaved LDS-DMA, MMF_DMA_ILV, forms every operand offset -- rows up to M + 255 / N + 255 --
+  // as one 32-bit voffset)
+  const size_t lim32 = (size_t)1 << 32;
+  return (a.K % BK) == 0 && !a.ascale && rows * a.ldc * 4 < lim && rows * (a.ldr > 0 ? a.ldr : 0) * 4 < lim &&
+         rows * (size_t)a.lda * 2 < lim32 && ((size_t)a.N + 256) * a.ldw * 2 < lim32;
 }
 
 #ifndef MMF_GEMM_DIAG

@@ -141,10 +141,10 @@ hipError_t launch_fusion(const float* x5, const float* w0, const float* b0, cons
 // cosine of unit rows: out[b*ostride] = dot(a[b], c[b])
 hipError_t launch_rowdot(const float* a, const float* c, float* out, int ostride, int B, int C, hipStream_t s);
 // vault: S[B][N] = Q[B][D] . V[N][D]^T (fp32)
-hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s);
+hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s, int ref = 0);
 hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, float* sims, int32_t* idx,
                              float* disc, int disc_stride, const float* text_emb, const float* title_emb, int D,
-                             float* text_sim, hipStream_t s);
+                             float* text_sim, hipStream_t s, int ref = 0);
 
 // EfficientNet-B0 pieces (NHWC fp16 activations)
 hipError_t launch_effnet_stem(const uint8_t* img, const float* w, const float* bias, f16_t* out, int B,

@@ -484,24 +484,23 @@ hipError_t launch_rowdot(const float* a, const float* c, float* out, int ostride
 #ifndef MMF_VAULT_CH
 #define MMF_VAULT_CH 4  // 16-deep K chunks per LDS stage / barrier
 #endif
-hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s) {
+hipError_t launch_vault_sims(const float* q, const float* v, float* S, int B, int N, int D, hipStream_t s, int ref) {
   if (D & 63) return hipErrorInvalidValue;
   if (B <= 0 || N <= 0) return hipSuccess;
-  // the fp32-MFMA kernel (bit-identical); a -DMMF_VAULT_VALU build keeps the VALU kernel (A/B builds)
-#ifdef MMF_VAULT_VALU
-  hipLaunchKernelGGL(vault_sims_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
-#else
-  if ((D % (16 * MMF_VAULT_CH)) == 0)
+  // the fp32-MFMA kernel; ref (option vault_ref, diagnostic): the VALU kernel it is bit-identical to
+  // (tests/test_gpu_vault_edge.py::test_vault_kernels_match_reference_kernels)
+  if (ref)
+    hipLaunchKernelGGL(vault_sims_kernel, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
+  else if ((D % (16 * MMF_VAULT_CH)) == 0)
     hipLaunchKernelGGL(vault_sims_mfma_kernel<MMF_VAULT_CH>, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
   else
     hipLaunchKernelGGL(vault_sims_mfma_kernel<1>, dim3((N + 63) / 64, (B + 15) / 16), dim3(256), 0, s, q, v, S, B, N, D);
-#endif
   return hipGetLastError();
 }
 
 hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, float* sims, int32_t* idx,
                              float* disc, int disc_stride, const float* text_emb, const float* title_emb, int D,
-                             float* text_sim, hipStream_t s) {
+                             float* text_sim, hipStream_t s, int ref) {
   const dim3 grid(B), blk(256);  // one block (four waves) per query row
 #define TOPK_CASE(KK)                                                                                          \
   case KK:                                                                                                     \
@@ -512,7 +511,9 @@ hipError_t launch_vault_topk(const float* S, int B, int N, int k, float thresh, 
   // register kernels pad slots N..k-1 with (-inf, -1) (the host drops idx < 0), so a fixed k = 5
   // (mmf_analyze_batch) serves a vault of any size; the sort kernel pads the same way up to P.
   if (k < 1 || N < 1) return hipErrorInvalidValue;
-  switch (k) {
+  // ref (option vault_ref, diagnostic): every k through the full-sort kernel -- an independent
+  // selection algorithm the register kernels must agree with bit for bit
+  switch (ref && N <= 16384 ? 0 : k) {
     TOPK_CASE(1) TOPK_CASE(2) TOPK_CASE(3) TOPK_CASE(4) TOPK_CASE(5) TOPK_CASE(6) TOPK_CASE(7) TOPK_CASE(8)
     default: {
 #define SORT_CASE(PP)                                                                                            \

@@ -90,6 +90,39 @@ def test_top_k_any_size(engine, fixture):
     assert sorted(full_i.cpu().numpy()[0].tolist()) == list(range(VE.N))  # a permutation
 
 
+@pytest.mark.parametrize("N", [3, 7, 1001, 2171])
+def test_vault_kernels_match_reference_kernels(engine, N):
+    """the production vault path (fp32-MFMA similarities, register top-k with its
+    block / merge structure) against the reference kernels kept callable at run time (option
+    vault_ref: the VALU similarity kernel -- one fp32 FMA chain per output in k order -- and the full
+    LDS sort): bit-identical similarities, indices, discrepancies and caption similarities, on
+    ragged vault sizes (N % 4 != 0, N < 8) and every register-kernel k <= N."""
+    rng = np.random.default_rng(N)
+    vault = rng.standard_normal((N, 512)).astype(np.float32)
+    B = 8  # (the fixture engine's reserved batch)
+    q = rng.standard_normal((B, 512)).astype(np.float32)
+    q[:5] = vault[rng.integers(0, N, 5)] * 3.0  # planted hits above the 0.85 threshold
+    ids = np.full((N, 77), 49407, np.int32)
+    ids[:, 0] = 49406
+    mask = np.zeros_like(ids)
+    mask[:, :2] = 1
+    engine.set_vault(vault, ids, mask)
+    qu = torch.as_tensor(q / np.linalg.norm(q, axis=1, keepdims=True)).cuda()
+    temb = torch.nn.functional.normalize(torch.randn(B, 512, generator=torch.Generator().manual_seed(N))).cuda()
+    old = engine.get_option("vault_ref")
+    try:
+        for k in [k for k in (1, 3, 5, 8) if k <= N]:  # (mmf_vault_topk: k <= N, as search_vault's argsort)
+            engine.set_option("vault_ref", 0)
+            got = [t.clone() for t in engine.vault_topk(qu, k, 0.85, temb)]
+            engine.set_option("vault_ref", 1)
+            ref = [t.clone() for t in engine.vault_topk(qu, k, 0.85, temb)]
+            torch.cuda.synchronize()
+            for name, a, b in zip(("sims", "idx", "disc", "text_sim"), got, ref):
+                assert torch.equal(a, b), (N, k, name)
+    finally:
+        engine.set_option("vault_ref", old)
+
+
 def test_vault_reload_frees_device_memory(engine):
     """mmf_set_vault_normalized / mmf_set_vault_titles replace (and free) the previous vault: ten
     reloads leave the handle's device bytes and the device's free memory where they were."""

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--shapes", default="rob_o,rob_fc2,rob_fc1,rob_qkv,vit_o,vit_fc2,txt_o,txt_fc2")
     ap.add_argument("--config", type=int, default=-1, help="forced gemm_config (default: production choice)")
     ap.add_argument("--warm", type=int, default=30)
+    ap.add_argument("--phases", action="store_true",
+                    help="a -DMMF_GEMM_STAMP=2 build: the four phase stamps of K-steps 1..20 of each workgroup's first tile")
     a = ap.parse_args()
     import mmf_amd.hip as hip
     lib = hip.load()
@@ -71,6 +73,9 @@ def main():
         st = buf.view(256, SLOTS).cpu().numpy()
         used = st[:, 2] > 0
         nk = K // 64
+        if a.phases:
+            phases(name, M, N, K, st, used, nk)
+            continue
         first, k0, kstep, epi, tail, life, clk, ntile = [], [], [], [], [], [], [], []
         for r in st[used]:
             n = int(r[2])
@@ -100,6 +105,32 @@ def main():
         print("    per phase: " + "  ".join(f"{k} {v:.0f}" for k, v in parts.items()))
         print("    shares:    " + "  ".join(f"{k} {100 * v / L:.1f}%" for k, v in shares.items()))
     hip.set_process_option("gemm_config", -1)
+
+
+def phases(name, M, N, K, st, used, nk):
+    """Per steady K-step (wave 0, steps 1..min(nk - 1, 20) of the first tile), cycles spent
+    issuing the next slab's LDS-DMA (dma), issuing the fragment reads and MFMAs until the last MFMA
+    is issued (reads+mfma: the partner wave's MFMAs share the pipe), waiting at the step barrier --
+    vmcnt(0) for the DMA plus the slowest wave (barrier), and from the barrier to the next step's
+    start (loop)."""
+    steps = min(nk - 1, 20)
+    rows = []
+    for r in st[used]:
+        t = r[3:3 + 4 * steps].reshape(steps, 4).astype(np.float64)
+        if (t <= 0).any():
+            continue
+        for i in range(steps):
+            nxt = t[i + 1, 0] if i + 1 < steps else np.nan
+            rows.append((t[i, 1] - t[i, 0], t[i, 2] - t[i, 1], t[i, 3] - t[i, 2], nxt - t[i, 3], t[i, 3] - t[i, 0]))
+    a = np.array(rows)
+    med = np.nanmedian(a, axis=0)
+    p90 = np.nanpercentile(a, 90, axis=0)
+    names = ("dma", "reads+mfma", "barrier", "loop", "step")
+    print(f"{name:8s} M={M} N={N} K={K}: {used.sum()} WGs x {steps} steady K-steps (wave 0; 48 MFMAs x 2 waves = "
+          f"1536 pipe cycles per step)")
+    print("    median cycles: " + "  ".join(f"{n} {v:.0f}" for n, v in zip(names, med)))
+    print("    p90 cycles:    " + "  ".join(f"{n} {v:.0f}" for n, v in zip(names, p90)))
+    print("    share of the median step: " + "  ".join(f"{n} {100 * v / med[4]:.0f}%" for n, v in zip(names[:3], med[:3])))
 
 
 if __name__ == "__main__":
