@@ -281,6 +281,14 @@ int mmf_gemm_f16_ex(const void* A, int lda, const void* W, int ldw, const float*
                      const float* ascale, int rows_per_batch, void* c16, int ldc, int M, int N, int K, int act,
                      void* stream);
 
+/* The RoBERTa precise mode's FFN-1 epilogue (gemm.hip epi 4), exported for its bit-identity test:
+ * out = act(A @ W^T + bias) written as the next GEMM's split operand row -- c16[m*ldc + n] = fp16(out)
+ * and, with split_lo, c16[m*ldc + N + n] = fp16(out - fp16(out)), c16[m*ldc + 2N + n] = fp16(out)
+ * (ldc >= 3N).  act 1 (gelu-erf) only; persistent-tile shapes only (K % 64 == 0, N % 8 == 0), else
+ * MMF_EINVAL. */
+int mmf_gemm_f16_split(const void* A, int lda, const void* W, int ldw, const float* bias, void* c16, int ldc, int M,
+                       int N, int K, int act, int split_lo, void* stream);
+
 /* Low-level attention op for tests: qkv fp16 [B*L, 3*H*64] (q|k|v), mask int32 [B,L] or NULL,
  * causal 0/1 -> out fp16 [B*L, H*64].  L <= 512. */
 int mmf_attention_f16(const void* qkv, const int32_t* mask, void* out, int B, int L, int H, int causal,

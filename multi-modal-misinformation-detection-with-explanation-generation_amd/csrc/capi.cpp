@@ -389,7 +389,7 @@ int free_group(mmf_handle* h, int group) {
 // ---- per-kernel timing: two hipEvents around each launch while profiling is on ------------
 // GEMM launches are profiled per (tile instantiation, epilogue, activation) -- one kernel symbol
 // each, so the numbers line up with a rocprofv3 kernel trace of the same run.
-constexpr int kGemmActs = 5, kGemmEpis = 4;
+constexpr int kGemmActs = 5, kGemmEpis = 5;
 enum ProfKind {
   PK_GEMM0 = 0, PK_GEMM_LAST = kGemmConfigs * kGemmEpis * kGemmActs - 1, PK_ATTN, PK_LN, PK_EMBED, PK_IM2COL, PK_STEM, PK_DW, PK_SE,
   PK_GAP, PK_HEADS, PK_VAULT, PK_FUSION, PK_PW32, PK_COUNT
@@ -832,7 +832,7 @@ int gemm(mmf_handle* h, GemmArgs g, hipStream_t s) {
   // writes ctx (N / 3 columns) instead of qkv
   const double att = g.epi == 3 ? 4.0 * (M / 128) * (N / 192) * 128.0 * 128.0 * 64.0 : 0.0;
   ProfScope ps(h, s, (gemm_config(g) * kGemmEpis + g.epi) * kGemmActs + g.act, 2.0 * M * N * K + att,
-               2.0 * (M * K + N * K) + M * (g.epi == 3 ? N / 3 : N) * out_b);
+               2.0 * (M * K + N * K) + M * (g.epi == 3 ? N / 3 : N) * out_b * (g.epi == 4 && g.split_lo ? 3 : 1));
   HIPCHK(launch_gemm(g, s));
   return 0;
 }
@@ -973,10 +973,22 @@ int run_text_precise(mmf_handle* h, const int32_t* ids, const int32_t* mask, int
     }
     g = with_ws(lin(w.s3, 2304, Ly.fc1, Ly.fc13, 2), w.sk_text, w.sk_elems);
     g.act = 1;  // GELU-erf
-    g.c32 = w.p32;
-    g.ldc = 3072;
-    CHK(gemm(h, g, s));
-    HIPCHK(launch_split3(w.p32, 3072, w.h3, M, 3072, s, pm >> 3 & 1));
+    // the hidden straight into FFN-2's operand rows (epilogue 4: hi | lo | hi, no fp32 hidden and
+    // no split3 pass: -8 B of HBM traffic per hidden element); the fp32 + split3 path where the
+    // persistent tiles do not apply (small batches)
+    GemmArgs ge = g;
+    ge.epi = 4;
+    ge.split_lo = pm >> 3 & 1;
+    ge.c16 = w.h3;
+    ge.ldc = 9216;
+    if (gemm_epi_ok(ge)) {
+      CHK(gemm(h, ge, s));
+    } else {
+      g.c32 = w.p32;
+      g.ldc = 3072;
+      CHK(gemm(h, g, s));
+      HIPCHK(launch_split3(w.p32, 3072, w.h3, M, 3072, s, pm >> 3 & 1));
+    }
     g = with_ws(lin(w.h3, 9216, Ly.fc2, Ly.fc23, 3), w.sk_text, w.sk_elems);
     g.c32 = y;
     CHK(gemm(h, g, s));
@@ -2324,6 +2336,30 @@ int mmf_gemm_f16_ex(const void* A, int lda, const void* W, int ldw, const float*
   apply_options(process_options(), &g);
   if (!A || !W || !c16) return fail(MMF_EINVAL, "null argument");
   if (ascale && rows_per_batch <= 0) return fail(MMF_EINVAL, "rows_per_batch must be > 0 with ascale");
+  hipError_t e = launch_gemm(g, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(MMF_EIO, "gemm: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int mmf_gemm_f16_split(const void* A, int lda, const void* W, int ldw, const float* bias, void* c16, int ldc, int M,
+                       int N, int K, int act, int split_lo, void* stream) {
+  GemmArgs g{};
+  g.A = (const f16_t*)A;
+  g.lda = lda;
+  g.W = (const f16_t*)W;
+  g.ldw = ldw;
+  g.bias = bias;
+  g.c16 = (f16_t*)c16;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.act = act;
+  g.epi = 4;
+  g.split_lo = split_lo ? 1 : 0;
+  apply_options(process_options(), &g);
+  if (!A || !W || !c16 || !bias) return fail(MMF_EINVAL, "null argument");
+  if (!gemm_epi_ok(g)) return fail(MMF_EINVAL, "split-operand epilogue not applicable (M=%d N=%d K=%d ldc=%d act=%d)", M, N, K, ldc, act);
   hipError_t e = launch_gemm(g, (hipStream_t)stream);
   if (e != hipSuccess) return fail(MMF_EIO, "gemm: %s", hipGetErrorString(e));
   return 0;

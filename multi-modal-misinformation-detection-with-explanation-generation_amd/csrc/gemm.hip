@@ -581,6 +581,9 @@ hipError_t run_glds_epi(const GemmArgs& a, hipStream_t s) {
       case ACT_QUICK_GELU: MMF_EPI_CASE(1, ACT_QUICK_GELU); break;
       default: return hipErrorInvalidValue;
     }
+  } else if (a.epi == 4) {
+    if (a.act != ACT_GELU) return hipErrorInvalidValue;
+    MMF_EPI_CASE(4, ACT_GELU);
   } else if (a.act != ACT_NONE || BN != 192) {
     return hipErrorInvalidValue;
   } else if (a.epi == 2) {
@@ -736,7 +739,7 @@ int gemm_config(const GemmArgs& a) {
   // only, so a row's statistics (and so its result) do not depend on the batch it runs in
   if (a.epi == 2 || a.epi == 3) return 10;
   const int f = forced_config(a);
-  if (a.epi == 1) return (f == 10 || f == 11) ? f : glds_pick(a, false);
+  if (a.epi == 1 || a.epi == 4) return (f == 10 || f == 11) ? f : glds_pick(a, false);
   if (f >= 0) return f;
   if (pw_applicable(a)) return 9;  // HBM-bound 1x1 convolutions (pointwise.hip)
   if (a.N <= 32) return 0;
@@ -769,8 +772,13 @@ static bool epi_ok(const GemmArgs& a) {
   if (a.epi == 3)  // whole 128-row sequences, whole heads (192 = q | k | v columns of one head)
     return a.c16 && !a.c32 && !a.res16 && !a.res32 && a.bias && a.act == ACT_NONE && a.N % 192 == 0 &&
            a.M % 128 == 0 && a.ldc >= a.N / 3;
+  if (a.epi == 4)
+    return a.c16 && !a.c32 && !a.res16 && !a.res32 && a.bias && a.act == ACT_GELU && a.N % 8 == 0 &&
+           a.ldc >= (a.split_lo ? 3 * a.N : a.N) && (size_t)(a.M + 256) * a.ldc * 2 < ((size_t)1 << 31);
   return false;
 }
+
+bool gemm_epi_ok(const GemmArgs& a) { return epi_ok(a); }
 
 const char* gemm_config_name(int c) {
   static const char* names[kGemmConfigs] = {

@@ -40,7 +40,14 @@ struct GemmArgs {
   // for two whole sequences; the epilogue runs their attention and writes ctx [M][ldc] (c16, head h
   // at columns 64 h) instead of qkv.  amask: key-padding mask int32 [M / 128][128] (1 keep) or null
   const int32_t* amask;
+  // epi 4 (RoBERTa precise mode, FFN-1): out = act(acc + bias) written as the next GEMM's split
+  // operand row: c16[m * ldc + n] = hi, and with split_lo also [+ N] = lo = fp16(out - hi), [+ 2N] = hi
+  // (ldc >= 3N), so the fp32 hidden and its split3 pass are never formed
+  int split_lo;
 };
+// whether launch_gemm accepts a (epi != 0) epilogue for these arguments (the host falls back to
+// the plain path otherwise)
+bool gemm_epi_ok(const GemmArgs& a);
 // epi 2: the column-block width (= P partials per row of ceil(N / tn)) launch_gemm will use
 int gemm_ln_tn(const GemmArgs& a);
 // split-K factor the skinny-M (M <= 512) GEMM path uses for this (K) -- independent of M, so

@@ -55,6 +55,7 @@ SIGNATURES = {
     "mmf_device_bytes": (ctypes.c_int64, [_P]),
     "mmf_gemm_f16": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "mmf_gemm_f16_ex": (_I, [_P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P]),
+    "mmf_gemm_f16_split": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "mmf_attention_f16": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }
 

@@ -20,7 +20,7 @@ from .hip import check
 PROFILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0
-NK = 512  # >= the library's PK_COUNT (kGemmConfigs x 3 epilogues x 5 activations + 12 other kinds)
+NK = 512  # >= the library's PK_COUNT (kGemmConfigs x 5 epilogues x 5 activations + 12 other kinds)
 
 
 def profile_kernels(eng, step: Callable[[], None], steps: int) -> List[Dict]:

@@ -205,3 +205,39 @@ def test_gemm_effnet_convs(lib, M, N, K, act, scale, res):
     got = out.cpu().float()
     scale_ = ref.abs().max().item()
     assert ((got - ref).abs() <= ref.abs() * 2 ** -7 + 2e-5 * scale_).all()
+
+
+@pytest.mark.parametrize("cfg", [10, 11])
+@pytest.mark.parametrize("split_lo", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(1000, 3072, 768), (777, 392, 512), (4096, 768, 2304)])
+def test_gemm_split_operand_epilogue_bit_identical(lib, gemm_config, cfg, split_lo, M, N, K):
+    """The precise mode's FFN-1 epilogue (epi 4: GELU output written as hi | lo | hi fp16 thirds) is
+    bit-identical to the fp32 output of the same tile split on the host: hi = fp16(c32),
+    lo = fp16(c32 - hi); nothing is written past N (split_lo 0) / 3N (split_lo 1)."""
+    import mmf_amd.hip as hip
+    gemm_config(cfg)
+    g = torch.Generator().manual_seed(M + 5 * N + K)
+    A = _f16(torch.randn(M, K, generator=g))
+    W = _f16(torch.randn(N, K, generator=g) * 0.05)
+    bias = torch.randn(N, generator=g)
+    dev = torch.device("cuda")
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    c32 = torch.empty(M, N, device=dev)
+    hip.check(lib.mmf_gemm_f16(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), None, c32.data_ptr(), None, N,
+                                M, N, K, 1, hip.stream_ptr()))
+    ld = 3 * N + 8
+    s3 = torch.full((M, ld), 7.0, device=dev, dtype=torch.float16)
+    hip.check(lib.mmf_gemm_f16_split(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), s3.data_ptr(), ld, M, N, K,
+                                      1, split_lo, hip.stream_ptr()))
+    torch.cuda.synchronize()
+    c = c32.cpu()
+    hi = c.half()
+    lo = (c - hi.float()).half()
+    out = s3.cpu()
+    assert torch.equal(out[:, :N].view(torch.int16), hi.view(torch.int16))
+    if split_lo:
+        assert torch.equal(out[:, N:2 * N].view(torch.int16), lo.view(torch.int16))
+        assert torch.equal(out[:, 2 * N:3 * N].view(torch.int16), hi.view(torch.int16))
+        assert (out[:, 3 * N:] == 7.0).all(), "wrote past 3N"
+    else:
+        assert (out[:, N:] == 7.0).all(), "wrote past N"
