@@ -563,7 +563,7 @@ class HostPipeline:
         # input/output slots = batches in flight (MMF_PIPE_SLOTS, default 3): the copy of batch i+1 beside
         # the compute of batch i, and the host one more batch ahead.  With 2, a host hiccup longer than
         # one batch's compute left the device idle: bench headline 18,365 -> 18,562 pairs/s (3
-        # interleaved processes), now level with the HBM-resident rate (profiles/r04_ab_pipe_slots.txt)
+        # interleaved processes), now level with the HBM-resident rate (profiles/r04_ab_pipe_slots.txt, git history at 168304c)
         self.n = max(2, int(os.environ.get("MMF_PIPE_SLOTS", "3")))
         self.slots = [{k: torch.empty(sh, dtype=dt, device=d) for k, (sh, dt) in shapes.items()} for _ in range(self.n)]
         self.outs = [eng.alloc_outputs(B) for _ in range(self.n)]

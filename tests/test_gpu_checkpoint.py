@@ -221,3 +221,23 @@ def test_effnet_calibration_follows_reloads(det_sd, clip_sd):
     assert mf.engine.effnet_check["tower"] == "fp16" and mf.engine.get_option("effnet_fp32") == 0
     _check(mf, _oracle(det_sd, clip_sd, inp), inp, "ordinary reload")
     mf.engine.close()
+
+
+def test_pinned_text_layout_survives_reload(det_sd, clip_sd, trained):
+    """a text layout pinned through set_option stays pinned across a detector
+    re-pack under text_precision "auto" -- the calibration leaves it alone instead of switching to
+    the precise mode whose weights a pinned load may not have packed -- and sync() / analyze work on
+    the reloaded weights at the bar."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    inp = _inputs()
+    mf = _mf(det_sd, clip_sd, "/nonexistent")
+    mf.engine.set_option("text_hilo", 1)
+    det = mf.detector
+    det.load_state_dict({k: torch.as_tensor(v) for k, v in trained.items()})
+    det.sync()
+    assert mf.engine.get_option("text_hilo") == 1
+    assert mf.engine.get_option("text_hilo_effective") == 1
+    assert mf.engine.text_check["mode"] == "pinned", mf.engine.text_check
+    _check(mf, _oracle(trained, clip_sd, inp), inp, "pinned split stream, reloaded weights")
+    mf.engine.close()

@@ -9,7 +9,7 @@
   trained here on a synthetic corpus because the roberta-base / CLIP vocab files are absent (so
   the rate is representative of the algorithm, not parity-pinned), encoding N news-length texts
   (~90 words) with truncation at 128 tokens, serial and batched (texts/s).
-Prints one JSON object; the GPU box numbers are committed as profiles/r02_host_pipeline.json.
+Prints one JSON object; the GPU box numbers are committed as profiles/r02_host_pipeline.json (git history at 168304c).
 """
 import argparse
 import io
