@@ -517,6 +517,9 @@ MMF_DEV unsigned long long gst_time() {
 #ifndef MMF_DMA_ILV
 #define MMF_DMA_ILV 1  // LDS-DMA pieces interleaved with the MFMAs of the PIPE2 K loop (gemm_glds_body.inc; 0: A/B builds)
 #endif
+#ifndef MMF_ILV_G192
+#define MMF_ILV_G192 0  // 256x192 plain / producer tiles: 0 = up-front issue, g = interleaved over g groups (A/B builds)
+#endif
 
 #ifndef MMF_GLDS_BUF
 #define MMF_GLDS_BUF 1  // descriptor LDS-DMA fills for full panels (0: 64-bit-address fills everywhere; A/B builds)
