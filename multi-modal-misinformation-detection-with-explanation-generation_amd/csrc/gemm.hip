@@ -478,7 +478,8 @@ MMF_DEV unsigned long long gst_time() {
   bool gst_first_ = true;                                                                                    \
   {                                                                                                          \
     const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                                          \
-    if (gst_ && threadIdx.x == 0) gst_[0] = r_;                                                              \
+    const unsigned long long m_ = gst_time();                                                                \
+    if (gst_ && threadIdx.x == 0) { gst_[0] = r_; gst_[kGStampSlots - 2] = m_; }                             \
   }
 #if MMF_GEMM_STAMP == 2
 // phase mode (-DMMF_GEMM_STAMP=2, tools/gemm_stamps.py --phases): wave 0 of each
@@ -495,7 +496,7 @@ MMF_DEV unsigned long long gst_time() {
 #define GST()                                                                                                \
   {                                                                                                          \
     const unsigned long long t_ = gst_time();                                                                \
-    if (gst_ && threadIdx.x == 0 && gst_n_ < kGStampSlots) gst_[gst_n_] = t_;                                \
+    if (gst_ && threadIdx.x == 0 && gst_n_ < kGStampSlots - 2) gst_[gst_n_] = t_;                                \
     ++gst_n_;                                                                                                \
   }
 #endif
@@ -504,7 +505,8 @@ MMF_DEV unsigned long long gst_time() {
   {                                                                                                          \
     GST()                                                                                                    \
     const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                                          \
-    if (gst_ && threadIdx.x == 0) { gst_[1] = r_; gst_[2] = (unsigned long long)gst_n_; }                    \
+    const unsigned long long m_ = gst_time();                                                                \
+    if (gst_ && threadIdx.x == 0) { gst_[1] = r_; gst_[2] = (unsigned long long)gst_n_; gst_[kGStampSlots - 1] = m_; } \
   }
 #else
 #define GST_INIT()

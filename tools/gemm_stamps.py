@@ -123,6 +123,9 @@ def phases(name, M, N, K, st, used, nk):
             nxt = t[i + 1, 0] if i + 1 < steps else np.nan
             rows.append((t[i, 1] - t[i, 0], t[i, 2] - t[i, 1], t[i, 3] - t[i, 2], nxt - t[i, 3], t[i, 3] - t[i, 0]))
     a = np.array(rows)
+    # shader clock over each workgroup's life: s_memtime (slots 94 / 95) against s_memrealtime
+    # (slots 0 / 1, 100 MHz)
+    clk = [(r[95] - r[94]) / max(r[1] - r[0], 1) * 0.1 for r in st[used] if r[95] > r[94] > 0 and r[1] > r[0]]
     med = np.nanmedian(a, axis=0)
     p90 = np.nanpercentile(a, 90, axis=0)
     names = ("dma", "reads+mfma", "barrier", "loop", "step")
@@ -131,6 +134,8 @@ def phases(name, M, N, K, st, used, nk):
     print("    median cycles: " + "  ".join(f"{n} {v:.0f}" for n, v in zip(names, med)))
     print("    p90 cycles:    " + "  ".join(f"{n} {v:.0f}" for n, v in zip(names, p90)))
     print("    share of the median step: " + "  ".join(f"{n} {100 * v / med[4]:.0f}%" for n, v in zip(names[:3], med[:3])))
+    if clk:
+        print(f"    shader clock over the workgroup's life: median {np.median(clk):.2f} GHz")
 
 
 if __name__ == "__main__":
