@@ -284,8 +284,8 @@ int mmf_gemm_f16_ex(const void* A, int lda, const void* W, int ldw, const float*
 /* The RoBERTa precise mode's FFN-1 epilogue (gemm.hip epi 4), exported for its bit-identity test:
  * out = act(A @ W^T + bias) written as the next GEMM's split operand row -- c16[m*ldc + n] = fp16(out)
  * and, with split_lo, c16[m*ldc + N + n] = fp16(out - fp16(out)), c16[m*ldc + 2N + n] = fp16(out)
- * (ldc >= 3N).  act 1 (gelu-erf) only; persistent-tile shapes only (K % 64 == 0, N % 8 == 0), else
- * MMF_EINVAL. */
+ * (ldc >= 3N).  bias fp32 [N] (required), act 1 (gelu-erf) only; persistent-tile shapes only
+ * (K % 64 == 0, N % 8 == 0), else MMF_EINVAL. */
 int mmf_gemm_f16_split(const void* A, int lda, const void* W, int ldw, const float* bias, void* c16, int ldc, int M,
                        int N, int K, int act, int split_lo, void* stream);
 
