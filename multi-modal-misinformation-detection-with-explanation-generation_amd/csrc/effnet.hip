@@ -410,6 +410,10 @@ __global__ __launch_bounds__(256, 3) void dwconv_kernel(const f16_t* __restrict_
 #ifndef MMF_EDW_PF
 #define MMF_EDW_PF 1
 #endif
+// MMF_EDW_PADSKIP = 1: fragment rows wholly in the zero padding skip their expand MFMAs and SiLU
+#ifndef MMF_EDW_PADSKIP
+#define MMF_EDW_PADSKIP 1
+#endif
 template <int K, int S, int KS, int TT, int R, int TPAD>
 #ifndef MMF_EDW_MINB1
 #define MMF_EDW_MINB1 4  // resident blocks per CU hipcc budgets registers for (KS = 1: stage 3.1 148 -> 128 VGPRs, 4 blocks/CU; -0.9 %)
@@ -520,6 +524,18 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
       for (int it = 0; it < MAXRF; ++it) {
         const int rf = wave + 4 * it;
         if ((TT > 0 && 4 * it + 3 < NRF_CT) || rf < nrf) {
+          const int pix = rf * 16 + fr;
+          const int ty = pix / IT, tx = pix - ty * IT;
+          const int iy = iy0 + ty, ix = ix0 + tx;
+          const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
+          if (MMF_EDW_PADSKIP && __builtin_amdgcn_ballot_w64(inimg) == 0) {
+            // all 16 pixels of the fragment row lie in the zero padding (tile rows above / below the
+            // image): their expanded values are the depthwise conv's zero padding, no MFMA or SiLU
+#pragma unroll
+            for (int nf = 0; nf < NF; ++nf)
+              if (pix < npix) *reinterpret_cast<uint2*>(tile + (size_t)pix * PS + nf * 16 + fg * 4) = make_uint2(0u, 0u);
+            continue;
+          }
           f32x4 acc[NF];
 #pragma unroll
           for (int nf = 0; nf < NF; ++nf) {
@@ -527,10 +543,6 @@ __global__ __launch_bounds__(256, KS == 1 ? MMF_EDW_MINB1 : KS == 2 ? 3 : 2) voi
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) acc[nf] = mfma16x16x32(wf[nf][ks], as_f16x8(xr[it][ks]), acc[nf]);
           }
-          const int pix = rf * 16 + fr;
-          const int ty = pix / IT, tx = pix - ty * IT;
-          const int iy = iy0 + ty, ix = ix0 + tx;
-          const bool inimg = pix < npix && iy >= 0 && iy < H && ix >= 0 && ix < W;
 #pragma unroll
           for (int nf = 0; nf < NF; ++nf) {
             float e[4] = {acc[nf][0] + bev[nf].x, acc[nf][1] + bev[nf].y, acc[nf][2] + bev[nf].z, acc[nf][3] + bev[nf].w};
